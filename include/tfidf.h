@@ -1,0 +1,172 @@
+/*
+ * tfidf.h — C-ABI of the MI355X-native TF-IDF engine (libtfidf_hip.so).
+ *
+ * The reference (ndas7/Parallel-Systems-MPI-TFIDF, TFIDF.c) has no library API: the
+ * whole path is one monolithic main() (TFIDF.c:52-287) whose seams are
+ *   ingest      input/docN bytes            TFIDF.c:98-110, 130-147
+ *   count       wordCount / docSize / df    TFIDF.c:141-196, 291-326
+ *   score       tf * log(N/df)              TFIDF.c:202, 243-244
+ *   emit        "docN@word\t%.16f", qsort   TFIDF.c:245, 273-282
+ * Every entry point below names the reference lines it replaces.  Plain C types only:
+ * pointers + sizes, no torch or HIP types.  Every function returns 0 or a negative
+ * TFIDF_E* code (never exit()s, unlike TFIDF.c:102,122,137,277).  A context is used
+ * by one host thread at a time.
+ */
+#ifndef TFIDF_H
+#define TFIDF_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TFIDF_ABI_VERSION 1
+
+enum tfidf_status {
+    TFIDF_OK = 0,
+    TFIDF_E_INVAL = -1,     /* bad argument */
+    TFIDF_E_NOMEM = -2,     /* host or device allocation failed */
+    TFIDF_E_HIP = -3,       /* HIP runtime error */
+    TFIDF_E_RCCL = -4,      /* RCCL error */
+    TFIDF_E_NODEV = -5,     /* no usable gfx950 device */
+    TFIDF_E_NOINPUT = -6,   /* ./input cannot be opened        (TFIDF.c:100-103) */
+    TFIDF_E_NODOC = -7,     /* input/docN cannot be opened     (TFIDF.c:134-138) */
+    TFIDF_E_OUTPUT = -8,    /* output.txt cannot be written    (TFIDF.c:274-278) */
+    TFIDF_E_CAPACITY = -9,  /* an internal table could not be grown */
+    TFIDF_E_STATE = -10     /* call out of order (e.g. fetch before run) */
+};
+
+/* ---------------------------------------------------------------- corpus ---- */
+
+#define TFIDF_CORPUS_DEVICE 1u   /* bytes/doc_off/doc_ids are device pointers on the ctx's GPU */
+
+/* One shard of documents.  Replaces the reference's per-rank fopen/fscanf ingest
+ * (TFIDF.c:130-147): document i (0-based, local) is bytes[doc_off[i], doc_off[i+1]).
+ * Document boundaries are token boundaries.  Tokens follow fscanf("%s") in the C
+ * locale: maximal runs of bytes not in {0x20,0x09..0x0D}; a term is the token's bytes
+ * up to its first NUL (strcmp semantics, TFIDF.c:152,172). */
+typedef struct tfidf_corpus {
+    const uint8_t*  bytes;
+    uint64_t        nbytes;
+    const uint64_t* doc_off;      /* ndocs + 1 entries, non-decreasing, doc_off[ndocs] <= nbytes */
+    const uint32_t* doc_ids;      /* global 1-based ids ("docN"); NULL means 1..ndocs */
+    uint32_t        ndocs;        /* documents in this shard */
+    uint32_t        flags;        /* TFIDF_CORPUS_* */
+    uint64_t        ndocs_total;  /* N of log(N/df) (TFIDF.c:98-115,243); 0 means ndocs */
+} tfidf_corpus;
+
+/* ---------------------------------------------------------------- result ---- */
+
+/* Host-side result, pairs in output order: the strcmp order of the reference's
+ * "docN@word\t%.16f" lines (TFIDF.c:245,273).  Arrays are owned by the library and
+ * released by tfidf_result_free(). */
+typedef struct tfidf_result {
+    uint64_t  npairs;       /* unique (doc, term) pairs in this shard = output lines */
+    uint32_t  ndocs;        /* documents in this shard */
+    uint32_t  nterms;       /* distinct terms in this shard */
+    uint64_t  ndocs_total;  /* N used for idf */
+    /* per pair (output order) */
+    uint32_t* pair_doc;     /* global doc id (TFIDF.c:132 "doc%d") */
+    uint32_t* pair_term;    /* index into the term table below */
+    uint32_t* pair_count;   /* wordCount     (TFIDF.c:154,163) */
+    uint32_t* pair_docsize; /* docSize       (TFIDF.c:141-143) */
+    uint32_t* pair_df;      /* numDocsWithWord over ALL shards (TFIDF.c:169-188,215-234) */
+    double*   pair_score;   /* tf * log(N/df) (TFIDF.c:202,243-244) */
+    /* per local document, input order */
+    uint32_t* doc_id;
+    uint32_t* doc_size;
+    /* term table: this shard's terms in strcmp("word\t") order */
+    uint64_t* term_off;     /* nterms + 1 */
+    uint8_t*  term_bytes;
+    uint32_t* term_df;      /* global df of each term */
+} tfidf_result;
+
+/* ---------------------------------------------------------------- context --- */
+
+typedef struct tfidf_ctx tfidf_ctx;
+
+/* Opens device `device` (HIP ordinal).  Fails with TFIDF_E_NODEV unless it is gfx950. */
+int tfidf_open(int device, tfidf_ctx** out);
+void tfidf_close(tfidf_ctx* ctx);
+const char* tfidf_strerror(int status);
+int tfidf_abi_version(void);
+
+/* ---- multi-GPU: one process per GPU; replaces MPI_Init/Comm_size/Comm_rank
+ *      (TFIDF.c:82,91-92) and the DF combine MPI_Reduce(CustomReduce)+MPI_Bcast
+ *      (TFIDF.c:209-222,291-326) with RCCL collectives over xGMI. */
+#define TFIDF_UNIQUE_ID_BYTES 128
+int tfidf_comm_unique_id(uint8_t id[TFIDF_UNIQUE_ID_BYTES]);
+int tfidf_comm_init(tfidf_ctx* ctx, const uint8_t id[TFIDF_UNIQUE_ID_BYTES], int rank, int nranks);
+
+/* Runs the whole hot path on this shard: tokenize -> per-document TF counts ->
+ * vocabulary -> DF (all-reduced across ranks when a communicator is attached) ->
+ * tf*log(N/df) -> output order.  Replaces TFIDF.c:130-273.  Results stay in HBM
+ * until tfidf_fetch().  Host-pointer corpora are copied to HBM first. */
+int tfidf_run(tfidf_ctx* ctx, const tfidf_corpus* corpus);
+
+/* Copies the last run's results to host memory. */
+int tfidf_fetch(tfidf_ctx* ctx, tfidf_result* out);
+void tfidf_result_free(tfidf_result* r);
+
+/* Counters of the last run (sizes, for roofline accounting). */
+typedef struct tfidf_run_info {
+    uint64_t nbytes;          /* C */
+    uint64_t ntokens;         /* T */
+    uint64_t npairs;          /* P */
+    uint32_t nterms;          /* V (this shard) */
+    uint32_t nterms_global;   /* V over all ranks */
+    uint64_t nchunks;         /* tokenize+count work units */
+    uint64_t partial_records; /* (doc, term) records of documents split across work units */
+    uint32_t ndocs;
+    uint32_t vocab_capacity;
+    double   ms_total;        /* device time of the whole run (HIP events) */
+    double   ms_tokcount;     /* device time of the tokenize+count kernels (HIP events) */
+    double   ms_stage[16];    /* per-stage device times, see tfidf_stage_name() */
+    uint32_t nstages;
+    uint32_t pad_;
+} tfidf_run_info;
+int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info);
+const char* tfidf_stage_name(int stage);
+/* Enables per-stage HIP event timing (adds a few event records per run). */
+int tfidf_set_timing(tfidf_ctx* ctx, int enable);
+
+/* ---------------------------------------------------------------- emission -- */
+
+/* Writes result lines "docN@word\t%.16f\n" (TFIDF.c:245,280-281) to `path`. */
+int tfidf_write_output(const tfidf_result* r, const char* path);
+/* Prints the debug TF Job / IDF Job blocks (TFIDF.c:199-205,236-239) to stdout,
+ * one block pair for this shard, pairs in output order. */
+int tfidf_print_jobs(const tfidf_result* r);
+
+/* ---------------------------------------------------------------- ingest ---- */
+
+/* Reference input contract (TFIDF.c:98-110,130-147): N = number of entries of `dir`
+ * other than "." and ".."; documents are dir/doc1 .. dir/docN.  Reads them into one
+ * malloc'd buffer with doc_off[N+1].  Returns TFIDF_E_NOINPUT / TFIDF_E_NODOC
+ * (with *bad_doc set) like the reference's error exits. */
+int tfidf_ingest_dir(const char* dir, uint8_t** bytes, uint64_t* nbytes,
+                     uint64_t** doc_off, uint32_t* ndocs, uint32_t* bad_doc);
+void tfidf_free(void* p);
+
+/* ---------------------------------------------------------------- synthetic - */
+
+/* Synthetic Zipfian corpus (generator in csrc/synth.h).  ntok[i] tokens
+ * in local document i whose global id is doc_ids[i]; cdf = Zipf CDF over V ranks
+ * (zipf mode) or NULL (mode 1: config-1 "4 words per doc").  Host version fills
+ * caller-provided buffers (query the size first with bytes == NULL). */
+int tfidf_synth_host(uint64_t seed, uint32_t V, uint32_t mode, const double* cdf,
+                     const uint32_t* doc_ids, const uint64_t* ntok, uint32_t ndocs,
+                     uint8_t* bytes, uint64_t* nbytes, uint64_t* doc_off);
+/* Device version: generates straight into HBM buffers owned by the ctx and returns a
+ * device corpus (flags = TFIDF_CORPUS_DEVICE) valid until the next synth call or
+ * tfidf_close. */
+int tfidf_synth_device(tfidf_ctx* ctx, uint64_t seed, uint32_t V, uint32_t mode,
+                       const double* cdf, const uint32_t* doc_ids, const uint64_t* ntok,
+                       uint32_t ndocs, uint64_t ndocs_total, tfidf_corpus* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TFIDF_H */

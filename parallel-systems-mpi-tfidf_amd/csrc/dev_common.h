@@ -1,0 +1,132 @@
+/*
+ * dev_common.h — device helpers shared by the gfx950 kernels.
+ *
+ * Term identity (TFIDF.c:152,161,172,184 compare and copy words with strcmp/strcpy,
+ * so a term is the token's bytes up to its first NUL).  Terms are 128-bit keys:
+ *
+ *   short term (<= 15 bytes): little-endian bytes w[0..n), byte n = 0x09 (TAB), rest 0.
+ *       Exact and injective.  Byte-swapped, the same 16 bytes are the big-endian sort
+ *       key "w \t 0...", whose unsigned order is the strcmp order of the reference's
+ *       "docN@w\t..." lines for a fixed document.
+ *   long term (>= 16 bytes): bytes 0..14 = 120-bit hash of the term, byte 15 = 0xFF.
+ *       Its ordering key is the word's first 16 bytes; equal prefixes are resolved by a
+ *       full byte compare (vocab_long_fixup).
+ * Byte 15 of a short key is 0x00 or 0x09 and of a long key 0xFF, so the sentinels
+ * below (byte 15 = 0xEE / 0xDD / 0xFE) never collide with a real key.
+ */
+#ifndef TFIDF_DEV_COMMON_H
+#define TFIDF_DEV_COMMON_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define KEY_EMPTY_HI   0xEEEEEEEEEEEEEEEEull   /* empty hash-table slot */
+#define KEY_PENDING_HI 0xDDDDDDDDDDDDDDDDull   /* claimed, key being published */
+#define KEY_GSLOT_TAG  0xFE00000000000000ull   /* LDS key already resolved to a global slot */
+#define KEY_LONG_TAG   0xFF00000000000000ull
+#define DOC_NONE       0xFFFFFFFFu
+
+/* C-locale isspace(): the byte set fscanf("%s") stops at (TFIDF.c:142,147) */
+__device__ __forceinline__ bool is_ws(uint32_t c) { return c == 0x20u || (c - 0x09u) <= 4u; }
+
+/* 16-bit mask of whitespace bytes in a 16-byte group (bit i = byte i) */
+__device__ __forceinline__ uint32_t ws_mask16(uint4 v) {
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            uint32_t c = (w[k] >> (8 * b)) & 0xFFu;
+            m |= (is_ws(c) ? 1u : 0u) << (4 * k + b);
+        }
+    }
+    return m;
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 27; z *= 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t key_hash(uint64_t lo, uint64_t hi) {
+    return mix64(lo * 0x9E3779B97F4A7C15ull ^ (hi + 0x632BE59BD9B4E019ull) * 0xC2B2AE3D27D4EB4Full);
+}
+
+/* first zero byte index in a u64 (8 if none) */
+__device__ __forceinline__ uint32_t first_zero_byte(uint64_t x) {
+    uint64_t t = (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;
+    return t ? (uint32_t)(__builtin_ctzll(t) >> 3) : 8u;
+}
+
+/* Builds the short key from 16 raw bytes (lo = bytes 0..7, hi = 8..15) of a token of
+ * length len (bytes beyond len are ignored).  Returns the term length after NUL
+ * truncation; the key is valid only when that length is <= 15. */
+__device__ __forceinline__ uint32_t make_short_key(uint64_t lo, uint64_t hi, uint32_t len,
+                                                   uint64_t* klo, uint64_t* khi) {
+    uint32_t n = len < 16u ? len : 16u;
+    /* NUL truncation (strcmp semantics) */
+    uint32_t z0 = first_zero_byte(lo);
+    uint32_t z = z0 < 8u ? z0 : 8u + first_zero_byte(hi);
+    if (z < n) n = z;
+    if (n >= 16u) return 16u;
+    /* keep bytes < n, put TAB at n, zero the rest */
+    uint64_t mlo = n >= 8u ? ~0ull : ((1ull << (8u * n)) - 1ull);
+    uint64_t mhi = n <= 8u ? 0ull : ((1ull << (8u * (n - 8u))) - 1ull);
+    lo &= mlo;
+    hi &= mhi;
+    if (n < 8u) lo |= 0x09ull << (8u * n);
+    else hi |= 0x09ull << (8u * (n - 8u));
+    *klo = lo;
+    *khi = hi;
+    return n;
+}
+
+/* Long-term key: 120-bit hash over the term bytes, byte 15 = 0xFF. */
+__device__ __forceinline__ void make_long_key(const uint8_t* p, uint64_t n, uint64_t* klo, uint64_t* khi) {
+    uint64_t h1 = 0x243F6A8885A308D3ull ^ n, h2 = 0x13198A2E03707344ull + n * 0x9E3779B97F4A7C15ull;
+    for (uint64_t i = 0; i < n; ++i) {
+        uint64_t c = p[i];
+        h1 = (h1 ^ c) * 0x100000001B3ull;
+        h2 = (h2 + c + 1) * 0xC2B2AE3D27D4EB4Full;
+        h2 ^= h2 >> 29;
+    }
+    *klo = mix64(h1 ^ (h2 << 1));
+    *khi = (mix64(h2 + 0x7F4A7C15ull * h1) & 0x00FFFFFFFFFFFFFFull) | KEY_LONG_TAG;
+}
+
+__device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
+
+/* ---- wave / block scans (wave64) ---- */
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+/* exclusive scan over the block (blockDim = NT, multiple of 64); wsum: NT/64 words LDS.
+ * Returns exclusive prefix; *total = block sum.  Contains two __syncthreads(). */
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = wave_incl_scan(v);
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < NT / 64; ++k) {
+        uint32_t s = wsum[k];
+        base += (k < w) ? s : 0u;
+        tot += s;
+    }
+    *total = tot;
+    __syncthreads();
+    return base + inc - v;
+}
+
+#endif

@@ -1,0 +1,763 @@
+/*
+ * engine.cpp — C-ABI implementation (include/tfidf.h): context, HBM buffers, stage
+ * orchestration on one HIP stream, RCCL exchange, result fetch.
+ *
+ * Pipeline of tfidf_run (reference lines replaced in brackets):
+ *   K0 plan chunks                                       [TFIDF.c:125-130 doc->rank split]
+ *   K1 tokenize + LDS-hash count + global vocabulary     [TFIDF.c:130-196]
+ *   vocabulary ranking (radix sort of strcmp keys)        [TFIDF.c:227-234 linear joins]
+ *   partial-document merge (radix sort + reduce-by-key)
+ *   DF histogram                                          [TFIDF.c:169-188,291-326]
+ *   RCCL: identity-key all-gather + DF all-reduce         [TFIDF.c:209-222 MPI_Reduce/Bcast]
+ *   idf LUT over the distinct df values, host libm log    [TFIDF.c:243]
+ *   document order + per-document term sort + score       [TFIDF.c:202,244-245,253-273]
+ * No stage has a CPU fallback: a missing device or HIP error is returned as an error.
+ */
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/tfidf.h"
+#include "kernels.h"
+#include "synth.h"
+
+extern "C" void tfidf_synth_spec(syn_spec* s, uint64_t seed, uint32_t V, uint32_t mode, const double* cdf);
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap && p) return 0;
+        if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+        size_t want = bytes < 256 ? 256 : bytes;
+        if (hipMalloc(&p, want) != hipSuccess) { p = nullptr; return -1; }
+        cap = want;
+        return 0;
+    }
+    /* grow preserving the first `keep` bytes */
+    int grow_keep(size_t bytes, size_t keep, hipStream_t s) {
+        if (bytes <= cap && p) return 0;
+        void* q = nullptr;
+        if (hipMalloc(&q, bytes) != hipSuccess) return -1;
+        if (p && keep) {
+            if (hipMemcpyAsync(q, p, keep, hipMemcpyDeviceToDevice, s) != hipSuccess) return -1;
+            if (hipStreamSynchronize(s) != hipSuccess) return -1;
+        }
+        if (p) (void)hipFree(p);
+        p = q;
+        cap = bytes;
+        return 0;
+    }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+    template <typename T> T* as() const { return (T*)p; }
+};
+
+enum Stage { S_PREP, S_TOKCOUNT, S_VOCAB, S_MERGE, S_DF, S_EXCHANGE, S_IDF, S_ORDER, S_SCORE, S_NSTAGES };
+const char* kStageNames[S_NSTAGES] = {"prep", "tokcount", "vocab", "merge", "df", "exchange", "idf", "order", "score"};
+
+}  // namespace
+
+struct tfidf_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    ncclComm_t comm = nullptr;
+    int rank = 0, nranks = 1;
+    bool timing = true;
+    hipEvent_t ev[S_NSTAGES + 1];
+    Arena arena;
+    DevBuf arena_buf;
+    /* host-input staging */
+    DevBuf in_bytes, in_off, in_ids;
+    /* synthetic corpus */
+    DevBuf syn_bytes, syn_off, syn_ids, syn_ntok, syn_blkfirst, syn_blkbytes, syn_cdf;
+    /* stage buffers */
+    DevBuf chunk_start, chunk_doc;
+    DevBuf vkeys, vrep;
+    uint64_t vcap = 1ull << 16;
+    DevBuf rec_slot, rec_cnt;
+    uint64_t rec_cap = 0;
+    DevBuf part_doc, part_slot, part_cnt;
+    uint64_t part_cap = 0;
+    DevBuf doc_recoff, doc_npairs, doc_size, doc_flags;
+    DevBuf counters;
+    DevBuf dense, vslot, skey0, skey1, seq0, seq1, rank_of_slot, slot_of_rank;
+    DevBuf pkey0, pkey1, pseq0, pseq1, phead;
+    DevBuf df_local, df_global, present, idf_vals;
+    DevBuf dkey0, dkey1, dseq0, dseq1, npairs_ord, out_off;
+    DevBuf out_doc, out_term, out_cnt, out_docsize, out_df, out_score;
+    DevBuf x_mine, x_send, x_recv, x_recv2, x_seq0, x_seq1, x_head, x_grank, x_dfv, x_cnt;
+    uint32_t* sorted_dense = nullptr; /* points into seq0/seq1 */
+    uint4* sorted_skey = nullptr;
+    const uint32_t* order = nullptr;
+    /* last run */
+    bool have_result = false;
+    tfidf_corpus corpus{};
+    const uint8_t* dev_bytes = nullptr;
+    const uint32_t* dev_ids = nullptr;
+    uint64_t npairs = 0, ntokens = 0, nchunks = 0, nrec_part = 0, ndocs_total = 0;
+    uint32_t ndocs = 0, V = 0, Vg = 0;
+    double ms_stage[S_NSTAGES] = {0};
+    double ms_total = 0;
+    hipError_t last_err = hipSuccess;
+    ncclResult_t last_nccl = ncclSuccess;
+};
+
+#define HIPCHK(x)                                                                          \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            ctx->last_err = e_;                                                            \
+            fprintf(stderr, "tfidf: HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+            return TFIDF_E_HIP;                                                            \
+        }                                                                                  \
+    } while (0)
+#define NCCLCHK(x)                                                                         \
+    do {                                                                                   \
+        ncclResult_t r_ = (x);                                                             \
+        if (r_ != ncclSuccess) {                                                           \
+            ctx->last_nccl = r_;                                                           \
+            fprintf(stderr, "tfidf: RCCL error %s at %s:%d\n", ncclGetErrorString(r_), __FILE__, __LINE__); \
+            return TFIDF_E_RCCL;                                                           \
+        }                                                                                  \
+    } while (0)
+#define ENSURE(buf, bytes)                                   \
+    do {                                                     \
+        if ((buf).ensure((size_t)(bytes)) != 0) return TFIDF_E_NOMEM; \
+    } while (0)
+#define LCHK(x)                                              \
+    do {                                                     \
+        int l_ = (x);                                        \
+        if (l_ == -2) return 1; /* arena too small: retry */ \
+        if (l_ < 0) { HIPCHK(hipGetLastError()); return TFIDF_E_HIP; } \
+    } while (0)
+
+static int arena_reset(tfidf_ctx* ctx, size_t want) {
+    if (want > ctx->arena_buf.cap) {
+        if (ctx->arena_buf.ensure(want) != 0) return TFIDF_E_NOMEM;
+    }
+    ctx->arena.base = (uint8_t*)ctx->arena_buf.p;
+    ctx->arena.cap = ctx->arena_buf.cap;
+    ctx->arena.used = 0;
+    return 0;
+}
+
+static void mark(tfidf_ctx* ctx, int stage) {
+    if (ctx->timing) (void)hipEventRecord(ctx->ev[stage], ctx->stream);
+}
+
+extern "C" {
+
+int tfidf_open(int device, tfidf_ctx** out) {
+    if (!out) return TFIDF_E_INVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) return TFIDF_E_NODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return TFIDF_E_NODEV;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        fprintf(stderr, "tfidf: device %d is %s, need gfx950\n", device, prop.gcnArchName);
+        return TFIDF_E_NODEV;
+    }
+    if (hipSetDevice(device) != hipSuccess) return TFIDF_E_NODEV;
+    tfidf_ctx* ctx = new tfidf_ctx();
+    ctx->device = device;
+    HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    for (int i = 0; i <= S_NSTAGES; ++i) HIPCHK(hipEventCreate(&ctx->ev[i]));
+    if (arena_reset(ctx, 64ull << 20) != 0) { delete ctx; return TFIDF_E_NOMEM; }
+    if (ctx->counters.ensure(256) != 0) { delete ctx; return TFIDF_E_NOMEM; }
+    *out = ctx;
+    return TFIDF_OK;
+}
+
+void tfidf_close(tfidf_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+    DevBuf* bufs[] = {&ctx->arena_buf, &ctx->in_bytes, &ctx->in_off, &ctx->in_ids, &ctx->syn_bytes, &ctx->syn_off,
+                      &ctx->syn_ids, &ctx->syn_ntok, &ctx->syn_blkfirst, &ctx->syn_blkbytes, &ctx->syn_cdf,
+                      &ctx->chunk_start, &ctx->chunk_doc, &ctx->vkeys, &ctx->vrep, &ctx->rec_slot, &ctx->rec_cnt,
+                      &ctx->part_doc, &ctx->part_slot, &ctx->part_cnt, &ctx->doc_recoff, &ctx->doc_npairs,
+                      &ctx->doc_size, &ctx->doc_flags, &ctx->counters, &ctx->dense, &ctx->vslot, &ctx->skey0,
+                      &ctx->skey1, &ctx->seq0, &ctx->seq1, &ctx->rank_of_slot, &ctx->slot_of_rank, &ctx->pkey0,
+                      &ctx->pkey1, &ctx->pseq0, &ctx->pseq1, &ctx->phead, &ctx->df_local, &ctx->df_global,
+                      &ctx->present, &ctx->idf_vals, &ctx->dkey0, &ctx->dkey1, &ctx->dseq0, &ctx->dseq1,
+                      &ctx->npairs_ord, &ctx->out_off, &ctx->out_doc, &ctx->out_term, &ctx->out_cnt,
+                      &ctx->out_docsize, &ctx->out_df, &ctx->out_score, &ctx->x_mine, &ctx->x_send, &ctx->x_recv,
+                      &ctx->x_recv2, &ctx->x_seq0, &ctx->x_seq1, &ctx->x_head, &ctx->x_grank, &ctx->x_dfv,
+                      &ctx->x_cnt};
+    for (DevBuf* b : bufs) b->release();
+    for (int i = 0; i <= S_NSTAGES; ++i) (void)hipEventDestroy(ctx->ev[i]);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int tfidf_set_timing(tfidf_ctx* ctx, int enable) {
+    if (!ctx) return TFIDF_E_INVAL;
+    ctx->timing = enable != 0;
+    return TFIDF_OK;
+}
+
+const char* tfidf_stage_name(int stage) { return (stage >= 0 && stage < S_NSTAGES) ? kStageNames[stage] : "?"; }
+
+int tfidf_comm_unique_id(uint8_t id[TFIDF_UNIQUE_ID_BYTES]) {
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return TFIDF_E_RCCL;
+    memcpy(id, &u, TFIDF_UNIQUE_ID_BYTES);
+    return TFIDF_OK;
+}
+
+int tfidf_comm_init(tfidf_ctx* ctx, const uint8_t id[TFIDF_UNIQUE_ID_BYTES], int rank, int nranks) {
+    if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return TFIDF_E_INVAL;
+    HIPCHK(hipSetDevice(ctx->device));
+    if (ctx->comm) { (void)ncclCommDestroy(ctx->comm); ctx->comm = nullptr; }
+    ncclUniqueId u;
+    memcpy(&u, id, TFIDF_UNIQUE_ID_BYTES);
+    NCCLCHK(ncclCommInitRank(&ctx->comm, nranks, u, rank));
+    ctx->rank = rank;
+    ctx->nranks = nranks;
+    return TFIDF_OK;
+}
+
+}  // extern "C"
+
+/* ------------------------------------------------------------------------------ */
+
+/* RCCL vocabulary agreement + DF all-reduce.  Returns df_global (by local rank). */
+static int exchange_df(tfidf_ctx* ctx, uint32_t V) {
+    hipStream_t s = ctx->stream;
+    Arena& ar = ctx->arena;
+    ENSURE(ctx->x_cnt, 8 * (size_t)ctx->nranks + 8);
+    ENSURE(ctx->x_mine, (size_t)V * 16 + 16);
+    LCHK(launch_keys_by_rank(ctx->vkeys.as<uint4>(), ctx->slot_of_rank.as<uint32_t>(), V, ctx->x_mine.as<uint4>(), s));
+    uint64_t* cnts = ctx->x_cnt.as<uint64_t>();
+    uint64_t myv = V;
+    HIPCHK(hipMemcpyAsync(cnts + ctx->nranks, &myv, 8, hipMemcpyHostToDevice, s));
+    NCCLCHK(ncclAllGather(cnts + ctx->nranks, cnts, 1, ncclUint64, ctx->comm, s));
+    std::vector<uint64_t> hc(ctx->nranks);
+    HIPCHK(hipMemcpyAsync(hc.data(), cnts, 8 * ctx->nranks, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    uint64_t maxv = 1;
+    for (uint64_t c : hc) maxv = c > maxv ? c : maxv;
+    uint64_t ntot = maxv * ctx->nranks;
+    ENSURE(ctx->x_send, maxv * 16);
+    ENSURE(ctx->x_recv, ntot * 16);
+    ENSURE(ctx->x_recv2, ntot * 16);
+    ENSURE(ctx->x_seq0, ntot * 4);
+    ENSURE(ctx->x_seq1, ntot * 4);
+    ENSURE(ctx->x_head, (ntot + 1) * 4);
+    HIPCHK(hipMemsetAsync(ctx->x_send.p, 0xEE, maxv * 16, s)); /* padding = empty-slot sentinel key */
+    if (V) HIPCHK(hipMemcpyAsync(ctx->x_send.p, ctx->x_mine.p, (size_t)V * 16, hipMemcpyDeviceToDevice, s));
+    NCCLCHK(ncclAllGather(ctx->x_send.p, ctx->x_recv.p, maxv * 16, ncclUint8, ctx->comm, s));
+    HIPCHK(hipMemsetAsync(ctx->x_seq0.p, 0, ntot * 4, s));
+    uint32_t vm = 0;
+    LCHK(key_varying_bytes_u128(ctx->x_recv.as<uint4>(), ntot, &vm, ar, s));
+    int cur = radix_sort_u128(ctx->x_recv.as<uint4>(), ctx->x_seq0.as<uint32_t>(), ctx->x_recv2.as<uint4>(),
+                              ctx->x_seq1.as<uint32_t>(), ntot, vm, ar, s);
+    LCHK(cur);
+    uint4* u = cur ? ctx->x_recv2.as<uint4>() : ctx->x_recv.as<uint4>();
+    uint32_t* head = ctx->x_head.as<uint32_t>();
+    LCHK(launch_union_heads(u, ntot, head, s));
+    LCHK(scan_excl_u32(head, head, ntot, ar, s));
+    uint32_t Vg = 0;
+    HIPCHK(hipMemcpyAsync(&Vg, head + ntot, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    ctx->Vg = Vg;
+    ENSURE(ctx->x_grank, (size_t)V * 4 + 4);
+    ENSURE(ctx->x_dfv, (size_t)Vg * 4 + 4);
+    LCHK(launch_union_lookup(ctx->x_mine.as<uint4>(), V, u, head, ntot, nullptr, ctx->x_grank.as<uint32_t>(), s));
+    HIPCHK(hipMemsetAsync(ctx->x_dfv.p, 0, (size_t)Vg * 4, s));
+    LCHK(launch_scatter_df(ctx->df_local.as<uint32_t>(), ctx->x_grank.as<uint32_t>(), V, ctx->x_dfv.as<uint32_t>(), s));
+    NCCLCHK(ncclAllReduce(ctx->x_dfv.p, ctx->x_dfv.p, Vg, ncclUint32, ncclSum, ctx->comm, s));
+    LCHK(launch_gather_df(ctx->x_dfv.as<uint32_t>(), ctx->x_grank.as<uint32_t>(), V, ctx->df_global.as<uint32_t>(), s));
+    return 0;
+}
+
+/* One attempt of the pipeline.  Returns 0 on success, 1 to retry with grown
+ * capacities, <0 on error. */
+static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids, uint64_t Nt) {
+    hipStream_t s = ctx->stream;
+    Arena& ar = ctx->arena;
+    const uint32_t N = c.ndocs;
+    ar.used = 0;
+    mark(ctx, S_PREP);
+    /* ---- buffers ---- */
+    const uint64_t span = c.hi - c.lo;
+    const uint64_t nchunks = span ? (span + CHUNK_BYTES - 1) / CHUNK_BYTES : 0;
+    if (ctx->rec_cap == 0) ctx->rec_cap = span / 6 + 4096;
+    if (ctx->part_cap == 0) ctx->part_cap = span / 64 + 4096;
+    ENSURE(ctx->chunk_start, (nchunks + 1) * 8);
+    ENSURE(ctx->chunk_doc, (nchunks + 1) * 4);
+    ENSURE(ctx->vkeys, ctx->vcap * 16);
+    ENSURE(ctx->vrep, ctx->vcap * 8);
+    ENSURE(ctx->rec_slot, ctx->rec_cap * 4);
+    ENSURE(ctx->rec_cnt, ctx->rec_cap * 4);
+    ENSURE(ctx->part_doc, ctx->part_cap * 4);
+    ENSURE(ctx->part_slot, ctx->part_cap * 4);
+    ENSURE(ctx->part_cnt, ctx->part_cap * 4);
+    ENSURE(ctx->doc_recoff, (size_t)N * 8 + 8);
+    ENSURE(ctx->doc_npairs, (size_t)N * 4 + 4);
+    ENSURE(ctx->doc_size, (size_t)N * 4 + 4);
+    ENSURE(ctx->doc_flags, (size_t)N + 1);
+    unsigned long long* cnt = ctx->counters.as<unsigned long long>(); /* rec, part, ntok, status */
+    HIPCHK(hipMemsetAsync(ctx->vkeys.p, 0xEE, ctx->vcap * 16, s));
+    HIPCHK(hipMemsetAsync(cnt, 0, 64, s));
+    HIPCHK(hipMemsetAsync(ctx->doc_npairs.p, 0, (size_t)N * 4 + 4, s));
+    HIPCHK(hipMemsetAsync(ctx->doc_size.p, 0, (size_t)N * 4 + 4, s));
+    HIPCHK(hipMemsetAsync(ctx->doc_flags.p, 0, (size_t)N + 1, s));
+    if (nchunks) LCHK(launch_plan_chunks(c, nchunks, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), s));
+    /* ---- K1 ---- */
+    mark(ctx, S_TOKCOUNT);
+    VocabDev vd{ctx->vkeys.as<uint4>(), ctx->vrep.as<uint64_t>(), ctx->vcap - 1};
+    K1Out o{};
+    o.rec_slot = ctx->rec_slot.as<uint32_t>();
+    o.rec_cnt = ctx->rec_cnt.as<uint32_t>();
+    o.rec_alloc = cnt + 0;
+    o.rec_cap = ctx->rec_cap;
+    o.part_doc = ctx->part_doc.as<uint32_t>();
+    o.part_slot = ctx->part_slot.as<uint32_t>();
+    o.part_cnt = ctx->part_cnt.as<uint32_t>();
+    o.part_alloc = cnt + 1;
+    o.part_cap = ctx->part_cap;
+    o.doc_recoff = ctx->doc_recoff.as<uint64_t>();
+    o.doc_npairs = ctx->doc_npairs.as<uint32_t>();
+    o.doc_size = ctx->doc_size.as<uint32_t>();
+    o.doc_flags = ctx->doc_flags.as<uint8_t>();
+    o.ntokens = cnt + 2;
+    o.status = (uint32_t*)(cnt + 3);
+    if (nchunks)
+        LCHK(launch_tokcount(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
+    mark(ctx, S_VOCAB);
+    unsigned long long hc[4];
+    HIPCHK(hipMemcpyAsync(hc, cnt, sizeof hc, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const uint64_t R_main = hc[0], Q = hc[1];
+    const uint32_t st = (uint32_t)hc[3];
+    ctx->ntokens = hc[2];
+    ctx->nchunks = nchunks;
+    ctx->nrec_part = Q;
+    if (st & ST_VOCAB_SPIN) return TFIDF_E_CAPACITY;
+    bool retry = false;
+    if (st & ST_VOCAB_FULL) { ctx->vcap *= 4; retry = true; }
+    if (st & ST_REC_FULL) { ctx->rec_cap = R_main + R_main / 4 + 4096; retry = true; }
+    if (st & ST_PART_FULL) { ctx->part_cap = Q + Q / 4 + 4096; retry = true; }
+    if (retry) return 1;
+    /* ---- vocabulary ---- */
+    const uint64_t cap = ctx->vcap;
+    ENSURE(ctx->dense, (cap + 1) * 4);
+    LCHK(launch_vocab_flags(vd, cap, ctx->dense.as<uint32_t>(), s));
+    LCHK(scan_excl_u32(ctx->dense.as<uint32_t>(), ctx->dense.as<uint32_t>(), cap, ar, s));
+    uint32_t V = 0;
+    HIPCHK(hipMemcpyAsync(&V, ctx->dense.as<uint32_t>() + cap, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    ctx->V = V;
+    if ((uint64_t)V * 2 > cap) { ctx->vcap *= 4; return 1; } /* keep probes short */
+    ENSURE(ctx->vslot, (size_t)V * 4 + 4);
+    ENSURE(ctx->skey0, (size_t)V * 16 + 16);
+    ENSURE(ctx->skey1, (size_t)V * 16 + 16);
+    ENSURE(ctx->seq0, (size_t)V * 4 + 4);
+    ENSURE(ctx->seq1, (size_t)V * 4 + 4);
+    ENSURE(ctx->rank_of_slot, cap * 4);
+    ENSURE(ctx->slot_of_rank, (size_t)V * 4 + 4);
+    LCHK(launch_vocab_compact(vd, cap, ctx->dense.as<uint32_t>(), c, ctx->vslot.as<uint32_t>(), ctx->skey0.as<uint4>(),
+                              ctx->seq0.as<uint32_t>(), s));
+    uint32_t vm = 0;
+    LCHK(key_varying_bytes_u128(ctx->skey0.as<uint4>(), V, &vm, ar, s));
+    int cur = radix_sort_u128(ctx->skey0.as<uint4>(), ctx->seq0.as<uint32_t>(), ctx->skey1.as<uint4>(),
+                              ctx->seq1.as<uint32_t>(), V, vm, ar, s);
+    LCHK(cur);
+    ctx->sorted_skey = cur ? ctx->skey1.as<uint4>() : ctx->skey0.as<uint4>();
+    ctx->sorted_dense = cur ? ctx->seq1.as<uint32_t>() : ctx->seq0.as<uint32_t>();
+    LCHK(launch_vocab_long_fixup(ctx->sorted_skey, ctx->sorted_dense, ctx->vslot.as<uint32_t>(), vd, c, V, s));
+    LCHK(launch_vocab_rank(ctx->sorted_dense, ctx->vslot.as<uint32_t>(), V, ctx->rank_of_slot.as<uint32_t>(),
+                           ctx->slot_of_rank.as<uint32_t>(), s));
+    /* ---- partial documents ---- */
+    mark(ctx, S_MERGE);
+    uint64_t R_total = R_main;
+    if (Q) {
+        ENSURE(ctx->pkey0, Q * 8);
+        ENSURE(ctx->pkey1, Q * 8);
+        ENSURE(ctx->pseq0, Q * 4);
+        ENSURE(ctx->pseq1, Q * 4);
+        ENSURE(ctx->phead, (Q + 1) * 4);
+        LCHK(launch_part_keys(ctx->part_doc.as<uint32_t>(), ctx->part_slot.as<uint32_t>(), ctx->rank_of_slot.as<uint32_t>(),
+                              Q, ctx->pkey0.as<uint64_t>(), ctx->pseq0.as<uint32_t>(), s));
+        uint32_t pm = 0;
+        LCHK(key_varying_bytes_u64(ctx->pkey0.as<uint64_t>(), Q, &pm, ar, s));
+        int pc = radix_sort_u64(ctx->pkey0.as<uint64_t>(), ctx->pseq0.as<uint32_t>(), ctx->pkey1.as<uint64_t>(),
+                                ctx->pseq1.as<uint32_t>(), Q, pm, ar, s);
+        LCHK(pc);
+        uint64_t* pk = pc ? ctx->pkey1.as<uint64_t>() : ctx->pkey0.as<uint64_t>();
+        uint32_t* ps = pc ? ctx->pseq1.as<uint32_t>() : ctx->pseq0.as<uint32_t>();
+        uint32_t* ph = ctx->phead.as<uint32_t>();
+        LCHK(launch_part_heads(pk, Q, ph, s));
+        LCHK(scan_excl_u32(ph, ph, Q, ar, s));
+        uint32_t U = 0;
+        HIPCHK(hipMemcpyAsync(&U, ph + Q, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (R_main + U > ctx->rec_cap) {
+            uint64_t ncap = R_main + U + (R_main + U) / 8 + 4096;
+            if (ctx->rec_slot.grow_keep(ncap * 4, R_main * 4, s) || ctx->rec_cnt.grow_keep(ncap * 4, R_main * 4, s))
+                return TFIDF_E_NOMEM;
+            ctx->rec_cap = ncap;
+        }
+        LCHK(launch_part_merge(pk, ps, ctx->part_cnt.as<uint32_t>(), ph, Q, ctx->slot_of_rank.as<uint32_t>(), R_main,
+                               ctx->rec_slot.as<uint32_t>(), ctx->rec_cnt.as<uint32_t>(),
+                               ctx->doc_recoff.as<uint64_t>(), ctx->doc_npairs.as<uint32_t>(),
+                               ctx->doc_flags.as<uint8_t>(), s));
+        R_total = R_main + U;
+    }
+    /* ---- DF ---- */
+    mark(ctx, S_DF);
+    ENSURE(ctx->df_local, (size_t)V * 4 + 4);
+    ENSURE(ctx->df_global, (size_t)V * 4 + 4);
+    LCHK(launch_df_hist(ctx->rec_slot.as<uint32_t>(), R_total, ctx->rank_of_slot.as<uint32_t>(), V,
+                        ctx->df_local.as<uint32_t>(), ar, s));
+    mark(ctx, S_EXCHANGE);
+    if (ctx->comm && ctx->nranks > 1) {
+        int rc = exchange_df(ctx, V);
+        if (rc) return rc;
+    } else {
+        ctx->Vg = V;
+        if (V) HIPCHK(hipMemcpyAsync(ctx->df_global.p, ctx->df_local.p, (size_t)V * 4, hipMemcpyDeviceToDevice, s));
+    }
+    /* ---- idf LUT: log(N/df) on the host's libm for each distinct df (TFIDF.c:243) ---- */
+    mark(ctx, S_IDF);
+    ENSURE(ctx->present, (Nt + 2) * 4);
+    HIPCHK(hipMemsetAsync(ctx->present.p, 0, (Nt + 2) * 4, s));
+    LCHK(launch_df_mark(ctx->df_global.as<uint32_t>(), V, ctx->present.as<uint32_t>(), s));
+    LCHK(scan_excl_u32(ctx->present.as<uint32_t>(), ctx->present.as<uint32_t>(), Nt + 1, ar, s));
+    uint32_t K = 0;
+    HIPCHK(hipMemcpyAsync(&K, ctx->present.as<uint32_t>() + Nt + 1, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    ENSURE(ctx->idf_vals, (size_t)K * 8 + 8);
+    uint32_t* vals_dev = (uint32_t*)ar.get((size_t)K * 4 + 4);
+    if (!vals_dev) return 1;
+    LCHK(launch_df_list(ctx->present.as<uint32_t>(), Nt + 1, vals_dev, s));
+    std::vector<uint32_t> vals(K);
+    std::vector<double> idf(K);
+    if (K) HIPCHK(hipMemcpyAsync(vals.data(), vals_dev, (size_t)K * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (uint32_t k = 0; k < K; ++k) idf[k] = log(1.0 * (double)Nt / (double)vals[k]);
+    if (K) HIPCHK(hipMemcpyAsync(ctx->idf_vals.p, idf.data(), (size_t)K * 8, hipMemcpyHostToDevice, s));
+    /* ---- document order ---- */
+    mark(ctx, S_ORDER);
+    ENSURE(ctx->dkey0, (size_t)N * 8 + 8);
+    ENSURE(ctx->dkey1, (size_t)N * 8 + 8);
+    ENSURE(ctx->dseq0, (size_t)N * 4 + 4);
+    ENSURE(ctx->dseq1, (size_t)N * 4 + 4);
+    ENSURE(ctx->npairs_ord, (size_t)N * 8 + 8);
+    ENSURE(ctx->out_off, (size_t)N * 8 + 8);
+    LCHK(launch_doc_keys(dev_ids, N, ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), s));
+    uint32_t dm = 0;
+    LCHK(key_varying_bytes_u64(ctx->dkey0.as<uint64_t>(), N, &dm, ar, s));
+    int dc = radix_sort_u64(ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), ctx->dkey1.as<uint64_t>(),
+                            ctx->dseq1.as<uint32_t>(), N, dm, ar, s);
+    LCHK(dc);
+    ctx->order = dc ? ctx->dseq1.as<uint32_t>() : ctx->dseq0.as<uint32_t>();
+    LCHK(launch_gather_npairs(ctx->order, ctx->doc_npairs.as<uint32_t>(), N, ctx->npairs_ord.as<uint64_t>(), s));
+    LCHK(scan_excl_u64(ctx->npairs_ord.as<uint64_t>(), ctx->out_off.as<uint64_t>(), N, ar, s));
+    uint64_t P = 0;
+    HIPCHK(hipMemcpyAsync(&P, ctx->out_off.as<uint64_t>() + N, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    ctx->npairs = P;
+    /* ---- score + per-document term order ---- */
+    mark(ctx, S_SCORE);
+    ENSURE(ctx->out_doc, P * 4 + 4);
+    ENSURE(ctx->out_term, P * 4 + 4);
+    ENSURE(ctx->out_cnt, P * 4 + 4);
+    ENSURE(ctx->out_docsize, P * 4 + 4);
+    ENSURE(ctx->out_df, P * 4 + 4);
+    ENSURE(ctx->out_score, P * 8 + 8);
+    K5Args a{};
+    a.order = ctx->order;
+    a.out_off = ctx->out_off.as<uint64_t>();
+    a.doc_recoff = ctx->doc_recoff.as<uint64_t>();
+    a.doc_npairs = ctx->doc_npairs.as<uint32_t>();
+    a.doc_size = ctx->doc_size.as<uint32_t>();
+    a.doc_flags = ctx->doc_flags.as<uint8_t>();
+    a.doc_ids = dev_ids;
+    a.rec_slot = ctx->rec_slot.as<uint32_t>();
+    a.rec_cnt = ctx->rec_cnt.as<uint32_t>();
+    a.rank_of_slot = ctx->rank_of_slot.as<uint32_t>();
+    a.df_of_rank = ctx->df_global.as<uint32_t>();
+    a.idf_idx = ctx->present.as<uint32_t>();
+    a.idf = ctx->idf_vals.as<double>();
+    a.ndocs = N;
+    a.out_doc = ctx->out_doc.as<uint32_t>();
+    a.out_term = ctx->out_term.as<uint32_t>();
+    a.out_cnt = ctx->out_cnt.as<uint32_t>();
+    a.out_docsize = ctx->out_docsize.as<uint32_t>();
+    a.out_df = ctx->out_df.as<uint32_t>();
+    a.out_score = ctx->out_score.as<double>();
+    LCHK(launch_score_order(a, s));
+    mark(ctx, S_NSTAGES);
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+}
+
+extern "C" int tfidf_run(tfidf_ctx* ctx, const tfidf_corpus* in) {
+    if (!ctx || !in) return TFIDF_E_INVAL;
+    if (in->ndocs && !in->doc_off) return TFIDF_E_INVAL;
+    if (in->nbytes && !in->bytes) return TFIDF_E_INVAL;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const uint32_t N = in->ndocs;
+    const bool dev = (in->flags & TFIDF_CORPUS_DEVICE) != 0;
+    CorpusDev c{};
+    const uint32_t* dev_ids = nullptr;
+    uint64_t lo = 0, hi = 0;
+    if (dev) {
+        c.bytes = in->bytes;
+        c.doc_off = in->doc_off;
+        dev_ids = in->doc_ids;
+        uint64_t e[2] = {0, 0};
+        if (N) {
+            HIPCHK(hipMemcpy(&e[0], in->doc_off, 8, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(&e[1], in->doc_off + N, 8, hipMemcpyDeviceToHost));
+        }
+        lo = e[0]; hi = e[1];
+    } else {
+        ENSURE(ctx->in_bytes, in->nbytes + 64);
+        ENSURE(ctx->in_off, ((size_t)N + 1) * 8);
+        if (in->nbytes) HIPCHK(hipMemcpyAsync(ctx->in_bytes.p, in->bytes, in->nbytes, hipMemcpyHostToDevice, s));
+        if (N || in->doc_off) HIPCHK(hipMemcpyAsync(ctx->in_off.p, in->doc_off, ((size_t)N + 1) * 8, hipMemcpyHostToDevice, s));
+        if (in->doc_ids) {
+            ENSURE(ctx->in_ids, (size_t)N * 4 + 4);
+            HIPCHK(hipMemcpyAsync(ctx->in_ids.p, in->doc_ids, (size_t)N * 4, hipMemcpyHostToDevice, s));
+            dev_ids = ctx->in_ids.as<uint32_t>();
+        }
+        c.bytes = ctx->in_bytes.as<uint8_t>();
+        c.doc_off = ctx->in_off.as<uint64_t>();
+        if (N) { lo = in->doc_off[0]; hi = in->doc_off[N]; }
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    if (hi > in->nbytes || lo > hi) return TFIDF_E_INVAL;
+    c.nbytes = in->nbytes;
+    c.ndocs = N;
+    c.lo = lo;
+    c.hi = hi;
+    const uint64_t Nt = in->ndocs_total ? in->ndocs_total : N;
+    if (Nt < N || Nt > 0xFFFFFFFFull) return TFIDF_E_INVAL;
+    ctx->have_result = false;
+    int rc = 1;
+    for (int attempt = 0; attempt < 8 && rc == 1; ++attempt) {
+        size_t need = ctx->arena.peak > ctx->arena_buf.cap ? ctx->arena.peak * 2 : ctx->arena_buf.cap;
+        if (arena_reset(ctx, need) != 0) return TFIDF_E_NOMEM;
+        rc = run_once(ctx, c, dev_ids, Nt);
+        if (rc == 1) HIPCHK(hipStreamSynchronize(s));
+    }
+    if (rc == 1) return TFIDF_E_CAPACITY;
+    if (rc) return rc;
+    ctx->corpus = *in;
+    ctx->dev_bytes = c.bytes;
+    ctx->dev_ids = dev_ids;
+    ctx->ndocs = N;
+    ctx->ndocs_total = Nt;
+    ctx->have_result = true;
+    if (ctx->timing) {
+        for (int i = 0; i < S_NSTAGES; ++i) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, ctx->ev[i], ctx->ev[i + 1]);
+            ctx->ms_stage[i] = ms;
+        }
+        float tot = 0;
+        (void)hipEventElapsedTime(&tot, ctx->ev[S_PREP], ctx->ev[S_NSTAGES]);
+        ctx->ms_total = tot;
+    }
+    return TFIDF_OK;
+}
+
+extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info) {
+    if (!ctx || !info) return TFIDF_E_INVAL;
+    if (!ctx->have_result) return TFIDF_E_STATE;
+    memset(info, 0, sizeof(*info));
+    info->nbytes = ctx->corpus.ndocs ? 0 : 0;
+    {
+        uint64_t lo = 0, hi = 0;
+        if (ctx->corpus.ndocs) {
+            if (ctx->corpus.flags & TFIDF_CORPUS_DEVICE) {
+                (void)hipMemcpy(&lo, ctx->corpus.doc_off, 8, hipMemcpyDeviceToHost);
+                (void)hipMemcpy(&hi, ctx->corpus.doc_off + ctx->corpus.ndocs, 8, hipMemcpyDeviceToHost);
+            } else {
+                lo = ctx->corpus.doc_off[0];
+                hi = ctx->corpus.doc_off[ctx->corpus.ndocs];
+            }
+        }
+        info->nbytes = hi - lo;
+    }
+    info->ntokens = ctx->ntokens;
+    info->npairs = ctx->npairs;
+    info->nterms = ctx->V;
+    info->nterms_global = ctx->Vg;
+    info->nchunks = ctx->nchunks;
+    info->partial_records = ctx->nrec_part;
+    info->ndocs = ctx->ndocs;
+    info->vocab_capacity = (uint32_t)ctx->vcap;
+    info->ms_total = ctx->ms_total;
+    info->ms_tokcount = ctx->ms_stage[S_TOKCOUNT];
+    for (int i = 0; i < S_NSTAGES; ++i) info->ms_stage[i] = ctx->ms_stage[i];
+    info->nstages = S_NSTAGES;
+    return TFIDF_OK;
+}
+
+/* ------------------------------------------------------------------- fetch -- */
+
+extern "C" void tfidf_result_free(tfidf_result* r) {
+    if (!r) return;
+    free(r->pair_doc); free(r->pair_term); free(r->pair_count); free(r->pair_docsize); free(r->pair_df);
+    free(r->pair_score); free(r->doc_id); free(r->doc_size); free(r->term_off); free(r->term_bytes);
+    free(r->term_df);
+    memset(r, 0, sizeof(*r));
+}
+
+extern "C" int tfidf_fetch(tfidf_ctx* ctx, tfidf_result* r) {
+    if (!ctx || !r) return TFIDF_E_INVAL;
+    if (!ctx->have_result) return TFIDF_E_STATE;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    memset(r, 0, sizeof(*r));
+    const uint64_t P = ctx->npairs;
+    const uint32_t N = ctx->ndocs, V = ctx->V;
+    r->npairs = P;
+    r->ndocs = N;
+    r->nterms = V;
+    r->ndocs_total = ctx->ndocs_total;
+    size_t p4 = (size_t)P * 4 + 4;
+    r->pair_doc = (uint32_t*)malloc(p4);
+    r->pair_term = (uint32_t*)malloc(p4);
+    r->pair_count = (uint32_t*)malloc(p4);
+    r->pair_docsize = (uint32_t*)malloc(p4);
+    r->pair_df = (uint32_t*)malloc(p4);
+    r->pair_score = (double*)malloc((size_t)P * 8 + 8);
+    r->doc_id = (uint32_t*)malloc((size_t)N * 4 + 4);
+    r->doc_size = (uint32_t*)malloc((size_t)N * 4 + 4);
+    r->term_df = (uint32_t*)malloc((size_t)V * 4 + 4);
+    r->term_off = (uint64_t*)malloc(((size_t)V + 1) * 8);
+    if (!r->pair_doc || !r->pair_term || !r->pair_count || !r->pair_docsize || !r->pair_df || !r->pair_score ||
+        !r->doc_id || !r->doc_size || !r->term_df || !r->term_off) {
+        tfidf_result_free(r);
+        return TFIDF_E_NOMEM;
+    }
+    if (P) {
+        HIPCHK(hipMemcpyAsync(r->pair_doc, ctx->out_doc.p, P * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(r->pair_term, ctx->out_term.p, P * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(r->pair_count, ctx->out_cnt.p, P * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(r->pair_docsize, ctx->out_docsize.p, P * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(r->pair_df, ctx->out_df.p, P * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(r->pair_score, ctx->out_score.p, P * 8, hipMemcpyDeviceToHost, s));
+    }
+    if (N) HIPCHK(hipMemcpyAsync(r->doc_size, ctx->doc_size.p, (size_t)N * 4, hipMemcpyDeviceToHost, s));
+    if (V) HIPCHK(hipMemcpyAsync(r->term_df, ctx->df_global.p, (size_t)V * 4, hipMemcpyDeviceToHost, s));
+    /* term strings in rank order */
+    std::vector<uint4> keys(V);
+    std::vector<uint32_t> sor(V);
+    if (V) {
+        HIPCHK(hipMemcpyAsync(sor.data(), ctx->slot_of_rank.p, (size_t)V * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        ENSURE(ctx->x_mine, (size_t)V * 16 + 16);
+        if (launch_keys_by_rank(ctx->vkeys.as<uint4>(), ctx->slot_of_rank.as<uint32_t>(), V, ctx->x_mine.as<uint4>(), s))
+            return TFIDF_E_HIP;
+        HIPCHK(hipMemcpyAsync(keys.data(), ctx->x_mine.p, (size_t)V * 16, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    if (ctx->corpus.doc_ids && !(ctx->corpus.flags & TFIDF_CORPUS_DEVICE)) {
+        memcpy(r->doc_id, ctx->corpus.doc_ids, (size_t)N * 4);
+    } else if (ctx->dev_ids) {
+        HIPCHK(hipMemcpy(r->doc_id, ctx->dev_ids, (size_t)N * 4, hipMemcpyDeviceToHost));
+    } else {
+        for (uint32_t i = 0; i < N; ++i) r->doc_id[i] = i + 1;
+    }
+    std::string pool;
+    pool.reserve((size_t)V * 8);
+    for (uint32_t t = 0; t < V; ++t) {
+        r->term_off[t] = pool.size();
+        uint64_t lo = ((uint64_t)keys[t].y << 32) | keys[t].x, hi = ((uint64_t)keys[t].w << 32) | keys[t].z;
+        if ((hi >> 56) == 0xFFu) {
+            uint64_t rep = 0;
+            HIPCHK(hipMemcpy(&rep, ctx->vrep.as<uint64_t>() + sor[t], 8, hipMemcpyDeviceToHost));
+            uint64_t off = rep & 0xFFFFFFFFFFull, len = rep >> 40;
+            std::string w(len, '\0');
+            HIPCHK(hipMemcpy(&w[0], ctx->dev_bytes + off, len, hipMemcpyDeviceToHost));
+            pool += w;
+        } else {
+            uint8_t b[16];
+            memcpy(b, &lo, 8);
+            memcpy(b + 8, &hi, 8);
+            int n = 0;
+            while (n < 16 && b[n] != 0x09) ++n;
+            pool.append((const char*)b, (size_t)n);
+        }
+    }
+    r->term_off[V] = pool.size();
+    r->term_bytes = (uint8_t*)malloc(pool.size() + 1);
+    if (!r->term_bytes) { tfidf_result_free(r); return TFIDF_E_NOMEM; }
+    memcpy(r->term_bytes, pool.data(), pool.size());
+    return TFIDF_OK;
+}
+
+/* ----------------------------------------------------------------- synthetic -- */
+
+extern "C" int tfidf_synth_device(tfidf_ctx* ctx, uint64_t seed, uint32_t V, uint32_t mode, const double* cdf,
+                                  const uint32_t* doc_ids, const uint64_t* ntok, uint32_t ndocs,
+                                  uint64_t ndocs_total, tfidf_corpus* out) {
+    if (!ctx || !ntok || !out || V == 0 || (mode == SYN_MODE_ZIPF && !cdf)) return TFIDF_E_INVAL;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    std::vector<uint64_t> bf((size_t)ndocs + 1);
+    uint64_t nb = 0;
+    for (uint32_t i = 0; i < ndocs; ++i) { bf[i] = nb; nb += (ntok[i] + SYN_BLOCK_TOKENS - 1) / SYN_BLOCK_TOKENS; }
+    bf[ndocs] = nb;
+    ENSURE(ctx->syn_blkfirst, bf.size() * 8);
+    ENSURE(ctx->syn_ntok, (size_t)ndocs * 8 + 8);
+    ENSURE(ctx->syn_blkbytes, (nb + 1) * 8);
+    ENSURE(ctx->syn_off, ((size_t)ndocs + 1) * 8);
+    HIPCHK(hipMemcpyAsync(ctx->syn_blkfirst.p, bf.data(), bf.size() * 8, hipMemcpyHostToDevice, s));
+    if (ndocs) HIPCHK(hipMemcpyAsync(ctx->syn_ntok.p, ntok, (size_t)ndocs * 8, hipMemcpyHostToDevice, s));
+    const uint32_t* dids = nullptr;
+    if (doc_ids) {
+        ENSURE(ctx->syn_ids, (size_t)ndocs * 4 + 4);
+        HIPCHK(hipMemcpyAsync(ctx->syn_ids.p, doc_ids, (size_t)ndocs * 4, hipMemcpyHostToDevice, s));
+        dids = ctx->syn_ids.as<uint32_t>();
+    }
+    const double* dcdf = nullptr;
+    if (mode == SYN_MODE_ZIPF) {
+        ENSURE(ctx->syn_cdf, (size_t)V * 8);
+        HIPCHK(hipMemcpyAsync(ctx->syn_cdf.p, cdf, (size_t)V * 8, hipMemcpyHostToDevice, s));
+        dcdf = ctx->syn_cdf.as<double>();
+    }
+    syn_spec sp;
+    tfidf_synth_spec(&sp, seed, V, mode, dcdf);
+    if (arena_reset(ctx, ctx->arena_buf.cap) != 0) return TFIDF_E_NOMEM;
+    if (launch_synth_bytes(&sp, dids, ctx->syn_ntok.as<uint64_t>(), ctx->syn_blkfirst.as<uint64_t>(), nb, ndocs,
+                           ctx->syn_blkbytes.as<uint64_t>(), s))
+        return TFIDF_E_HIP;
+    if (scan_excl_u64(ctx->syn_blkbytes.as<uint64_t>(), ctx->syn_blkbytes.as<uint64_t>(), nb, ctx->arena, s))
+        return TFIDF_E_HIP;
+    uint64_t total = 0;
+    HIPCHK(hipMemcpyAsync(&total, ctx->syn_blkbytes.as<uint64_t>() + nb, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    ENSURE(ctx->syn_bytes, total + 64);
+    if (launch_synth_fill(&sp, dids, ctx->syn_ntok.as<uint64_t>(), ctx->syn_blkfirst.as<uint64_t>(), nb, ndocs,
+                          ctx->syn_blkbytes.as<uint64_t>(), ctx->syn_bytes.as<uint8_t>(), ctx->syn_off.as<uint64_t>(), s))
+        return TFIDF_E_HIP;
+    HIPCHK(hipStreamSynchronize(s));
+    memset(out, 0, sizeof(*out));
+    out->bytes = ctx->syn_bytes.as<uint8_t>();
+    out->nbytes = total;
+    out->doc_off = ctx->syn_off.as<uint64_t>();
+    out->doc_ids = dids;
+    out->ndocs = ndocs;
+    out->flags = TFIDF_CORPUS_DEVICE;
+    out->ndocs_total = ndocs_total ? ndocs_total : ndocs;
+    return TFIDF_OK;
+}

@@ -1,0 +1,489 @@
+/*
+ * finalize.hip — everything after K1 (tokenize + count):
+ *
+ *   vocabulary   compact the HBM hash table, radix-sort the strcmp("word\t") keys,
+ *                rank_of_slot / slot_of_rank                 (replaces TFIDF.c:227-234 joins)
+ *   partials     documents split across flushes/chunks: radix sort on (doc, rank) and
+ *                reduce-by-key into presorted record runs     (TFIDF.c:151-167 semantics)
+ *   DF           histogram of records per term rank: #documents containing the term
+ *                (TFIDF.c:169-188 + CustomReduce TFIDF.c:291-319)
+ *   order+score  documents in "docN@" strcmp order (base-11 keys), terms by rank inside a
+ *                document (LDS bitonic sort), tf = wc/ds, score = tf * idf   (TFIDF.c:202,
+ *                243-245,273)
+ *   multi-GPU    identity-key union + dense DF vector for the RCCL all-reduce
+ *   synthetic    device-side corpus generation (csrc/synth.h)
+ */
+#include "dev_common.h"
+#include "kernels.h"
+#include "synth.h"
+
+namespace {
+constexpr int NT = 256;
+inline unsigned grid_for(uint64_t n, int nt = NT) { return (unsigned)((n + nt - 1) / nt); }
+inline int ok() { return hipGetLastError() == hipSuccess ? 0 : -1; }
+
+__device__ __forceinline__ uint4 u128_from(uint64_t lo, uint64_t hi) {
+    return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+__device__ __forceinline__ bool u128_eq(uint4 a, uint4 b) { return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w; }
+__device__ __forceinline__ bool u128_lt(uint4 a, uint4 b) {
+    if (a.w != b.w) return a.w < b.w;
+    if (a.z != b.z) return a.z < b.z;
+    if (a.y != b.y) return a.y < b.y;
+    return a.x < b.x;
+}
+}  // namespace
+
+/* ------------------------------------------------------------ vocabulary -- */
+
+__global__ void k_vocab_flags(VocabDev v, uint64_t cap, uint32_t* __restrict__ flags) {
+    uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= cap) return;
+    uint4 k = v.keys[s];
+    uint64_t hi = ((uint64_t)k.w << 32) | k.z;
+    flags[s] = (hi != KEY_EMPTY_HI && hi != KEY_PENDING_HI) ? 1u : 0u;
+}
+int launch_vocab_flags(const VocabDev& v, uint64_t cap, uint32_t* flags, hipStream_t s) {
+    k_vocab_flags<<<grid_for(cap), NT, 0, s>>>(v, cap, flags);
+    return ok();
+}
+
+/* sort key = the term's bytes big-endian: short terms "w\t0..", long terms their first 16 bytes */
+__global__ void k_vocab_compact(VocabDev v, uint64_t cap, const uint32_t* __restrict__ dense_of_slot, CorpusDev c,
+                                uint32_t* __restrict__ vslot, uint4* __restrict__ sortkey, uint32_t* __restrict__ seq) {
+    uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= cap) return;
+    uint32_t dn = dense_of_slot[s];
+    if (dense_of_slot[s + 1] == dn) return; /* empty slot */
+    uint4 k = v.keys[s];
+    uint64_t lo = ((uint64_t)k.y << 32) | k.x, hi = ((uint64_t)k.w << 32) | k.z;
+    uint64_t skhi, sklo;
+    if ((hi >> 56) == 0xFFu) {
+        uint64_t rep = v.rep[s], off = rep & 0xFFFFFFFFFFull;
+        uint64_t a = 0, b = 0;
+        for (int i = 0; i < 8; ++i) a = (a << 8) | c.bytes[off + i];
+        for (int i = 8; i < 16; ++i) b = (b << 8) | c.bytes[off + i];
+        skhi = a; sklo = b;
+    } else {
+        skhi = bswap64(lo);
+        sklo = bswap64(hi);
+    }
+    vslot[dn] = (uint32_t)s;
+    sortkey[dn] = u128_from(sklo, skhi);
+    seq[dn] = dn;
+}
+int launch_vocab_compact(const VocabDev& v, uint64_t cap, const uint32_t* dense_of_slot, const CorpusDev& c,
+                         uint32_t* vslot, uint4* sortkey, uint32_t* seq, hipStream_t s) {
+    k_vocab_compact<<<grid_for(cap), NT, 0, s>>>(v, cap, dense_of_slot, c, vslot, sortkey, seq);
+    return ok();
+}
+
+__global__ void k_vocab_rank(const uint32_t* __restrict__ sorted_dense, const uint32_t* __restrict__ vslot, uint32_t V,
+                             uint32_t* __restrict__ rank_of_slot, uint32_t* __restrict__ slot_of_rank) {
+    uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= V) return;
+    uint32_t s = vslot[sorted_dense[r]];
+    rank_of_slot[s] = r;
+    slot_of_rank[r] = s;
+}
+int launch_vocab_rank(const uint32_t* sorted_dense, const uint32_t* vslot, uint32_t V, uint32_t* rank_of_slot,
+                      uint32_t* slot_of_rank, hipStream_t s) {
+    k_vocab_rank<<<grid_for(V), NT, 0, s>>>(sorted_dense, vslot, V, rank_of_slot, slot_of_rank);
+    return ok();
+}
+
+/* long terms sharing their first 16 bytes: order the tie run by full byte compare
+ * (strcmp of "w\t": a word sorts before its extensions unless the next byte < 0x09) */
+__device__ int long_cmp(const CorpusDev& c, uint64_t ra, uint64_t rb) {
+    uint64_t oa = ra & 0xFFFFFFFFFFull, la = ra >> 40, ob = rb & 0xFFFFFFFFFFull, lb = rb >> 40;
+    uint64_t n = la < lb ? la : lb;
+    for (uint64_t i = 0; i < n; ++i) {
+        uint32_t x = c.bytes[oa + i], y = c.bytes[ob + i];
+        if (x != y) return x < y ? -1 : 1;
+    }
+    if (la == lb) return 0;
+    uint32_t nx = la < lb ? 0x09u : c.bytes[oa + n];
+    uint32_t ny = la < lb ? c.bytes[ob + n] : 0x09u;
+    return nx < ny ? -1 : 1;
+}
+__global__ void k_vocab_long_fixup(const uint4* __restrict__ sk, uint32_t* __restrict__ sorted_dense,
+                                   const uint32_t* __restrict__ vslot, VocabDev v, CorpusDev c, uint32_t V) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i + 1 >= V) return;
+    bool head = (i == 0 || !u128_eq(sk[i], sk[i - 1])) && u128_eq(sk[i], sk[i + 1]);
+    if (!head) return;
+    uint32_t e = i + 1;
+    while (e < V && u128_eq(sk[e], sk[i])) ++e;
+    for (uint32_t a = i + 1; a < e; ++a) { /* insertion sort of the tie run */
+        uint32_t x = sorted_dense[a];
+        uint64_t rx = v.rep[vslot[x]];
+        uint32_t b = a;
+        while (b > i && long_cmp(c, v.rep[vslot[sorted_dense[b - 1]]], rx) > 0) {
+            sorted_dense[b] = sorted_dense[b - 1];
+            --b;
+        }
+        sorted_dense[b] = x;
+    }
+}
+int launch_vocab_long_fixup(const uint4* sorted_keys, uint32_t* sorted_dense, const uint32_t* vslot,
+                            const VocabDev& v, const CorpusDev& c, uint32_t V, hipStream_t s) {
+    if (V < 2) return 0;
+    k_vocab_long_fixup<<<grid_for(V), NT, 0, s>>>(sorted_keys, sorted_dense, vslot, v, c, V);
+    return ok();
+}
+
+/* -------------------------------------------------------------- partials -- */
+
+__global__ void k_part_keys(const uint32_t* __restrict__ pdoc, const uint32_t* __restrict__ pslot,
+                            const uint32_t* __restrict__ rank_of_slot, uint64_t n, uint64_t* __restrict__ keys,
+                            uint32_t* __restrict__ seq) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    keys[i] = ((uint64_t)pdoc[i] << 32) | rank_of_slot[pslot[i]];
+    seq[i] = (uint32_t)i;
+}
+int launch_part_keys(const uint32_t* part_doc, const uint32_t* part_slot, const uint32_t* rank_of_slot, uint64_t n,
+                     uint64_t* keys, uint32_t* seq, hipStream_t s) {
+    if (!n) return 0;
+    k_part_keys<<<grid_for(n), NT, 0, s>>>(part_doc, part_slot, rank_of_slot, n, keys, seq);
+    return ok();
+}
+
+__global__ void k_part_heads(const uint64_t* __restrict__ keys, uint64_t n, uint32_t* __restrict__ head) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    head[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
+}
+int launch_part_heads(const uint64_t* keys, uint64_t n, uint32_t* head, hipStream_t s) {
+    if (!n) return 0;
+    k_part_heads<<<grid_for(n), NT, 0, s>>>(keys, n, head);
+    return ok();
+}
+
+__global__ void k_part_merge(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ seq,
+                             const uint32_t* __restrict__ pcnt, const uint32_t* __restrict__ head_pos, uint64_t n,
+                             const uint32_t* __restrict__ slot_of_rank, uint64_t rec_base,
+                             uint32_t* __restrict__ rec_slot, uint32_t* __restrict__ rec_cnt,
+                             uint64_t* __restrict__ doc_recoff, uint8_t* __restrict__ doc_flags) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t k = keys[i];
+    if (i > 0 && keys[i - 1] == k) return;
+    uint32_t sum = 0;
+    for (uint64_t j = i; j < n && keys[j] == k; ++j) sum += pcnt[seq[j]];
+    uint64_t u = rec_base + head_pos[i];
+    rec_slot[u] = slot_of_rank[(uint32_t)k];
+    rec_cnt[u] = sum;
+    uint32_t d = (uint32_t)(k >> 32);
+    if (i == 0 || (uint32_t)(keys[i - 1] >> 32) != d) {
+        doc_recoff[d] = u;
+        doc_flags[d] = DF_PARTIAL | DF_PRESORTED;
+    }
+}
+__global__ void k_part_npairs(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ head_pos, uint64_t n,
+                              uint64_t rec_base, const uint64_t* __restrict__ doc_recoff,
+                              uint32_t* __restrict__ doc_npairs) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t d = (uint32_t)(keys[i] >> 32);
+    if (i + 1 < n && (uint32_t)(keys[i + 1] >> 32) == d) return; /* last record of d */
+    doc_npairs[d] = (uint32_t)(rec_base + head_pos[i] + 1 - doc_recoff[d]);
+}
+int launch_part_merge(const uint64_t* keys, const uint32_t* seq, const uint32_t* part_cnt, const uint32_t* head_pos,
+                      uint64_t n, const uint32_t* slot_of_rank, uint64_t rec_base, uint32_t* rec_slot,
+                      uint32_t* rec_cnt, uint64_t* doc_recoff, uint32_t* doc_npairs, uint8_t* doc_flags,
+                      hipStream_t s) {
+    if (!n) return 0;
+    k_part_merge<<<grid_for(n), NT, 0, s>>>(keys, seq, part_cnt, head_pos, n, slot_of_rank, rec_base, rec_slot,
+                                           rec_cnt, doc_recoff, doc_flags);
+    k_part_npairs<<<grid_for(n), NT, 0, s>>>(keys, head_pos, n, rec_base, doc_recoff, doc_npairs);
+    return ok();
+}
+
+/* -------------------------------------------------------------------- DF -- */
+
+constexpr uint32_t DFH_RECS = 65535;      /* records per workgroup: u16 bins cannot overflow */
+constexpr uint32_t DFH_MAXV = 65536;
+
+__global__ __launch_bounds__(NT) void k_df_hist_lds(const uint32_t* __restrict__ rec_slot, uint64_t nrec,
+                                                    const uint32_t* __restrict__ rank_of_slot, uint32_t V,
+                                                    uint32_t* __restrict__ part /* [grid][V/2 words] */) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t bins[]; /* V/2 words of two u16 counters */
+    const uint32_t W = (V + 1) / 2;
+    for (uint32_t k = threadIdx.x; k < W; k += NT) bins[k] = 0;
+    __syncthreads();
+    uint64_t r0 = (uint64_t)blockIdx.x * DFH_RECS;
+    uint64_t r1 = r0 + DFH_RECS < nrec ? r0 + DFH_RECS : nrec;
+    for (uint64_t i = r0 + threadIdx.x; i < r1; i += NT) {
+        uint32_t r = rank_of_slot[rec_slot[i]];
+        atomicAdd(&bins[r >> 1], 1u << (16 * (r & 1)));
+    }
+    __syncthreads();
+    uint32_t* out = part + (uint64_t)blockIdx.x * W;
+    for (uint32_t k = threadIdx.x; k < W; k += NT) out[k] = bins[k];
+}
+__global__ void k_df_colsum(const uint32_t* __restrict__ part, uint32_t nparts, uint32_t V, uint32_t* __restrict__ df) {
+    uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= V) return;
+    const uint32_t W = (V + 1) / 2;
+    uint32_t sum = 0, sh = 16 * (r & 1);
+    for (uint32_t p = 0; p < nparts; ++p) sum += (part[(uint64_t)p * W + (r >> 1)] >> sh) & 0xFFFFu;
+    df[r] = sum;
+}
+__global__ void k_df_hist_atomic(const uint32_t* __restrict__ rec_slot, uint64_t nrec,
+                                 const uint32_t* __restrict__ rank_of_slot, uint32_t* __restrict__ df) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nrec; i += (uint64_t)gridDim.x * blockDim.x)
+        atomicAdd(&df[rank_of_slot[rec_slot[i]]], 1u);
+}
+int launch_df_hist(const uint32_t* rec_slot, uint64_t nrec, const uint32_t* rank_of_slot, uint32_t V, uint32_t* df,
+                   Arena& ar, hipStream_t s) {
+    if (V == 0) return 0;
+    if (nrec == 0) return hipMemsetAsync(df, 0, (size_t)V * 4, s) == hipSuccess ? 0 : -1;
+    if (V <= DFH_MAXV) {
+        uint32_t nparts = (uint32_t)((nrec + DFH_RECS - 1) / DFH_RECS);
+        uint32_t W = (V + 1) / 2;
+        size_t m = ar.mark();
+        uint32_t* part = (uint32_t*)ar.get((size_t)nparts * W * 4);
+        if (!part) return -2;
+        k_df_hist_lds<<<nparts, NT, (size_t)W * 4, s>>>(rec_slot, nrec, rank_of_slot, V, part);
+        k_df_colsum<<<grid_for(V), NT, 0, s>>>(part, nparts, V, df);
+        ar.release(m);
+        return ok();
+    }
+    if (hipMemsetAsync(df, 0, (size_t)V * 4, s) != hipSuccess) return -1;
+    k_df_hist_atomic<<<2048, NT, 0, s>>>(rec_slot, nrec, rank_of_slot, df);
+    return ok();
+}
+
+/* present[df] = 1 for every df value in use (present sized N+2, pre-zeroed) */
+__global__ void k_df_mark(const uint32_t* __restrict__ df, uint32_t V, uint32_t* __restrict__ present) {
+    uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < V) present[df[r]] = 1u;
+}
+int launch_df_mark(const uint32_t* df, uint32_t V, uint32_t* present, hipStream_t s) {
+    if (!V) return 0;
+    k_df_mark<<<grid_for(V), NT, 0, s>>>(df, V, present);
+    return ok();
+}
+/* vals[k] = k-th distinct df value; present_scan = exclusive scan of present (nvals+1) */
+__global__ void k_df_list(const uint32_t* __restrict__ ps, uint64_t nvals, uint32_t* __restrict__ vals) {
+    uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= nvals) return;
+    if (ps[x + 1] != ps[x]) vals[ps[x]] = (uint32_t)x;
+}
+int launch_df_list(const uint32_t* present_scan, uint64_t nvals, uint32_t* vals, hipStream_t s) {
+    k_df_list<<<grid_for(nvals), NT, 0, s>>>(present_scan, nvals, vals);
+    return ok();
+}
+
+/* ------------------------------------------------------- document order -- */
+
+/* "docN@" strcmp order: decimal digits padded on the right with the value 10 ('@' sorts
+ * after every digit, TFIDF.c:132,245,273), read as a base-11 number. */
+__global__ void k_doc_keys(const uint32_t* __restrict__ ids, uint32_t n, uint64_t* __restrict__ keys,
+                           uint32_t* __restrict__ seq) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t id = ids ? ids[i] : i + 1;
+    uint32_t dg[10];
+    int k = 0;
+    do { dg[k++] = id % 10; id /= 10; } while (id);
+    uint64_t key = 0;
+    for (int p = 0; p < 10; ++p) key = key * 11 + (p < k ? dg[k - 1 - p] : 10u);
+    keys[i] = key;
+    seq[i] = i;
+}
+int launch_doc_keys(const uint32_t* doc_ids, uint32_t ndocs, uint64_t* keys, uint32_t* seq, hipStream_t s) {
+    if (!ndocs) return 0;
+    k_doc_keys<<<grid_for(ndocs), NT, 0, s>>>(doc_ids, ndocs, keys, seq);
+    return ok();
+}
+__global__ void k_gather_npairs(const uint32_t* __restrict__ order, const uint32_t* __restrict__ np, uint32_t n,
+                                uint64_t* __restrict__ out) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = np[order[i]];
+}
+int launch_gather_npairs(const uint32_t* order, const uint32_t* doc_npairs, uint32_t ndocs, uint64_t* out,
+                         hipStream_t s) {
+    if (!ndocs) return 0;
+    k_gather_npairs<<<grid_for(ndocs), NT, 0, s>>>(order, doc_npairs, ndocs, out);
+    return ok();
+}
+
+/* ------------------------------------------------------ score + order (K5) */
+
+constexpr int K5_MAX = 2048;
+
+__device__ __forceinline__ void k5_emit(const K5Args& a, uint64_t o, uint32_t id, uint32_t ds, uint32_t rank,
+                                        uint32_t cnt) {
+    uint32_t df = a.df_of_rank[rank];
+    double idf = a.idf[a.idf_idx[df]];
+    double tf = (double)cnt / (double)ds;  /* TFIDF.c:202 */
+    a.out_doc[o] = id;
+    a.out_term[o] = rank;
+    a.out_cnt[o] = cnt;
+    a.out_docsize[o] = ds;
+    a.out_df[o] = df;
+    a.out_score[o] = tf * idf;             /* TFIDF.c:244 */
+}
+
+__global__ __launch_bounds__(NT) void k_score_order(K5Args a) {
+    __shared__ uint32_t skey[K5_MAX];
+    __shared__ uint32_t sval[K5_MAX];
+    const uint32_t i = blockIdx.x;
+    const uint32_t d = a.order[i];
+    const uint32_t n = a.doc_npairs[d];
+    if (n == 0) return;
+    const uint64_t ob = a.out_off[i], rb = a.doc_recoff[d];
+    const uint32_t ds = a.doc_size[d];
+    const uint32_t id = a.doc_ids ? a.doc_ids[d] : d + 1;
+    if ((a.doc_flags[d] & DF_PRESORTED) || n > (uint32_t)K5_MAX) {
+        for (uint32_t j = threadIdx.x; j < n; j += NT) {
+            uint32_t r = a.rank_of_slot[a.rec_slot[rb + j]];
+            k5_emit(a, ob + j, id, ds, r, a.rec_cnt[rb + j]);
+        }
+        return;
+    }
+    uint32_t P = 1;
+    while (P < n) P <<= 1;
+    for (uint32_t j = threadIdx.x; j < P; j += NT) {
+        if (j < n) { skey[j] = a.rank_of_slot[a.rec_slot[rb + j]]; sval[j] = a.rec_cnt[rb + j]; }
+        else { skey[j] = 0xFFFFFFFFu; sval[j] = 0; }
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            for (uint32_t t = threadIdx.x; t < P; t += NT) {
+                uint32_t p = t ^ jj;
+                if (p > t) {
+                    bool up = (t & k) == 0;
+                    uint32_t x = skey[t], y = skey[p];
+                    if ((x > y) == up) {
+                        skey[t] = y; skey[p] = x;
+                        uint32_t tv = sval[t]; sval[t] = sval[p]; sval[p] = tv;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t j = threadIdx.x; j < n; j += NT) k5_emit(a, ob + j, id, ds, skey[j], sval[j]);
+}
+int launch_score_order(const K5Args& a, hipStream_t s) {
+    if (!a.ndocs) return 0;
+    k_score_order<<<a.ndocs, NT, 0, s>>>(a);
+    return ok();
+}
+
+/* ------------------------------------------------------ multi-GPU union -- */
+
+__global__ void k_keys_by_rank(const uint4* __restrict__ vkeys, const uint32_t* __restrict__ slot_of_rank, uint32_t V,
+                               uint4* __restrict__ out) {
+    uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < V) out[r] = vkeys[slot_of_rank[r]];
+}
+int launch_keys_by_rank(const uint4* vkeys, const uint32_t* slot_of_rank, uint32_t V, uint4* out, hipStream_t s) {
+    if (!V) return 0;
+    k_keys_by_rank<<<grid_for(V), NT, 0, s>>>(vkeys, slot_of_rank, V, out);
+    return ok();
+}
+__global__ void k_union_heads(const uint4* __restrict__ k, uint64_t n, uint32_t* __restrict__ head) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) head[i] = (i == 0 || !u128_eq(k[i], k[i - 1])) ? 1u : 0u;
+}
+int launch_union_heads(const uint4* sorted, uint64_t n, uint32_t* head, hipStream_t s) {
+    if (!n) return 0;
+    k_union_heads<<<grid_for(n), NT, 0, s>>>(sorted, n, head);
+    return ok();
+}
+/* grank[r] = dense union id of my key r: binary search in the sorted union (with
+ * duplicates), id = exclusive head scan at the first match */
+__global__ void k_union_lookup(const uint4* __restrict__ mine, uint32_t V, const uint4* __restrict__ u,
+                               const uint32_t* __restrict__ hscan, uint64_t nu, uint32_t* __restrict__ grank) {
+    uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= V) return;
+    uint4 k = mine[r];
+    uint64_t lo = 0, hi = nu;
+    while (lo < hi) {
+        uint64_t mid = (lo + hi) >> 1;
+        if (u128_lt(u[mid], k)) lo = mid + 1; else hi = mid;
+    }
+    grank[r] = hscan[lo];
+}
+int launch_union_lookup(const uint4* my_keys, uint32_t V, const uint4* ukeys, const uint32_t* hscan,
+                        uint64_t nu_sorted, const uint32_t* head, uint32_t* grank, hipStream_t s) {
+    (void)head;
+    if (!V) return 0;
+    k_union_lookup<<<grid_for(V), NT, 0, s>>>(my_keys, V, ukeys, hscan, nu_sorted, grank);
+    return ok();
+}
+__global__ void k_scatter_df(const uint32_t* __restrict__ df, const uint32_t* __restrict__ grank, uint32_t V,
+                             uint32_t* __restrict__ dfv) {
+    uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < V) dfv[grank[r]] = df[r];
+}
+__global__ void k_gather_df(const uint32_t* __restrict__ dfv, const uint32_t* __restrict__ grank, uint32_t V,
+                            uint32_t* __restrict__ out) {
+    uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < V) out[r] = dfv[grank[r]];
+}
+int launch_scatter_df(const uint32_t* df_local, const uint32_t* grank, uint32_t V, uint32_t* dfv, hipStream_t s) {
+    if (!V) return 0;
+    k_scatter_df<<<grid_for(V), NT, 0, s>>>(df_local, grank, V, dfv);
+    return ok();
+}
+int launch_gather_df(const uint32_t* dfv, const uint32_t* grank, uint32_t V, uint32_t* df_out, hipStream_t s) {
+    if (!V) return 0;
+    k_gather_df<<<grid_for(V), NT, 0, s>>>(dfv, grank, V, df_out);
+    return ok();
+}
+
+/* ------------------------------------------------------------- synthetic -- */
+
+__device__ __forceinline__ uint32_t blk_doc(const uint64_t* blk_first, uint32_t ndocs, uint64_t b) {
+    uint32_t lo = 0, hi = ndocs + 1; /* last i with blk_first[i] <= b */
+    while (lo < hi) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (blk_first[mid] <= b) lo = mid + 1; else hi = mid;
+    }
+    return lo - 1;
+}
+__global__ void k_synth_bytes(syn_spec sp, const uint32_t* __restrict__ ids, const uint64_t* __restrict__ ntok,
+                              const uint64_t* __restrict__ blk_first, uint64_t nblocks, uint32_t ndocs,
+                              uint64_t* __restrict__ out) {
+    uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblocks) return;
+    uint32_t i = blk_doc(blk_first, ndocs, b);
+    uint64_t id = ids ? ids[i] : (uint64_t)i + 1;
+    out[b] = syn_block_bytes(&sp, id, ntok[i], b - blk_first[i]);
+}
+__global__ void k_synth_fill(syn_spec sp, const uint32_t* __restrict__ ids, const uint64_t* __restrict__ ntok,
+                             const uint64_t* __restrict__ blk_first, uint64_t nblocks, uint32_t ndocs,
+                             const uint64_t* __restrict__ blk_off, uint8_t* __restrict__ bytes) {
+    uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblocks) return;
+    uint32_t i = blk_doc(blk_first, ndocs, b);
+    uint64_t id = ids ? ids[i] : (uint64_t)i + 1;
+    syn_block_fill(&sp, id, ntok[i], b - blk_first[i], bytes + blk_off[b]);
+}
+__global__ void k_synth_docoff(const uint64_t* __restrict__ blk_first, uint32_t ndocs,
+                               const uint64_t* __restrict__ blk_off, uint64_t* __restrict__ doc_off) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= ndocs) doc_off[i] = blk_off[blk_first[i]];
+}
+int launch_synth_bytes(const void* spec, const uint32_t* doc_ids, const uint64_t* ntok, const uint64_t* blk_first,
+                       uint64_t nblocks, uint32_t ndocs, uint64_t* blk_bytes, hipStream_t s) {
+    if (!nblocks) return 0;
+    k_synth_bytes<<<grid_for(nblocks, 64), 64, 0, s>>>(*(const syn_spec*)spec, doc_ids, ntok, blk_first, nblocks,
+                                                      ndocs, blk_bytes);
+    return ok();
+}
+int launch_synth_fill(const void* spec, const uint32_t* doc_ids, const uint64_t* ntok, const uint64_t* blk_first,
+                      uint64_t nblocks, uint32_t ndocs, const uint64_t* blk_off, uint8_t* bytes, uint64_t* doc_off,
+                      hipStream_t s) {
+    if (nblocks)
+        k_synth_fill<<<grid_for(nblocks, 64), 64, 0, s>>>(*(const syn_spec*)spec, doc_ids, ntok, blk_first, nblocks,
+                                                         ndocs, blk_off, bytes);
+    k_synth_docoff<<<grid_for((uint64_t)ndocs + 1), NT, 0, s>>>(blk_first, ndocs, blk_off, doc_off);
+    return ok();
+}

@@ -1,0 +1,135 @@
+/* kernels.h — parameter blocks and host launchers of the TF-IDF path kernels. */
+#ifndef TFIDF_KERNELS_H
+#define TFIDF_KERNELS_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "prims.h"
+
+/* chunking (K0/K1) */
+#define K1_NT        256                 /* threads per tokenize+count workgroup */
+#define K1_WIN       (K1_NT * 16)        /* bytes per window: one 16-byte group per thread */
+#define CHUNK_BYTES  16384u              /* nominal chunk (work unit) size */
+#define BIG_DOC      65536u              /* documents longer than this are split across chunks */
+
+/* status bits (device word) */
+#define ST_VOCAB_FULL  1u
+#define ST_VOCAB_SPIN  2u
+#define ST_REC_FULL    4u
+#define ST_PART_FULL   8u
+
+/* doc flags */
+#define DF_PARTIAL     1u
+#define DF_PRESORTED   2u
+
+#define INVALID_SLOT   0xFFFFFFFFu
+
+struct CorpusDev {
+    const uint8_t* bytes;
+    uint64_t nbytes;
+    const uint64_t* doc_off;   /* ndocs + 1 */
+    uint32_t ndocs;
+    uint64_t lo, hi;           /* doc_off[0], doc_off[ndocs] (host-known) */
+};
+
+struct VocabDev {
+    uint4* keys;               /* cap identity keys (see dev_common.h) */
+    uint64_t* rep;             /* long terms: (len << 40) | byte offset */
+    uint64_t mask;             /* cap - 1 */
+};
+
+struct K1Out {
+    uint32_t* rec_slot;        /* complete documents' (term slot, count) records */
+    uint32_t* rec_cnt;
+    unsigned long long* rec_alloc;
+    uint64_t rec_cap;
+    uint32_t* part_doc;        /* records of documents split across flushes/chunks */
+    uint32_t* part_slot;
+    uint32_t* part_cnt;
+    unsigned long long* part_alloc;
+    uint64_t part_cap;
+    uint64_t* doc_recoff;
+    uint32_t* doc_npairs;
+    uint32_t* doc_size;
+    uint8_t* doc_flags;
+    uint32_t* status;
+    unsigned long long* ntokens;
+};
+
+/* K0: chunk boundaries; chunk_start has nchunks+1 entries, chunk_doc nchunks */
+int launch_plan_chunks(const CorpusDev& c, uint64_t nchunks, uint64_t* chunk_start, uint32_t* chunk_doc,
+                       hipStream_t s);
+/* K1: tokenize + per-document term counts for chunks [c0, c1) */
+int launch_tokcount(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc,
+                    uint64_t c0, uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s);
+
+/* vocabulary finalisation */
+int launch_vocab_flags(const VocabDev& v, uint64_t cap, uint32_t* flags, hipStream_t s);
+int launch_vocab_compact(const VocabDev& v, uint64_t cap, const uint32_t* dense_of_slot, const CorpusDev& c,
+                         uint32_t* vslot, uint4* sortkey, uint32_t* seq, hipStream_t s);
+int launch_vocab_rank(const uint32_t* sorted_dense, const uint32_t* vslot, uint32_t V, uint32_t* rank_of_slot,
+                      uint32_t* slot_of_rank, hipStream_t s);
+int launch_vocab_long_fixup(const uint4* sorted_keys, uint32_t* sorted_dense, const uint32_t* vslot,
+                            const VocabDev& v, const CorpusDev& c, uint32_t V, hipStream_t s);
+
+/* partial documents: sort key (doc << 32 | rank) and merge */
+int launch_part_keys(const uint32_t* part_doc, const uint32_t* part_slot, const uint32_t* rank_of_slot, uint64_t n,
+                     uint64_t* keys, uint32_t* seq, hipStream_t s);
+int launch_part_heads(const uint64_t* keys, uint64_t n, uint32_t* head, hipStream_t s);
+int launch_part_merge(const uint64_t* keys, const uint32_t* seq, const uint32_t* part_cnt, const uint32_t* head_pos,
+                      uint64_t n, const uint32_t* slot_of_rank, uint64_t rec_base, uint32_t* rec_slot,
+                      uint32_t* rec_cnt, uint64_t* doc_recoff, uint32_t* doc_npairs, uint8_t* doc_flags,
+                      hipStream_t s);
+
+/* DF */
+int launch_df_hist(const uint32_t* rec_slot, uint64_t nrec, const uint32_t* rank_of_slot, uint32_t V,
+                   uint32_t* df, Arena& ar, hipStream_t s);
+int launch_df_mark(const uint32_t* df, uint32_t V, uint32_t* present, hipStream_t s);
+int launch_df_list(const uint32_t* present_scan, uint64_t nvals, uint32_t* vals, hipStream_t s);
+
+/* documents: name order key and output */
+int launch_doc_keys(const uint32_t* doc_ids, uint32_t ndocs, uint64_t* keys, uint32_t* seq, hipStream_t s);
+int launch_gather_npairs(const uint32_t* order, const uint32_t* doc_npairs, uint32_t ndocs, uint64_t* out,
+                         hipStream_t s);
+struct K5Args {
+    const uint32_t* order;       /* docs in output order */
+    const uint64_t* out_off;     /* per output position */
+    const uint64_t* doc_recoff;
+    const uint32_t* doc_npairs;
+    const uint32_t* doc_size;
+    const uint8_t* doc_flags;
+    const uint32_t* doc_ids;     /* NULL: 1..ndocs */
+    const uint32_t* rec_slot;
+    const uint32_t* rec_cnt;
+    const uint32_t* rank_of_slot;
+    const uint32_t* df_of_rank;  /* global df */
+    const uint32_t* idf_idx;     /* df value -> index into idf */
+    const double* idf;
+    uint32_t ndocs;
+    uint32_t* out_doc;
+    uint32_t* out_term;
+    uint32_t* out_cnt;
+    uint32_t* out_docsize;
+    uint32_t* out_df;
+    double* out_score;
+};
+int launch_score_order(const K5Args& a, hipStream_t s);
+
+/* multi-GPU vocabulary agreement */
+int launch_keys_by_rank(const uint4* vkeys, const uint32_t* slot_of_rank, uint32_t V, uint4* out, hipStream_t s);
+int launch_union_heads(const uint4* sorted, uint64_t n, uint32_t* head, hipStream_t s);
+int launch_union_lookup(const uint4* my_keys, uint32_t V, const uint4* ukeys, const uint32_t* useq_head_scan,
+                        uint64_t nu_sorted, const uint32_t* head, uint32_t* grank, hipStream_t s);
+int launch_scatter_df(const uint32_t* df_local, const uint32_t* grank, uint32_t V, uint32_t* dfv, hipStream_t s);
+int launch_gather_df(const uint32_t* dfv, const uint32_t* grank, uint32_t V, uint32_t* df_out, hipStream_t s);
+
+/* synthetic corpus generation on the device */
+struct SynSpecDev;
+int launch_synth_bytes(const void* spec, const uint32_t* doc_ids, const uint64_t* ntok, const uint64_t* blk_first,
+                       uint64_t nblocks, uint32_t ndocs, uint64_t* blk_bytes, hipStream_t s);
+int launch_synth_fill(const void* spec, const uint32_t* doc_ids, const uint64_t* ntok, const uint64_t* blk_first,
+                      uint64_t nblocks, uint32_t ndocs, const uint64_t* blk_off, uint8_t* bytes, uint64_t* doc_off,
+                      hipStream_t s);
+
+#endif

@@ -1,0 +1,285 @@
+/*
+ * prims.hip — device-wide primitives for the TF-IDF path (gfx950, wave64):
+ *   exclusive scan (u32/u64), LSD radix sort of (u64|u128 key, u32 value) pairs with
+ *   8-bit digits and a stable wave64 multisplit (8 ballots per digit), and the
+ *   varying-byte probe that lets callers skip constant digit passes.
+ */
+#include "prims.h"
+#include "dev_common.h"
+
+namespace {
+
+constexpr int SC_NT = 256;
+constexpr int SC_IT = 8;
+constexpr int SC_TILE = SC_NT * SC_IT;
+
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan_t(T v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        T t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T block_excl_scan_t(T v, T* wsum, T* total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    T inc = wave_incl_scan_t(v);
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    T base = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < SC_NT / 64; ++k) {
+        T s = wsum[k];
+        base += (k < w) ? s : (T)0;
+        tot += s;
+    }
+    *total = tot;
+    __syncthreads();
+    return base + inc - v;
+}
+
+template <typename T>
+__global__ __launch_bounds__(SC_NT) void k_scan_reduce(const T* __restrict__ in, uint64_t n, T* __restrict__ bsum) {
+    __shared__ T wsum[SC_NT / 64];
+    uint64_t base = (uint64_t)blockIdx.x * SC_TILE + (uint64_t)threadIdx.x * SC_IT;
+    T s = 0;
+#pragma unroll
+    for (int j = 0; j < SC_IT; ++j)
+        if (base + j < n) s += in[base + j];
+    T tot;
+    (void)block_excl_scan_t<T>(s, wsum, &tot);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+template <typename T>
+__global__ __launch_bounds__(SC_NT) void k_scan_apply(const T* in, T* out, uint64_t n, const T* __restrict__ boff) {
+    __shared__ T wsum[SC_NT / 64];
+    uint64_t base = (uint64_t)blockIdx.x * SC_TILE + (uint64_t)threadIdx.x * SC_IT;
+    T v[SC_IT];
+    T s = 0;
+#pragma unroll
+    for (int j = 0; j < SC_IT; ++j) {
+        v[j] = (base + j < n) ? in[base + j] : (T)0;
+        s += v[j];
+    }
+    T tot;
+    T run = block_excl_scan_t<T>(s, wsum, &tot) + (boff ? boff[blockIdx.x] : (T)0);
+#pragma unroll
+    for (int j = 0; j < SC_IT; ++j) {
+        if (base + j < n) out[base + j] = run;
+        run += v[j];
+        if (base + j + 1 == n) out[n] = run;
+    }
+}
+
+template <typename T>
+int scan_excl_t(const T* in, T* out, uint64_t n, Arena& ar, hipStream_t s) {
+    if (n == 0) return hipMemsetAsync(out, 0, sizeof(T), s) == hipSuccess ? 0 : -1;
+    uint64_t nb = (n + SC_TILE - 1) / SC_TILE;
+    if (nb == 1) {
+        k_scan_apply<T><<<1, SC_NT, 0, s>>>(in, out, n, nullptr);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+    size_t m = ar.mark();
+    T* bsum = (T*)ar.get((nb + 1) * sizeof(T));
+    if (!bsum) return -2;
+    k_scan_reduce<T><<<(unsigned)nb, SC_NT, 0, s>>>(in, n, bsum);
+    int rc = scan_excl_t<T>(bsum, bsum, nb, ar, s);
+    if (rc) return rc;
+    k_scan_apply<T><<<(unsigned)nb, SC_NT, 0, s>>>(in, out, n, bsum);
+    ar.release(m);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+/* ------------------------------------------------------------ radix sort ---- */
+
+constexpr int RS_NT = 256;
+constexpr int RS_IT = 8;
+constexpr int RS_TILE = RS_NT * RS_IT;
+
+__device__ __forceinline__ uint32_t digit_of(uint64_t k, int p) { return (uint32_t)(k >> (8 * p)) & 0xFFu; }
+__device__ __forceinline__ uint32_t digit_of(uint4 k, int p) {
+    uint32_t w = (p < 4) ? k.x : (p < 8) ? k.y : (p < 12) ? k.z : k.w;
+    return (w >> (8 * (p & 3))) & 0xFFu;
+}
+
+template <typename K>
+__global__ __launch_bounds__(RS_NT) void k_rs_hist(const K* __restrict__ keys, uint64_t n, int p,
+                                                  uint32_t* __restrict__ hist, uint32_t nblocks) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    uint64_t base = (uint64_t)blockIdx.x * RS_TILE + threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < RS_IT; ++j) {
+        uint64_t idx = base + (uint64_t)j * RS_NT;
+        if (idx < n) atomicAdd(&h[digit_of(keys[idx], p)], 1u);
+    }
+    __syncthreads();
+    hist[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+}
+
+template <typename K>
+__global__ __launch_bounds__(RS_NT) void k_rs_scatter(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                     K* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                     uint64_t n, int p, const uint32_t* __restrict__ offs,
+                                                     uint32_t nblocks) {
+    __shared__ uint32_t run[256];
+    __shared__ uint32_t boff[256];
+    __shared__ uint32_t wcnt[RS_NT / 64][256];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    run[tid] = 0;
+    boff[tid] = offs[(uint64_t)tid * nblocks + blockIdx.x];
+#pragma unroll
+    for (int q = 0; q < RS_NT / 64; ++q) wcnt[q][tid] = 0;
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint64_t base = (uint64_t)blockIdx.x * RS_TILE + tid;
+    for (int j = 0; j < RS_IT; ++j) {
+        uint64_t idx = base + (uint64_t)j * RS_NT;
+        bool valid = idx < n;
+        K k{};
+        uint32_t v = 0, d = 0;
+        if (valid) { k = kin[idx]; v = vin[idx]; d = digit_of(k, p); }
+        uint64_t m = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            bool bit = (d >> b) & 1u;
+            uint64_t bb = __ballot(valid && bit);
+            m &= bit ? bb : ~bb;
+        }
+        uint32_t lrank = (uint32_t)__popcll(m & lt);
+        if (valid && lrank == 0) wcnt[w][d] = (uint32_t)__popcll(m);
+        __syncthreads();
+        if (valid) {
+            uint32_t pre = run[d] + lrank;
+            for (int q = 0; q < w; ++q) pre += wcnt[q][d];
+            uint32_t o = boff[d] + pre;
+            kout[o] = k;
+            vout[o] = v;
+        }
+        __syncthreads();
+        uint32_t add = 0;
+#pragma unroll
+        for (int q = 0; q < RS_NT / 64; ++q) { add += wcnt[q][tid]; wcnt[q][tid] = 0; }
+        run[tid] += add;
+        __syncthreads();
+    }
+}
+
+template <typename K>
+int radix_sort_t(K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t n, uint32_t byte_mask, int nbytes,
+                 Arena& ar, hipStream_t s) {
+    if (n <= 1 || byte_mask == 0) return 0;
+    if (n > 0xFFFFFFFFull) return -3;
+    uint32_t nb = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+    size_t m = ar.mark();
+    uint32_t* hist = (uint32_t*)ar.get(((uint64_t)256 * nb + 1) * sizeof(uint32_t));
+    if (!hist) return -2;
+    int cur = 0;
+    for (int p = 0; p < nbytes; ++p) {
+        if (!((byte_mask >> p) & 1u)) continue;
+        K* ki = cur ? k1 : k0;
+        uint32_t* vi = cur ? v1 : v0;
+        K* ko = cur ? k0 : k1;
+        uint32_t* vo = cur ? v0 : v1;
+        k_rs_hist<K><<<nb, RS_NT, 0, s>>>(ki, n, p, hist, nb);
+        int rc = scan_excl_t<uint32_t>(hist, hist, (uint64_t)256 * nb, ar, s);
+        if (rc) return rc;
+        k_rs_scatter<K><<<nb, RS_NT, 0, s>>>(ki, vi, ko, vo, n, p, hist, nb);
+        cur ^= 1;
+    }
+    ar.release(m);
+    return hipGetLastError() == hipSuccess ? cur : -1;
+}
+
+__global__ void k_orand_u64(const uint64_t* __restrict__ k, uint64_t n, unsigned long long* acc) {
+    uint64_t a = ~0ull, o = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        a &= k[i];
+        o |= k[i];
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        a &= __shfl_xor(a, off, 64);
+        o |= __shfl_xor(o, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) { atomicAnd(&acc[0], a); atomicOr(&acc[1], o); }
+}
+
+__global__ void k_orand_u128(const uint4* __restrict__ k, uint64_t n, unsigned long long* acc) {
+    uint64_t a0 = ~0ull, a1 = ~0ull, o0 = 0, o1 = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint4 v = k[i];
+        uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
+        a0 &= lo; a1 &= hi; o0 |= lo; o1 |= hi;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        a0 &= __shfl_xor(a0, off, 64); a1 &= __shfl_xor(a1, off, 64);
+        o0 |= __shfl_xor(o0, off, 64); o1 |= __shfl_xor(o1, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAnd(&acc[0], a0); atomicAnd(&acc[1], a1);
+        atomicOr(&acc[2], o0); atomicOr(&acc[3], o1);
+    }
+}
+
+}  // namespace
+
+int scan_excl_u32(const uint32_t* in, uint32_t* out, uint64_t n, Arena& ar, hipStream_t s) {
+    return scan_excl_t<uint32_t>(in, out, n, ar, s);
+}
+int scan_excl_u64(const uint64_t* in, uint64_t* out, uint64_t n, Arena& ar, hipStream_t s) {
+    return scan_excl_t<uint64_t>(in, out, n, ar, s);
+}
+int radix_sort_u64(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, uint64_t n, uint32_t byte_mask,
+                   Arena& ar, hipStream_t s) {
+    return radix_sort_t<uint64_t>(k0, v0, k1, v1, n, byte_mask, 8, ar, s);
+}
+int radix_sort_u128(uint4* k0, uint32_t* v0, uint4* k1, uint32_t* v1, uint64_t n, uint32_t byte_mask,
+                    Arena& ar, hipStream_t s) {
+    return radix_sort_t<uint4>(k0, v0, k1, v1, n, byte_mask, 16, ar, s);
+}
+
+static int varying_common(int words, const void* k, uint64_t n, uint32_t* mask, Arena& ar, hipStream_t s) {
+    size_t m = ar.mark();
+    unsigned long long* acc = (unsigned long long*)ar.get(4 * sizeof(unsigned long long));
+    if (!acc) return -2;
+    unsigned long long init[4] = {~0ull, ~0ull, 0ull, 0ull};
+    if (words == 1) { init[1] = 0ull; }
+    if (hipMemcpyAsync(acc, init, sizeof init, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
+    unsigned grid = (unsigned)((n + 255) / 256);
+    if (grid > 1024) grid = 1024;
+    if (grid == 0) grid = 1;
+    if (words == 1) k_orand_u64<<<grid, 256, 0, s>>>((const uint64_t*)k, n, acc);
+    else k_orand_u128<<<grid, 256, 0, s>>>((const uint4*)k, n, acc);
+    unsigned long long h[4];
+    if (hipMemcpyAsync(h, acc, sizeof h, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
+    if (hipStreamSynchronize(s) != hipSuccess) return -1;
+    ar.release(m);
+    uint32_t msk = 0;
+    if (words == 1) {
+        uint64_t x = h[0] ^ h[1];
+        for (int p = 0; p < 8; ++p) if ((x >> (8 * p)) & 0xFF) msk |= 1u << p;
+    } else {
+        uint64_t x0 = h[0] ^ h[2], x1 = h[1] ^ h[3];
+        for (int p = 0; p < 8; ++p) {
+            if ((x0 >> (8 * p)) & 0xFF) msk |= 1u << p;
+            if ((x1 >> (8 * p)) & 0xFF) msk |= 1u << (p + 8);
+        }
+    }
+    *mask = msk;
+    return 0;
+}
+
+int key_varying_bytes_u64(const uint64_t* k, uint64_t n, uint32_t* mask, Arena& ar, hipStream_t s) {
+    if (n == 0) { *mask = 0; return 0; }
+    return varying_common(1, k, n, mask, ar, s);
+}
+int key_varying_bytes_u128(const uint4* k, uint64_t n, uint32_t* mask, Arena& ar, hipStream_t s) {
+    if (n == 0) { *mask = 0; return 0; }
+    return varying_common(2, k, n, mask, ar, s);
+}

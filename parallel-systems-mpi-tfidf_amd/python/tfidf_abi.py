@@ -1,0 +1,220 @@
+"""ctypes binding of include/tfidf.h (libtfidf_hip.so).
+
+Plumbing for tests and bench.py: every compute call goes through the C-ABI into the
+gfx950 HIP kernels.  Loading fails loudly when the library has not been built; there is
+no Python or CPU fallback for any stage.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libtfidf_hip.so")
+CLI_PATH = os.path.join(PKG_DIR, "bin", "tfidf")
+
+TFIDF_CORPUS_DEVICE = 1
+UNIQUE_ID_BYTES = 128
+
+# exported symbols declared by include/tfidf.h
+EXPORTS = [
+    "tfidf_open", "tfidf_close", "tfidf_strerror", "tfidf_abi_version", "tfidf_comm_unique_id",
+    "tfidf_comm_init", "tfidf_run", "tfidf_fetch", "tfidf_result_free", "tfidf_last_run_info",
+    "tfidf_stage_name", "tfidf_set_timing", "tfidf_write_output", "tfidf_print_jobs",
+    "tfidf_ingest_dir", "tfidf_free", "tfidf_synth_host", "tfidf_synth_device",
+]
+
+
+class Corpus(C.Structure):
+    _fields_ = [
+        ("bytes", C.c_void_p), ("nbytes", C.c_uint64), ("doc_off", C.c_void_p), ("doc_ids", C.c_void_p),
+        ("ndocs", C.c_uint32), ("flags", C.c_uint32), ("ndocs_total", C.c_uint64),
+    ]
+
+
+class Result(C.Structure):
+    _fields_ = [
+        ("npairs", C.c_uint64), ("ndocs", C.c_uint32), ("nterms", C.c_uint32), ("ndocs_total", C.c_uint64),
+        ("pair_doc", C.POINTER(C.c_uint32)), ("pair_term", C.POINTER(C.c_uint32)),
+        ("pair_count", C.POINTER(C.c_uint32)), ("pair_docsize", C.POINTER(C.c_uint32)),
+        ("pair_df", C.POINTER(C.c_uint32)), ("pair_score", C.POINTER(C.c_double)),
+        ("doc_id", C.POINTER(C.c_uint32)), ("doc_size", C.POINTER(C.c_uint32)),
+        ("term_off", C.POINTER(C.c_uint64)), ("term_bytes", C.POINTER(C.c_uint8)),
+        ("term_df", C.POINTER(C.c_uint32)),
+    ]
+
+
+class RunInfo(C.Structure):
+    _fields_ = [
+        ("nbytes", C.c_uint64), ("ntokens", C.c_uint64), ("npairs", C.c_uint64), ("nterms", C.c_uint32),
+        ("nterms_global", C.c_uint32), ("nchunks", C.c_uint64), ("partial_records", C.c_uint64),
+        ("ndocs", C.c_uint32), ("vocab_capacity", C.c_uint32), ("ms_total", C.c_double),
+        ("ms_tokcount", C.c_double), ("ms_stage", C.c_double * 16), ("nstages", C.c_uint32), ("pad_", C.c_uint32),
+    ]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libtfidf_hip.so not built ({LIB_PATH}); run __graft_entry__.build()")
+        L = C.CDLL(LIB_PATH)
+        L.tfidf_open.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+        L.tfidf_close.argtypes = [C.c_void_p]
+        L.tfidf_close.restype = None
+        L.tfidf_strerror.restype = C.c_char_p
+        L.tfidf_run.argtypes = [C.c_void_p, C.POINTER(Corpus)]
+        L.tfidf_fetch.argtypes = [C.c_void_p, C.POINTER(Result)]
+        L.tfidf_result_free.argtypes = [C.POINTER(Result)]
+        L.tfidf_result_free.restype = None
+        L.tfidf_last_run_info.argtypes = [C.c_void_p, C.POINTER(RunInfo)]
+        L.tfidf_stage_name.restype = C.c_char_p
+        L.tfidf_set_timing.argtypes = [C.c_void_p, C.c_int]
+        L.tfidf_comm_unique_id.argtypes = [C.c_void_p]
+        L.tfidf_comm_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+        L.tfidf_write_output.argtypes = [C.POINTER(Result), C.c_char_p]
+        L.tfidf_synth_host.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_uint32, C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p]
+        L.tfidf_synth_device.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.c_uint32, C.c_uint64, C.POINTER(Corpus)]
+        _lib = L
+    return _lib
+
+
+class TfidfError(RuntimeError):
+    def __init__(self, rc: int, what: str):
+        super().__init__(f"{what}: {lib().tfidf_strerror(rc).decode()} ({rc})")
+        self.rc = rc
+
+
+def _chk(rc: int, what: str) -> None:
+    if rc != 0:
+        raise TfidfError(rc, what)
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def synth_host(seed: int, V: int, mode: int, cdf, doc_ids, ntok):
+    """Host generation (csrc/synth.h).  Returns (bytes uint8, doc_off uint64)."""
+    ntok = np.ascontiguousarray(ntok, dtype=np.uint64)
+    ids = None if doc_ids is None else np.ascontiguousarray(doc_ids, dtype=np.uint32)
+    cdf = None if cdf is None else np.ascontiguousarray(cdf, dtype=np.float64)
+    n = C.c_uint64(0)
+    _chk(lib().tfidf_synth_host(seed, V, mode, _ptr(cdf), _ptr(ids), _ptr(ntok), len(ntok), None, C.byref(n), None),
+         "synth size")
+    buf = np.empty(max(int(n.value), 1), dtype=np.uint8)
+    off = np.empty(len(ntok) + 1, dtype=np.uint64)
+    _chk(lib().tfidf_synth_host(seed, V, mode, _ptr(cdf), _ptr(ids), _ptr(ntok), len(ntok), _ptr(buf), C.byref(n),
+                                _ptr(off)), "synth")
+    return buf[: int(n.value)], off
+
+
+class Engine:
+    """One GPU context (one HIP stream; optional RCCL communicator)."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        _chk(lib().tfidf_open(device, C.byref(h)), "tfidf_open")
+        self.h = h
+        self._keep = None
+
+    def close(self):
+        if self.h:
+            lib().tfidf_close(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def set_timing(self, on: bool):
+        _chk(lib().tfidf_set_timing(self.h, 1 if on else 0), "set_timing")
+
+    def comm_init(self, uid: bytes, rank: int, nranks: int):
+        buf = (C.c_uint8 * UNIQUE_ID_BYTES).from_buffer_copy(uid)
+        _chk(lib().tfidf_comm_init(self.h, buf, rank, nranks), "tfidf_comm_init")
+
+    def run_host(self, data: np.ndarray, doc_off: np.ndarray, doc_ids=None, ndocs_total: int = 0):
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        doc_off = np.ascontiguousarray(doc_off, dtype=np.uint64)
+        ids = None if doc_ids is None else np.ascontiguousarray(doc_ids, dtype=np.uint32)
+        c = Corpus()
+        c.bytes = data.ctypes.data if len(data) else None
+        c.nbytes = len(data)
+        c.doc_off = doc_off.ctypes.data
+        c.doc_ids = None if ids is None else ids.ctypes.data
+        c.ndocs = len(doc_off) - 1
+        c.flags = 0
+        c.ndocs_total = ndocs_total
+        self._keep = (data, doc_off, ids)
+        _chk(lib().tfidf_run(self.h, C.byref(c)), "tfidf_run")
+
+    def run_corpus(self, c: Corpus):
+        _chk(lib().tfidf_run(self.h, C.byref(c)), "tfidf_run")
+
+    def synth_device(self, seed, V, mode, cdf, doc_ids, ntok, ndocs_total=0) -> Corpus:
+        ntok = np.ascontiguousarray(ntok, dtype=np.uint64)
+        ids = None if doc_ids is None else np.ascontiguousarray(doc_ids, dtype=np.uint32)
+        cdf = None if cdf is None else np.ascontiguousarray(cdf, dtype=np.float64)
+        c = Corpus()
+        _chk(lib().tfidf_synth_device(self.h, seed, V, mode, _ptr(cdf), _ptr(ids), _ptr(ntok), len(ntok),
+                                      ndocs_total, C.byref(c)), "tfidf_synth_device")
+        return c
+
+    def info(self) -> dict:
+        r = RunInfo()
+        _chk(lib().tfidf_last_run_info(self.h, C.byref(r)), "tfidf_last_run_info")
+        d = {k: getattr(r, k) for k, _ in RunInfo._fields_ if k not in ("ms_stage", "pad_")}
+        d["stages"] = {lib().tfidf_stage_name(i).decode(): r.ms_stage[i] for i in range(r.nstages)}
+        return d
+
+    def fetch(self) -> dict:
+        r = Result()
+        _chk(lib().tfidf_fetch(self.h, C.byref(r)), "tfidf_fetch")
+        try:
+            P, N, V = int(r.npairs), int(r.ndocs), int(r.nterms)
+
+            def arr(p, n, dt):
+                if n == 0:
+                    return np.zeros(0, dtype=dt)
+                return np.ctypeslib.as_array(p, shape=(n,)).astype(dt, copy=True)
+
+            out = {
+                "npairs": P, "ndocs": N, "nterms": V, "ndocs_total": int(r.ndocs_total),
+                "doc": arr(r.pair_doc, P, np.uint32), "term": arr(r.pair_term, P, np.uint32),
+                "count": arr(r.pair_count, P, np.uint32), "docsize": arr(r.pair_docsize, P, np.uint32),
+                "df": arr(r.pair_df, P, np.uint32), "score": arr(r.pair_score, P, np.float64),
+                "doc_id": arr(r.doc_id, N, np.uint32), "doc_size": arr(r.doc_size, N, np.uint32),
+                "term_df": arr(r.term_df, V, np.uint32),
+            }
+            toff = arr(r.term_off, V + 1, np.uint64)
+            tb = bytes(arr(r.term_bytes, int(toff[-1]) if V else 0, np.uint8))
+            out["terms"] = [tb[int(toff[i]):int(toff[i + 1])] for i in range(V)]
+            out["output_txt"] = format_lines(out)
+            return out
+        finally:
+            lib().tfidf_result_free(C.byref(r))
+
+
+def format_lines(res: dict) -> bytes:
+    """output.txt bytes ("docN@word\\t%.16f\\n", TFIDF.c:245,281) from a fetched result."""
+    terms = res["terms"]
+    parts = []
+    for d, t, s in zip(res["doc"].tolist(), res["term"].tolist(), res["score"].tolist()):
+        parts.append(b"doc%d@" % d + terms[t] + b"\t%.16f\n" % s)
+    return b"".join(parts)
+
+
+def comm_unique_id() -> bytes:
+    buf = (C.c_uint8 * UNIQUE_ID_BYTES)()
+    _chk(lib().tfidf_comm_unique_id(buf), "tfidf_comm_unique_id")
+    return bytes(buf)

@@ -1,0 +1,218 @@
+"""GPU parity tests: the HIP path (through the C-ABI) against the reference goldens and
+the oracle restatement.  TF counts, docSize and DF are compared bit-exactly; scores are
+compared bit-exactly too (host-libm idf LUT), the north-star tolerance being 1e-12
+relative.  Edge cases follow SURVEY §8c / Appendix A."""
+import ctypes as C
+import os
+import shutil
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+import oracle_py
+import tfidf_abi
+import tfidf_configs
+from conftest import golden_cases, GOLDEN
+from helpers import assert_same_result, docs_to_arrays, jobs_from_result, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def check_vs_oracle(engine, data, off, ids=None, n_total=0):
+    engine.run_host(data, off, ids, n_total)
+    res = engine.fetch()
+    ora = oracle_py.run(data, off, ids, n_total)
+    assert_same_result(res, ora)
+    assert res["output_txt"] == ora["output_txt"]
+    return res
+
+
+@pytest.mark.parametrize("case", golden_cases())
+def test_golden_output_txt(engine, case):
+    g = load_golden(case)
+    engine.run_host(g["data"], g["off"])
+    res = engine.fetch()
+    assert res["output_txt"] == g["output"]
+    tf, idf = jobs_from_result(res)
+    assert tf == g["tf_jobs"]
+    assert idf == g["idf_jobs"]
+
+
+@pytest.mark.parametrize("cfg,scale", [("c1", 1.0), ("c2", 0.003), ("c3", 0.00005), ("c4", 0.002), ("c5", 0.0005)])
+def test_synthetic_configs_vs_oracle(engine, cfg, scale):
+    p = tfidf_configs.plan(cfg, scale=scale)
+    data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
+    res = check_vs_oracle(engine, data, off, p["doc_ids"], p["ndocs_total"])
+    assert res["npairs"] > 0
+
+
+def test_document_boundaries_split_tokens(engine):
+    data, off = docs_to_arrays([b"ab", b"cd", b"ab", b"", b"ab cd"])
+    res = check_vs_oracle(engine, data, off)
+    assert res["output_txt"].count(b"\n") == 5
+
+
+def test_empty_corpus_and_blank_docs(engine):
+    data, off = docs_to_arrays([b"", b"  \n\t", b"\r\n", b"x"])
+    res = check_vs_oracle(engine, data, off)
+    assert res["npairs"] == 1
+
+
+def test_nul_and_control_bytes(engine):
+    docs = [b"ab\x00cd ab \x00zz \x01\x02 a\x01 a\x7f a\xff\xfe",
+            b"\x00 \x00\x00 ab\x00 ab\x00\x00x",
+            b"a\x08 a\x09a a\x0ea"]
+    check_vs_oracle(engine, *docs_to_arrays(docs))
+
+
+def test_long_tokens_and_shared_prefixes(engine):
+    rng = np.random.default_rng(7)
+    base = b"abcdefghijklmnop"  # 16 bytes
+    words = [base, base + b"q", base + b"\x01", base + b"qr" * 40, b"x" * 15, b"x" * 16, b"x" * 17,
+             base[:15], base[:15] + b"\x00tail", bytes(rng.integers(33, 127, 5000, dtype=np.uint8)),
+             b"y" * 70000]
+    docs = []
+    for i in range(6):
+        pick = rng.choice(len(words), size=12)
+        docs.append(b" ".join(words[j] for j in pick) + b"\n")
+    check_vs_oracle(engine, *docs_to_arrays(docs))
+
+
+def test_tokens_across_windows_and_chunks(engine):
+    # one big document (> BIG_DOC, split across chunks) whose tokens straddle the 4 KiB
+    # windows and 16 KiB chunk boundaries at every offset
+    rng = np.random.default_rng(3)
+    parts = []
+    n = 0
+    while n < 300_000:
+        L = int(rng.integers(1, 40))
+        w = bytes(rng.integers(97, 100, L, dtype=np.uint8))
+        sep = b" " if rng.random() < 0.9 else b"\n\t "
+        parts.append(w + sep)
+        n += L + len(sep)
+    docs = [b"".join(parts), b"aa bb", b"".join(parts[:5000])]
+    check_vs_oracle(engine, *docs_to_arrays(docs))
+
+
+def test_many_tiny_documents(engine):
+    rng = np.random.default_rng(11)
+    docs = []
+    for i in range(20000):
+        k = int(rng.integers(0, 4))
+        docs.append(b"" if k == 0 else b" ".join(b"w%d" % rng.integers(0, 50) for _ in range(k)))
+    check_vs_oracle(engine, *docs_to_arrays(docs))
+
+
+def test_doc_ids_and_ndocs_total(engine):
+    p = tfidf_configs.plan("c2", scale=0.002, rank=1, nranks=3)
+    data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
+    check_vs_oracle(engine, data, off, p["doc_ids"], p["ndocs_total"])
+
+
+def _hip_d2h(dst: np.ndarray, src_ptr: int):
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    assert hip.hipMemcpy(dst.ctypes.data, C.c_void_p(src_ptr), dst.nbytes, 2) == 0
+
+
+def test_device_generator_matches_host(engine):
+    p = tfidf_configs.plan("c5", scale=0.0002)
+    h, hoff = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
+    c = engine.synth_device(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"], p["ndocs_total"])
+    assert c.nbytes == len(h)
+    d = np.empty(len(h), dtype=np.uint8)
+    _hip_d2h(d, c.bytes)
+    doff = np.empty(len(hoff), dtype=np.uint64)
+    _hip_d2h(doff, c.doc_off)
+    assert np.array_equal(d, h) and np.array_equal(doff, hoff)
+    engine.run_corpus(c)
+    res = engine.fetch()
+    ora = oracle_py.run(h, hoff, p["doc_ids"], p["ndocs_total"])
+    assert_same_result(res, ora)
+
+
+def test_rccl_single_rank_exchange_path():
+    """Attaching a 1-rank RCCL communicator runs the vocabulary all-gather + DF
+    all-reduce path; results must not change."""
+    p = tfidf_configs.plan("c2", scale=0.002)
+    data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
+    with tfidf_abi.Engine(0) as e:
+        e.comm_init(tfidf_abi.comm_unique_id(), 0, 1)
+        e.run_host(data, off, p["doc_ids"], p["ndocs_total"])
+        res = e.fetch()
+        assert e.info()["nterms_global"] == res["nterms"]
+    assert_same_result(res, oracle_py.run(data, off, p["doc_ids"], p["ndocs_total"]))
+
+
+def test_repeat_runs_identical(engine):
+    p = tfidf_configs.plan("c2", scale=0.002)
+    data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
+    outs = []
+    for _ in range(3):
+        engine.run_host(data, off, p["doc_ids"], p["ndocs_total"])
+        outs.append(engine.fetch()["output_txt"])
+    assert outs[0] == outs[1] == outs[2]
+
+
+@pytest.mark.parametrize("case", ["g1_whitespace", "g2_twelve_docs", "g4_config1"])
+def test_cli_drop_in(case):
+    """`tfidf` with no arguments in the fixture directory writes the reference output.txt."""
+    with tempfile.TemporaryDirectory() as td:
+        shutil.copytree(os.path.join(GOLDEN, case, "input"), os.path.join(td, "input"))
+        p = subprocess.run([tfidf_abi.CLI_PATH], cwd=td, capture_output=True, timeout=120)
+        assert p.returncode == 0, p.stderr
+        with open(os.path.join(td, "output.txt"), "rb") as f:
+            assert f.read() == load_golden(case)["output"]
+        p = subprocess.run([tfidf_abi.CLI_PATH, "--debug-jobs"], cwd=td, capture_output=True, timeout=120)
+        assert b"-------------TF Job-------------" in p.stdout
+
+
+def test_cli_error_contract():
+    with tempfile.TemporaryDirectory() as td:
+        p = subprocess.run([tfidf_abi.CLI_PATH], cwd=td, capture_output=True, timeout=60)
+        assert p.returncode == 1 and p.stdout == b"Directory failed to open\n"
+        os.makedirs(os.path.join(td, "input"))
+        with open(os.path.join(td, "input", "doc2"), "wb") as f:
+            f.write(b"x")
+        p = subprocess.run([tfidf_abi.CLI_PATH], cwd=td, capture_output=True, timeout=60)
+        assert p.returncode == 0 and p.stdout.startswith(b"Error Opening File: input/doc1")
+
+
+def test_full_c2_properties():
+    """Config 2 at full size (1e5 docs, ~1 GB, device-generated): size-independent
+    properties — sum of counts = tokens, per-document sums = docSize, DF = pairs per term,
+    strict output order, scores recomputed (<= 1e-12 relative)."""
+    p = tfidf_configs.plan("c2")
+    with tfidf_abi.Engine(0) as e:
+        c = e.synth_device(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"], p["ndocs_total"])
+        e.run_corpus(c)
+        info = e.info()
+        r = e.fetch()
+    assert info["ntokens"] == int(p["ntok"].sum())
+    P = r["npairs"]
+    assert P == info["npairs"] and P > 1_000_000
+    cnt = r["count"].astype(np.int64)
+    assert cnt.sum() == info["ntokens"]
+    # per document: sum of counts == docSize (docs are contiguous runs in the output)
+    starts = np.flatnonzero(np.r_[True, r["doc"][1:] != r["doc"][:-1]])
+    sums = np.add.reduceat(cnt, starts)
+    assert np.array_equal(sums, r["docsize"][starts].astype(np.int64))
+    ds = dict(zip(r["doc_id"].tolist(), r["doc_size"].tolist()))
+    assert sum(ds.values()) == info["ntokens"]
+    # DF == number of pairs per term
+    dfc = np.bincount(r["term"], minlength=r["nterms"])
+    assert np.array_equal(dfc, r["term_df"])
+    assert np.array_equal(r["df"], r["term_df"][r["term"]])
+    # strict strcmp order: (doc key, term rank) increasing
+    dk = tfidf_configs.doc_name_key(r["doc"]).astype(np.uint64)
+    key = (dk.astype(object) * 0)  # placeholder to keep numpy from overflowing below
+    del key
+    assert np.all((dk[1:] > dk[:-1]) | ((dk[1:] == dk[:-1]) & (r["term"][1:] > r["term"][:-1])))
+    terms = r["terms"]
+    assert all((terms[i] + b"\t") < (terms[i + 1] + b"\t") for i in range(0, len(terms) - 1, 97))
+    # scores
+    N = r["ndocs_total"]
+    ref = (cnt / r["docsize"].astype(np.float64)) * np.log(N / r["df"].astype(np.float64))
+    np.testing.assert_allclose(r["score"], ref, rtol=1e-12, atol=1e-300)
