@@ -1,0 +1,178 @@
+#!/usr/bin/env python3
+"""bench.py — TF-IDF hot path throughput on MI355X (BASELINE.json metric: corpus GB/s and
+TF-IDF pairs/s at 1/2/4/8 GPUs; % of HBM peak).
+
+A step = one full pass of the hot path (tokenize -> per-document TF -> vocabulary -> DF
+[RCCL all-gather + all-reduce across ranks] -> idf -> tf*idf -> output order) over one
+batch: the config-2 corpus (1e5 synthetic Zipfian documents, V = 5e4, ~1 GB) resident in
+HBM.  Multi-GPU is weak scaling: every rank owns one config-2-sized shard of a corpus of
+N x 1e5 documents (contiguous "docN" strcmp ranges; idf uses the global N).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints one JSON line.  `roofline` is priced on the dominant kernel (K1
+tokenize+count), algorithmic bytes per launch = C + 12*P, divided by K1's
+average duration measured with HIP events on the engine's stream inside the timed steps.
+`cpu_baseline` times the oracle restatement (single thread) on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "parallel-systems-mpi-tfidf_amd", "python"))
+
+import numpy as np  # noqa: E402
+
+import tfidf_abi  # noqa: E402  (loads libtfidf_hip.so before torch: one HIP runtime)
+import tfidf_configs  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
+
+
+def hip_device_sync():
+    hip = C.CDLL("libamdhip64.so.7")
+    if hip.hipDeviceSynchronize() != 0:
+        raise RuntimeError("hipDeviceSynchronize failed")
+
+
+def load_traffic():
+    """HBM bytes per K1 launch from the committed rocprofv3 PMC summary (or None)."""
+    p = os.path.join(REPO, "profiles", "k1_pmc_traffic.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    return None
+
+
+def cpu_baseline(cfg: str, ndocs_sample: int):
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle_py  # oracle: CPU baseline only (never the measured GPU path)
+    p = tfidf_configs.plan(cfg)
+    ids, ntok = p["doc_ids"][:ndocs_sample], p["ntok"][:ndocs_sample]
+    data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], ids, ntok)
+    t0 = time.perf_counter()
+    r = oracle_py.run(data, off, ids, p["ndocs_total"], arrays=False)
+    dt = time.perf_counter() - t0
+    return {"value": round(len(data) / dt / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/tfidf_oracle.c (C restatement of TFIDF.c, 1 thread) on the first {ndocs_sample} "
+                      f"documents of {cfg} ({len(data) / 1e6:.1f} MB, {r['npairs']} pairs), tokenize through "
+                      f"sorted output lines; {dt:.2f} s",
+            "pairs_per_s": round(r["npairs"] / dt, 1)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--cpu-sample-docs", type=int, default=12000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # rendezvous, barriers and max-reduce over gloo (CPU)
+        dist.init_process_group("gloo", init_method="env://")
+    ngpu = world
+
+    eng = tfidf_abi.Engine(local)
+    if world > 1:
+        import torch
+        uid = torch.zeros(tfidf_abi.UNIQUE_ID_BYTES, dtype=torch.uint8)
+        if rank == 0:
+            uid[:] = torch.frombuffer(bytearray(tfidf_abi.comm_unique_id()), dtype=torch.uint8)
+        dist.broadcast(uid, 0)
+        eng.comm_init(bytes(uid.numpy().tobytes()), rank, world)
+
+    p = tfidf_configs.plan(args.config, scale=args.scale, rank=rank, nranks=world, weak=True)
+    corpus = eng.synth_device(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"], p["ndocs_total"])
+    eng.set_timing(True)
+
+    for _ in range(args.warmup):
+        eng.run_corpus(corpus)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    k1_ms, tot_ms = [], []
+    barrier()
+    hip_device_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.run_corpus(corpus)
+        info = eng.info()
+        k1_ms.append(info["ms_tokcount"])
+        tot_ms.append(info["ms_total"])
+    hip_device_sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    info = eng.info()
+    C_bytes, P_pairs, T_tok = info["nbytes"], info["npairs"], info["ntokens"]
+
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tot = torch.tensor([C_bytes, P_pairs, T_tok], dtype=torch.float64)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        C_all, P_all, T_all = (float(x) for x in tot.tolist())
+    else:
+        C_all, P_all, T_all = float(C_bytes), float(P_pairs), float(T_tok)
+
+    if rank == 0:
+        ms_step = elapsed / args.steps * 1e3
+        k1_avg_ms = float(np.mean(k1_ms))
+        alg_bytes = C_bytes + 12.0 * P_pairs  # per K1 launch on this rank
+        achieved = alg_bytes / (k1_avg_ms * 1e-3) / 1e9
+        traffic = load_traffic()
+        line = {
+            "metric": "corpus GB/s (TF-IDF hot path: tokenize->TF->DF->tf*idf->ordered output)",
+            "value": round(C_all * args.steps / elapsed / 1e9, 4),
+            "unit": "GB/s",
+            "n_gpus": ngpu,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8/u32 (f64 score)",
+            "data": "synthetic (device-generated Zipfian corpus, csrc/synth.h), resident in HBM",
+            "config": {"workload": f"{args.config}: {len(p['doc_ids'])} docs/GPU, V={p['V']}, "
+                                   f"{C_bytes / 1e9:.3f} GB/GPU, {P_pairs} pairs/GPU",
+                       "docs_total": int(p["ndocs_total"]), "corpus_bytes_total": int(C_all),
+                       "parallelism": f"doc-shard x{ngpu} + RCCL DF all-reduce" if ngpu > 1 else "1 GPU"},
+            "pairs_per_s": round(P_all * args.steps / elapsed, 1),
+            "tokens_per_s": round(T_all * args.steps / elapsed, 1),
+            "device_ms_per_step": round(float(np.mean(tot_ms)), 4),
+            "stage_ms": {k: round(v, 4) for k, v in info["stages"].items()},
+            "roofline": {"bound": "hbm", "kernel": "k_tokcount (K1)", "achieved": round(achieved, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "alg_bytes_per_launch": int(alg_bytes),
+                         "k1_avg_ms": round(k1_avg_ms, 4)},
+            "cpu_baseline": None,
+        }
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_sample_docs)
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

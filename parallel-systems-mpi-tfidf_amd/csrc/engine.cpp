@@ -493,6 +493,9 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     a.idf_idx = ctx->present.as<uint32_t>();
     a.idf = ctx->idf_vals.as<double>();
     a.ndocs = N;
+    a.rec_total = R_total;
+    a.slot_cap = cap;
+    a.status = (uint32_t*)(cnt + 3);
     a.out_doc = ctx->out_doc.as<uint32_t>();
     a.out_term = ctx->out_term.as<uint32_t>();
     a.out_cnt = ctx->out_cnt.as<uint32_t>();
@@ -501,7 +504,13 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     a.out_score = ctx->out_score.as<double>();
     LCHK(launch_score_order(a, s));
     mark(ctx, S_NSTAGES);
+    uint32_t st_end = 0;
+    HIPCHK(hipMemcpyAsync(&st_end, cnt + 3, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    if (st_end & ST_BOUNDS) {
+        fprintf(stderr, "tfidf: internal bounds check tripped (status 0x%x)\n", st_end);
+        return TFIDF_E_STATE;
+    }
     return 0;
 }
 

@@ -187,7 +187,10 @@ __global__ void k_part_npairs(const uint64_t* __restrict__ keys, const uint32_t*
     if (i >= n) return;
     uint32_t d = (uint32_t)(keys[i] >> 32);
     if (i + 1 < n && (uint32_t)(keys[i + 1] >> 32) == d) return; /* last record of d */
-    doc_npairs[d] = (uint32_t)(rec_base + head_pos[i] + 1 - doc_recoff[d]);
+    /* unique index of record i's run: head_pos is an EXCLUSIVE scan of run heads */
+    const bool is_head = (i == 0 || keys[i] != keys[i - 1]);
+    const uint64_t u = head_pos[i] - (is_head ? 0u : 1u);
+    doc_npairs[d] = (uint32_t)(rec_base + u + 1 - doc_recoff[d]);
 }
 int launch_part_merge(const uint64_t* keys, const uint32_t* seq, const uint32_t* part_cnt, const uint32_t* head_pos,
                       uint64_t n, const uint32_t* slot_of_rank, uint64_t rec_base, uint32_t* rec_slot,
@@ -337,18 +340,27 @@ __global__ __launch_bounds__(NT) void k_score_order(K5Args a) {
     const uint64_t ob = a.out_off[i], rb = a.doc_recoff[d];
     const uint32_t ds = a.doc_size[d];
     const uint32_t id = a.doc_ids ? a.doc_ids[d] : d + 1;
+    if (rb + n > a.rec_total) { /* never expected: report instead of reading past the records */
+        if (threadIdx.x == 0) atomicOr(a.status, ST_BOUNDS);
+        return;
+    }
     if ((a.doc_flags[d] & DF_PRESORTED) || n > (uint32_t)K5_MAX) {
         for (uint32_t j = threadIdx.x; j < n; j += NT) {
-            uint32_t r = a.rank_of_slot[a.rec_slot[rb + j]];
-            k5_emit(a, ob + j, id, ds, r, a.rec_cnt[rb + j]);
+            uint32_t sl = a.rec_slot[rb + j];
+            if (sl >= a.slot_cap) { atomicOr(a.status, ST_BOUNDS); continue; }
+            k5_emit(a, ob + j, id, ds, a.rank_of_slot[sl], a.rec_cnt[rb + j]);
         }
         return;
     }
     uint32_t P = 1;
     while (P < n) P <<= 1;
     for (uint32_t j = threadIdx.x; j < P; j += NT) {
-        if (j < n) { skey[j] = a.rank_of_slot[a.rec_slot[rb + j]]; sval[j] = a.rec_cnt[rb + j]; }
-        else { skey[j] = 0xFFFFFFFFu; sval[j] = 0; }
+        if (j < n) {
+            uint32_t sl = a.rec_slot[rb + j];
+            if (sl >= a.slot_cap) { atomicOr(a.status, ST_BOUNDS); sl = 0; }
+            skey[j] = a.rank_of_slot[sl];
+            sval[j] = a.rec_cnt[rb + j];
+        } else { skey[j] = 0xFFFFFFFFu; sval[j] = 0; }
     }
     __syncthreads();
     for (uint32_t k = 2; k <= P; k <<= 1) {

@@ -18,6 +18,7 @@
 #define ST_VOCAB_SPIN  2u
 #define ST_REC_FULL    4u
 #define ST_PART_FULL   8u
+#define ST_BOUNDS      16u   /* internal consistency guard tripped (a bug, reported as an error) */
 
 /* doc flags */
 #define DF_PARTIAL     1u
@@ -107,6 +108,9 @@ struct K5Args {
     const uint32_t* idf_idx;     /* df value -> index into idf */
     const double* idf;
     uint32_t ndocs;
+    uint64_t rec_total;          /* bounds guard: records in rec_slot/rec_cnt */
+    uint64_t slot_cap;           /* bounds guard: vocabulary capacity */
+    uint32_t* status;            /* ST_BOUNDS set instead of faulting */
     uint32_t* out_doc;
     uint32_t* out_term;
     uint32_t* out_cnt;

@@ -392,14 +392,17 @@ __global__ __launch_bounds__(NT, 2) void k_tokcount(CorpusDev c, const uint64_t*
             if (tid == 0) {
                 S.cut = 0xFFFFFFFFu;
                 if (S.epoch_lo == DOC_NONE) S.epoch_lo = d; /* thread 0 holds token `base` */
+                S.base_doc_tok = d;
             }
             __syncthreads();
+            /* Block-uniform decisions use values captured here, between two barriers with
+             * no writers: the insert phase below updates fill/open_doc while slower waves
+             * could still be deciding. */
+            const uint32_t elo = S.epoch_lo, fill0 = S.fill, open0 = S.open_doc, dbase = S.base_doc_tok;
             /* cut the batch at the first token whose document must start a new epoch */
             {
-                const uint32_t elo = S.epoch_lo;
                 uint32_t cut_doc = elo + FDOCS;
-                if (S.fill > (uint32_t)FLUSH_THR && S.open_doc != DOC_NONE && S.open_doc + 1 < cut_doc)
-                    cut_doc = S.open_doc + 1;
+                if (fill0 > (uint32_t)FLUSH_THR && open0 != DOC_NONE && open0 + 1 < cut_doc) cut_doc = open0 + 1;
                 bool f = has && d >= cut_doc;
                 uint64_t bm = __ballot(f);
                 if (bm && lane == (int)__builtin_ctzll(bm)) atomicMin(&S.cut, i);
@@ -412,13 +415,9 @@ __global__ __launch_bounds__(NT, 2) void k_tokcount(CorpusDev c, const uint64_t*
                 k1_flush(S, c, v, o, cs, ce, DOC_NONE);
                 continue;
             }
-            if (S.fill + (end - base) > (uint32_t)TBL_HARD) {
+            if (fill0 + (end - base) > (uint32_t)TBL_HARD) {
                 /* cannot fit: flush now; the open document straddles iff it continues at base */
-                uint32_t dbase = __shfl(d, 0, 64); /* thread 0 holds token `base` */
-                if (tid == 0) S.more = dbase;
-                __syncthreads();
-                uint32_t db = S.more;
-                k1_flush(S, c, v, o, cs, ce, (S.open_doc == db) ? db : DOC_NONE);
+                k1_flush(S, c, v, o, cs, ce, (open0 == dbase) ? dbase : DOC_NONE);
                 continue;
             }
             /* ---- insert tokens [base, end) ---- */
@@ -467,8 +466,9 @@ __global__ __launch_bounds__(NT, 2) void k_tokcount(CorpusDev c, const uint64_t*
                     if (td == DOC_NONE) {
                         uint32_t old = atomicCAS(&S.tdoc[h], DOC_NONE, d);
                         if (old == DOC_NONE) {
+                            /* publish: klo, then khi with release (a reader that sees khi sees klo) */
                             S.klo[h] = klo;
-                            S.khi[h] = khi;
+                            __hip_atomic_store(&S.khi[h], khi, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                             atomicAdd(&S.tcnt[h], 1u);
                             atomicAdd(&S.fill, 1u);
                             break;
@@ -476,7 +476,7 @@ __global__ __launch_bounds__(NT, 2) void k_tokcount(CorpusDev c, const uint64_t*
                         td = old;
                     }
                     if (td == d) {
-                        uint64_t kh = S.khi[h];
+                        uint64_t kh = __hip_atomic_load(&S.khi[h], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
                         if (kh == KEY_EMPTY_HI) continue;      /* claimer still publishing: retry */
                         if (kh == khi && S.klo[h] == klo) { atomicAdd(&S.tcnt[h], 1u); break; }
                     }

@@ -59,9 +59,27 @@ def jobs_from_result(res: dict):
     return b"".join(x + b"\n" for x in sorted(tf)), b"".join(x + b"\n" for x in sorted(idf))
 
 
+def describe_diff(gpu: dict, ora: dict) -> str:
+    """First document whose pairs differ, for the failure message."""
+    def by_doc(r):
+        out = {}
+        for d, t, c, ds in zip(r["doc"].tolist(), r["term"].tolist(), r["count"].tolist(), r["docsize"].tolist()):
+            out.setdefault(d, []).append((r["terms"][t], c, ds))
+        return out
+    g, o = by_doc(gpu), by_doc(ora)
+    for d in sorted(set(g) | set(o)):
+        if g.get(d) != o.get(d):
+            gs, os_ = g.get(d, []), o.get(d, [])
+            extra = sorted(set(gs) - set(os_))[:10]
+            missing = sorted(set(os_) - set(gs))[:10]
+            return (f"doc{d}: gpu {len(gs)} pairs, oracle {len(os_)}; gpu-only {extra}; oracle-only {missing}; "
+                    f"docsize gpu {gs[0][2] if gs else None} oracle {os_[0][2] if os_ else None}")
+    return "no per-document difference"
+
+
 def assert_same_result(gpu: dict, ora: dict, exact_scores: bool = True):
     """Field-by-field parity: integers bit-exact, scores exact (or <= 1e-12 relative)."""
-    assert gpu["npairs"] == ora["npairs"]
+    assert gpu["npairs"] == ora["npairs"], describe_diff(gpu, ora)
     np.testing.assert_array_equal(gpu["doc"], ora["doc"])
     gterms = [gpu["terms"][t] for t in gpu["term"].tolist()]
     oterms = [ora["terms"][t] for t in ora["term"].tolist()]
