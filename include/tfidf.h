@@ -125,12 +125,17 @@ typedef struct tfidf_run_info {
     double   ms_tokcount;     /* device time of the tokenize+count kernels (HIP events) */
     double   ms_stage[16];    /* per-stage device times, see tfidf_stage_name() */
     uint32_t nstages;
-    uint32_t pad_;
+    uint32_t flags;           /* TFIDF_RUN_* */
 } tfidf_run_info;
+#define TFIDF_RUN_K1_FAST 1u  /* whitespace-separated documents: fast tokenize+count kernel */
 int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info);
 const char* tfidf_stage_name(int stage);
 /* Enables per-stage HIP event timing (adds a few event records per run). */
 int tfidf_set_timing(tfidf_ctx* ctx, int enable);
+/* Diagnostics: per-phase cycle sums of the fast tokenize+count kernel, available only
+ * from the diagnostic build lib/libtfidf_hip_stamps.so with TFIDF_STAMPS=1 set before
+ * tfidf_open.  Returns the number of values written (phases + workgroup count). */
+int tfidf_debug_k1_stamps(tfidf_ctx* ctx, uint64_t* out, int n);
 
 /* ---------------------------------------------------------------- emission -- */
 

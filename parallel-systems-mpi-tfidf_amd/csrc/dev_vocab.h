@@ -1,0 +1,52 @@
+/* dev_vocab.h — the global HBM vocabulary: lock-free 128-bit key insert shared by the
+ * tokenize+count kernels (term identity keys: dev_common.h). */
+#ifndef TFIDF_DEV_VOCAB_H
+#define TFIDF_DEV_VOCAB_H
+
+#include "dev_common.h"
+#include "kernels.h"
+
+#define VOCAB_MAX_PROBE (1u << 20)
+
+/* Lock-free find-or-insert of a 128-bit key into the global vocabulary.
+ * A slot is {lo, hi}; hi is the claim word: EMPTY -> PENDING (CAS) -> key (exchange)
+ * after lo has been exchanged in, so a 16-byte snapshot whose hi is a real key always
+ * carries its lo.  Plain loads may return stale EMPTY/PENDING lines from this XCD's L2;
+ * those cases are re-read at the memory side with atomics (MI355X L2s are not coherent
+ * across XCDs, device-scope atomics are). */
+__device__ __noinline__ uint32_t vocab_insert(const VocabDev v, uint64_t klo, uint64_t khi, uint64_t rep, uint32_t* status) {
+    uint64_t h = key_hash(klo, khi) & v.mask;
+    for (uint32_t probe = 0; probe < VOCAB_MAX_PROBE && probe <= v.mask; ++probe, h = (h + 1) & v.mask) {
+        unsigned long long* slot = reinterpret_cast<unsigned long long*>(&v.keys[h]);
+        uint4 s = v.keys[h];
+        uint64_t lo = ((uint64_t)s.y << 32) | s.x, hi = ((uint64_t)s.w << 32) | s.z;
+        if (hi == khi && lo == klo) return (uint32_t)h;
+        if (hi != KEY_EMPTY_HI && hi != KEY_PENDING_HI) continue;
+        if (hi == KEY_EMPTY_HI) {
+            unsigned long long old = atomicCAS(&slot[1], (unsigned long long)KEY_EMPTY_HI,
+                                               (unsigned long long)KEY_PENDING_HI);
+            if (old == KEY_EMPTY_HI) {
+                atomicExch(&slot[0], (unsigned long long)klo);
+                if ((khi >> 56) == 0xFFu) v.rep[h] = rep;
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                atomicExch(&slot[1], (unsigned long long)khi);
+                return (uint32_t)h;
+            }
+            hi = old;
+        }
+        uint32_t spins = 0;
+        while (hi == KEY_PENDING_HI) {
+            __builtin_amdgcn_s_sleep(2);
+            hi = atomicOr(&slot[1], 0ull);
+            if (++spins > (1u << 24)) { atomicOr(status, ST_VOCAB_SPIN); return INVALID_SLOT; }
+        }
+        if (hi == khi) {
+            lo = atomicOr(&slot[0], 0ull);
+            if (lo == klo) return (uint32_t)h;
+        }
+    }
+    atomicOr(status, ST_VOCAB_FULL);
+    return INVALID_SLOT;
+}
+
+#endif

@@ -72,6 +72,10 @@ struct tfidf_ctx {
     ncclComm_t comm = nullptr;
     int rank = 0, nranks = 1;
     bool timing = true;
+    int k1_mode = 0;        /* 0 auto, 2 force the general K1 (env TFIDF_K1=general) */
+    bool stamps_on = false; /* env TFIDF_STAMPS=1 with the diagnostic library build */
+    DevBuf stamps;
+    bool k1_fast = false;   /* last run used the whitespace-separated fast path */
     hipEvent_t ev[S_NSTAGES + 1];
     Arena arena;
     DevBuf arena_buf;
@@ -170,6 +174,10 @@ int tfidf_open(int device, tfidf_ctx** out) {
     if (hipSetDevice(device) != hipSuccess) return TFIDF_E_NODEV;
     tfidf_ctx* ctx = new tfidf_ctx();
     ctx->device = device;
+    const char* km = getenv("TFIDF_K1");
+    if (km && !strcmp(km, "general")) ctx->k1_mode = 2;
+    const char* ks = getenv("TFIDF_STAMPS");
+    ctx->stamps_on = ks && ks[0] == '1';
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     for (int i = 0; i <= S_NSTAGES; ++i) HIPCHK(hipEventCreate(&ctx->ev[i]));
     if (arena_reset(ctx, 64ull << 20) != 0) { delete ctx; return TFIDF_E_NOMEM; }
@@ -194,7 +202,7 @@ void tfidf_close(tfidf_ctx* ctx) {
                       &ctx->npairs_ord, &ctx->out_off, &ctx->out_doc, &ctx->out_term, &ctx->out_cnt,
                       &ctx->out_docsize, &ctx->out_df, &ctx->out_score, &ctx->x_mine, &ctx->x_send, &ctx->x_recv,
                       &ctx->x_recv2, &ctx->x_seq0, &ctx->x_seq1, &ctx->x_head, &ctx->x_grank, &ctx->x_dfv,
-                      &ctx->x_cnt};
+                      &ctx->x_cnt, &ctx->stamps};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i <= S_NSTAGES; ++i) (void)hipEventDestroy(ctx->ev[i]);
     (void)hipStreamDestroy(ctx->stream);
@@ -315,6 +323,15 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     HIPCHK(hipMemsetAsync(ctx->doc_size.p, 0, (size_t)N * 4 + 4, s));
     HIPCHK(hipMemsetAsync(ctx->doc_flags.p, 0, (size_t)N + 1, s));
     if (nchunks) LCHK(launch_plan_chunks(c, nchunks, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), s));
+    /* K1 variant: whitespace-separated documents take the fast path */
+    uint32_t not_ws_sep = 1;
+    if (nchunks && ctx->k1_mode != 2) {
+        LCHK(launch_docs_ws_sep(c, (uint32_t*)(cnt + 4), s));
+        HIPCHK(hipMemcpyAsync(&not_ws_sep, cnt + 4, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    /* the fast path's clamped 16-byte group loads need a 16-byte aligned corpus base */
+    ctx->k1_fast = (not_ws_sep == 0) && ctx->k1_mode != 2 && (((uintptr_t)c.bytes & 15u) == 0);
     /* ---- K1 ---- */
     mark(ctx, S_TOKCOUNT);
     VocabDev vd{ctx->vkeys.as<uint4>(), ctx->vrep.as<uint64_t>(), ctx->vcap - 1};
@@ -334,7 +351,15 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     o.doc_flags = ctx->doc_flags.as<uint8_t>();
     o.ntokens = cnt + 2;
     o.status = (uint32_t*)(cnt + 3);
-    if (nchunks)
+    o.stamps = nullptr;
+    if (ctx->stamps_on) {
+        ENSURE(ctx->stamps, 8 * K1_STAMP_WORDS);
+        HIPCHK(hipMemsetAsync(ctx->stamps.p, 0, 8 * K1_STAMP_WORDS, s));
+        o.stamps = ctx->stamps.as<unsigned long long>();
+    }
+    if (nchunks && ctx->k1_fast)
+        LCHK(launch_tokcount_ws(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
+    else if (nchunks)
         LCHK(launch_tokcount(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
     mark(ctx, S_VOCAB);
     unsigned long long hc[4];
@@ -493,6 +518,7 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     a.idf_idx = ctx->present.as<uint32_t>();
     a.idf = ctx->idf_vals.as<double>();
     a.ndocs = N;
+    a.rank_bits = V > 1 ? 32u - (uint32_t)__builtin_clz(V - 1) : 1u;
     a.rec_total = R_total;
     a.slot_cap = cap;
     a.status = (uint32_t*)(cnt + 3);
@@ -586,6 +612,14 @@ extern "C" int tfidf_run(tfidf_ctx* ctx, const tfidf_corpus* in) {
     return TFIDF_OK;
 }
 
+extern "C" int tfidf_debug_k1_stamps(tfidf_ctx* ctx, uint64_t* out, int n) {
+    if (!ctx || !out || n <= 0) return TFIDF_E_INVAL;
+    if (!ctx->stamps_on || !ctx->stamps.p) return TFIDF_E_STATE;
+    int m = n < K1_STAMP_WORDS ? n : K1_STAMP_WORDS;
+    HIPCHK(hipMemcpy(out, ctx->stamps.p, 8 * (size_t)m, hipMemcpyDeviceToHost));
+    return m;
+}
+
 extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info) {
     if (!ctx || !info) return TFIDF_E_INVAL;
     if (!ctx->have_result) return TFIDF_E_STATE;
@@ -616,6 +650,7 @@ extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info) {
     info->ms_tokcount = ctx->ms_stage[S_TOKCOUNT];
     for (int i = 0; i < S_NSTAGES; ++i) info->ms_stage[i] = ctx->ms_stage[i];
     info->nstages = S_NSTAGES;
+    info->flags = ctx->k1_fast ? TFIDF_RUN_K1_FAST : 0u;
     return TFIDF_OK;
 }
 

@@ -330,60 +330,121 @@ __device__ __forceinline__ void k5_emit(const K5Args& a, uint64_t o, uint32_t id
     a.out_score[o] = tf * idf;             /* TFIDF.c:244 */
 }
 
-__global__ __launch_bounds__(NT) void k_score_order(K5Args a) {
-    __shared__ uint32_t skey[K5_MAX];
-    __shared__ uint32_t sval[K5_MAX];
+constexpr uint32_t K5_SMALL = 64;
+
+__device__ __forceinline__ uint32_t k5_rank(const K5Args& a, uint32_t sl) {
+    if (sl >= a.slot_cap) { atomicOr(a.status, ST_BOUNDS); sl = 0; }
+    return a.rank_of_slot[sl];
+}
+
+/* Documents with <= 64 pairs: one wave each, bitonic sort of (rank, count) across the
+ * 64 lanes with __shfl_xor; four documents per workgroup, no barriers. */
+__global__ __launch_bounds__(NT) void k_score_small(K5Args a) {
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t i = blockIdx.x * (NT / 64) + w;
+    if (i >= a.ndocs) return;
+    const uint32_t d = a.order[i];
+    const uint32_t n = a.doc_npairs[d];
+    if (n == 0 || n > K5_SMALL) return;
+    const uint64_t ob = a.out_off[i], rb = a.doc_recoff[d];
+    if (rb + n > a.rec_total) { if (lane == 0) atomicOr(a.status, ST_BOUNDS); return; }
+    uint32_t key = 0xFFFFFFFFu, val = 0;
+    if (lane < n) { key = k5_rank(a, a.rec_slot[rb + lane]); val = a.rec_cnt[rb + lane]; }
+#pragma unroll
+    for (uint32_t k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            uint32_t pk = __shfl_xor(key, j, 64), pv = __shfl_xor(val, j, 64);
+            bool take_min = ((lane & k) == 0) == ((lane & j) == 0);
+            if (take_min ? (pk < key) : (pk > key)) { key = pk; val = pv; }
+        }
+    }
+    if (lane < n) {
+        const uint32_t id = a.doc_ids ? a.doc_ids[d] : d + 1;
+        k5_emit(a, ob + lane, id, a.doc_size[d], key, val);
+    }
+}
+
+/* Documents with > 64 pairs: one workgroup each.  Presorted (merged) runs are scored
+ * straight through; others are LSD radix-sorted by rank in LDS, 8-bit digits, with a
+ * stable wave64 multisplit (8 ballots) per round of 256 elements. */
+__global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
+    __shared__ uint32_t kbuf[2][K5_MAX];
+    __shared__ uint32_t vbuf[2][K5_MAX];
+    __shared__ uint32_t hist[256], run[256];
+    __shared__ uint32_t wcnt[NT / 64][256];
+    __shared__ uint32_t wsum[NT / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t i = blockIdx.x;
     const uint32_t d = a.order[i];
     const uint32_t n = a.doc_npairs[d];
-    if (n == 0) return;
+    if (n <= K5_SMALL) return;
     const uint64_t ob = a.out_off[i], rb = a.doc_recoff[d];
     const uint32_t ds = a.doc_size[d];
     const uint32_t id = a.doc_ids ? a.doc_ids[d] : d + 1;
     if (rb + n > a.rec_total) { /* never expected: report instead of reading past the records */
-        if (threadIdx.x == 0) atomicOr(a.status, ST_BOUNDS);
+        if (tid == 0) atomicOr(a.status, ST_BOUNDS);
         return;
     }
     if ((a.doc_flags[d] & DF_PRESORTED) || n > (uint32_t)K5_MAX) {
-        for (uint32_t j = threadIdx.x; j < n; j += NT) {
-            uint32_t sl = a.rec_slot[rb + j];
-            if (sl >= a.slot_cap) { atomicOr(a.status, ST_BOUNDS); continue; }
-            k5_emit(a, ob + j, id, ds, a.rank_of_slot[sl], a.rec_cnt[rb + j]);
-        }
+        if (n > (uint32_t)K5_MAX && !(a.doc_flags[d] & DF_PRESORTED)) { if (tid == 0) atomicOr(a.status, ST_BOUNDS); return; }
+        for (uint32_t j = tid; j < n; j += NT) k5_emit(a, ob + j, id, ds, k5_rank(a, a.rec_slot[rb + j]), a.rec_cnt[rb + j]);
         return;
     }
-    uint32_t P = 1;
-    while (P < n) P <<= 1;
-    for (uint32_t j = threadIdx.x; j < P; j += NT) {
-        if (j < n) {
-            uint32_t sl = a.rec_slot[rb + j];
-            if (sl >= a.slot_cap) { atomicOr(a.status, ST_BOUNDS); sl = 0; }
-            skey[j] = a.rank_of_slot[sl];
-            sval[j] = a.rec_cnt[rb + j];
-        } else { skey[j] = 0xFFFFFFFFu; sval[j] = 0; }
+    for (uint32_t j = tid; j < n; j += NT) {
+        kbuf[0][j] = k5_rank(a, a.rec_slot[rb + j]);
+        vbuf[0][j] = a.rec_cnt[rb + j];
     }
-    __syncthreads();
-    for (uint32_t k = 2; k <= P; k <<= 1) {
-        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
-            for (uint32_t t = threadIdx.x; t < P; t += NT) {
-                uint32_t p = t ^ jj;
-                if (p > t) {
-                    bool up = (t & k) == 0;
-                    uint32_t x = skey[t], y = skey[p];
-                    if ((x > y) == up) {
-                        skey[t] = y; skey[p] = x;
-                        uint32_t tv = sval[t]; sval[t] = sval[p]; sval[p] = tv;
-                    }
-                }
+    const uint64_t lt = (1ull << lane) - 1ull;
+    int cur = 0;
+    for (uint32_t sh = 0; sh < a.rank_bits; sh += 8) {
+        hist[tid] = 0;
+        run[tid] = 0;
+#pragma unroll
+        for (int q = 0; q < NT / 64; ++q) wcnt[q][tid] = 0;
+        __syncthreads();
+        for (uint32_t j = tid; j < n; j += NT) atomicAdd(&hist[(kbuf[cur][j] >> sh) & 0xFFu], 1u);
+        __syncthreads();
+        uint32_t tot;
+        const uint32_t base = block_excl_scan<NT>(hist[tid], wsum, &tot);
+        hist[tid] = base; /* hist now holds each digit's first output slot */
+        __syncthreads();
+        for (uint32_t r0 = 0; r0 < n; r0 += NT) {
+            const uint32_t j = r0 + tid;
+            const bool valid = j < n;
+            uint32_t key = 0, val = 0, dg = 0;
+            if (valid) { key = kbuf[cur][j]; val = vbuf[cur][j]; dg = (key >> sh) & 0xFFu; }
+            uint64_t m = __ballot(valid);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                bool bit = (dg >> b) & 1u;
+                uint64_t bb = __ballot(valid && bit);
+                m &= bit ? bb : ~bb;
+            }
+            const uint32_t lrank = (uint32_t)__popcll(m & lt);
+            if (valid && lrank == 0) wcnt[w][dg] = (uint32_t)__popcll(m);
+            __syncthreads();
+            if (valid) {
+                uint32_t pos = hist[dg] + run[dg] + lrank;
+                for (uint32_t q = 0; q < w; ++q) pos += wcnt[q][dg];
+                kbuf[cur ^ 1][pos] = key;
+                vbuf[cur ^ 1][pos] = val;
             }
             __syncthreads();
+            uint32_t add = 0;
+#pragma unroll
+            for (int q = 0; q < NT / 64; ++q) { add += wcnt[q][tid]; wcnt[q][tid] = 0; }
+            run[tid] += add;
+            __syncthreads();
         }
+        cur ^= 1;
     }
-    for (uint32_t j = threadIdx.x; j < n; j += NT) k5_emit(a, ob + j, id, ds, skey[j], sval[j]);
+    for (uint32_t j = tid; j < n; j += NT) k5_emit(a, ob + j, id, ds, kbuf[cur][j], vbuf[cur][j]);
 }
 int launch_score_order(const K5Args& a, hipStream_t s) {
     if (!a.ndocs) return 0;
-    k_score_order<<<a.ndocs, NT, 0, s>>>(a);
+    k_score_small<<<(a.ndocs + NT / 64 - 1) / (NT / 64), NT, 0, s>>>(a);
+    k_score_large<<<a.ndocs, NT, 0, s>>>(a);
     return ok();
 }
 

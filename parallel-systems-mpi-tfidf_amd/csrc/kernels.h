@@ -56,7 +56,12 @@ struct K1Out {
     uint8_t* doc_flags;
     uint32_t* status;
     unsigned long long* ntokens;
+    unsigned long long* stamps;  /* diagnostic build only: K1_NSTAMP phase cycle sums, WG count,
+                                    then K1_NCOUNT event counters */
 };
+#define K1_NSTAMP 12
+#define K1_NCOUNT 4   /* segments, flushes, tokens taking the full probe, probe iterations */
+#define K1_STAMP_WORDS (K1_NSTAMP + 1 + K1_NCOUNT)
 
 /* K0: chunk boundaries; chunk_start has nchunks+1 entries, chunk_doc nchunks */
 int launch_plan_chunks(const CorpusDev& c, uint64_t nchunks, uint64_t* chunk_start, uint32_t* chunk_doc,
@@ -64,6 +69,11 @@ int launch_plan_chunks(const CorpusDev& c, uint64_t nchunks, uint64_t* chunk_sta
 /* K1: tokenize + per-document term counts for chunks [c0, c1) */
 int launch_tokcount(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc,
                     uint64_t c0, uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s);
+
+/* K1 fast path for whitespace-separated documents (tokcount_ws.hip) */
+int launch_docs_ws_sep(const CorpusDev& c, uint32_t* flag, hipStream_t s);
+int launch_tokcount_ws(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc, uint64_t c0,
+                       uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s);
 
 /* vocabulary finalisation */
 int launch_vocab_flags(const VocabDev& v, uint64_t cap, uint32_t* flags, hipStream_t s);
@@ -108,6 +118,7 @@ struct K5Args {
     const uint32_t* idf_idx;     /* df value -> index into idf */
     const double* idf;
     uint32_t ndocs;
+    uint32_t rank_bits;          /* bits of the largest term rank (radix passes) */
     uint64_t rec_total;          /* bounds guard: records in rec_slot/rec_cnt */
     uint64_t slot_cap;           /* bounds guard: vocabulary capacity */
     uint32_t* status;            /* ST_BOUNDS set instead of faulting */

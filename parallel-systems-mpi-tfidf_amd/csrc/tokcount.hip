@@ -23,6 +23,7 @@
  *   a radix sort later (finalize.hip).
  */
 #include "dev_common.h"
+#include "dev_vocab.h"
 #include "kernels.h"
 
 namespace {
@@ -38,7 +39,6 @@ constexpr int FLUSH_THR = 384;              /* flush at the next document bounda
 constexpr int FDOCS = 256;                  /* documents per flush epoch */
 constexpr int WDS_CAP = 256;                /* document starts listed per window */
 constexpr uint32_t LEN_OPEN = 0xFFFFu;      /* token end not within the staged bytes */
-constexpr uint32_t MAX_PROBE = 1u << 20;
 
 /* upper_bound(doc_off[lo..hi), x) - 1 : document containing absolute byte x */
 __device__ uint32_t doc_containing(const uint64_t* __restrict__ doc_off, uint32_t lo, uint32_t hi, uint64_t x) {
@@ -69,47 +69,6 @@ __device__ __forceinline__ uint4 load16_guarded(const uint8_t* __restrict__ byte
 
 }  // namespace
 
-/* Lock-free find-or-insert of a 128-bit key into the global vocabulary.
- * A slot is {lo, hi}; hi is the claim word: EMPTY -> PENDING (CAS) -> key (exchange)
- * after lo has been exchanged in, so a 16-byte snapshot whose hi is a real key always
- * carries its lo.  Plain loads may return stale EMPTY/PENDING lines from this XCD's L2;
- * those cases are re-read at the memory side with atomics (MI355X L2s are not coherent
- * across XCDs, device-scope atomics are). */
-__device__ uint32_t vocab_insert(const VocabDev v, uint64_t klo, uint64_t khi, uint64_t rep, uint32_t* status) {
-    uint64_t h = key_hash(klo, khi) & v.mask;
-    for (uint32_t probe = 0; probe < MAX_PROBE && probe <= v.mask; ++probe, h = (h + 1) & v.mask) {
-        unsigned long long* slot = reinterpret_cast<unsigned long long*>(&v.keys[h]);
-        uint4 s = v.keys[h];
-        uint64_t lo = ((uint64_t)s.y << 32) | s.x, hi = ((uint64_t)s.w << 32) | s.z;
-        if (hi == khi && lo == klo) return (uint32_t)h;
-        if (hi != KEY_EMPTY_HI && hi != KEY_PENDING_HI) continue;
-        if (hi == KEY_EMPTY_HI) {
-            unsigned long long old = atomicCAS(&slot[1], (unsigned long long)KEY_EMPTY_HI,
-                                               (unsigned long long)KEY_PENDING_HI);
-            if (old == KEY_EMPTY_HI) {
-                atomicExch(&slot[0], (unsigned long long)klo);
-                if ((khi >> 56) == 0xFFu) v.rep[h] = rep;
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                atomicExch(&slot[1], (unsigned long long)khi);
-                return (uint32_t)h;
-            }
-            hi = old;
-        }
-        uint32_t spins = 0;
-        while (hi == KEY_PENDING_HI) {
-            __builtin_amdgcn_s_sleep(2);
-            hi = atomicOr(&slot[1], 0ull);
-            if (++spins > (1u << 24)) { atomicOr(status, ST_VOCAB_SPIN); return INVALID_SLOT; }
-        }
-        if (hi == khi) {
-            lo = atomicOr(&slot[0], 0ull);
-            if (lo == klo) return (uint32_t)h;
-        }
-    }
-    atomicOr(status, ST_VOCAB_FULL);
-    return INVALID_SLOT;
-}
-
 /* ----------------------------------------------------------------- K0 ----- */
 
 __global__ void k_plan_chunks(CorpusDev c, uint64_t nchunks, uint64_t* __restrict__ chunk_start,
@@ -119,7 +78,7 @@ __global__ void k_plan_chunks(CorpusDev c, uint64_t nchunks, uint64_t* __restric
     uint64_t b = c.lo + i * (uint64_t)CHUNK_BYTES;
     if (i == nchunks || b >= c.hi) {
         chunk_start[i] = c.hi;
-        if (i < nchunks) chunk_doc[i] = c.ndocs;
+        chunk_doc[i] = c.ndocs ? c.ndocs - 1 : 0;
         return;
     }
     uint32_t d = doc_containing(c.doc_off, 0, c.ndocs + 1, b); /* doc_off[d] <= b < doc_off[d+1] */
@@ -140,8 +99,7 @@ int launch_plan_chunks(const CorpusDev& c, uint64_t nchunks, uint64_t* chunk_sta
 struct K1Shared {
     uint8_t bytes[WIN + LOOK + 32];     /* staged window (16-B aligned) */
     uint32_t tok[MAXTOK];               /* (offset << 16) | length */
-    uint64_t klo[TBL];
-    uint64_t khi[TBL];
+    ulonglong2 key[TBL];                /* {lo, hi}: one 128-bit LDS write publishes a key */
     uint32_t tdoc[TBL];
     uint32_t tcnt[TBL];
     uint16_t ws[NGRP];                  /* whitespace mask per group */
@@ -187,9 +145,9 @@ __device__ void k1_flush(K1Shared& S, const CorpusDev& c, const VocabDev& v, con
         for (int s = tid; s < TBL; s += NT) {
             uint32_t d = S.tdoc[s];
             if (d == DOC_NONE) continue;
-            uint64_t lo = S.klo[s], hi = S.khi[s];
+            uint64_t lo = S.key[s].x, hi = S.key[s].y;
             uint32_t g = (hi == KEY_GSLOT_TAG) ? (uint32_t)lo : vocab_insert(v, lo, hi, 0, o.status);
-            S.klo[s] = g;
+            S.key[s].x = g;
             uint32_t rel = d - elo;
             if (S.dcomplete[rel]) atomicAdd(&S.dcnt[rel], 1u);
             else atomicAdd(&S.npart, 1u);
@@ -213,7 +171,7 @@ __device__ void k1_flush(K1Shared& S, const CorpusDev& c, const VocabDev& v, con
         for (int s = tid; s < TBL; s += NT) {
             uint32_t d = S.tdoc[s];
             if (d == DOC_NONE) continue;
-            uint32_t g = (uint32_t)S.klo[s], cnt = S.tcnt[s], rel = d - elo;
+            uint32_t g = (uint32_t)S.key[s].x, cnt = S.tcnt[s], rel = d - elo;
             if (S.dcomplete[rel]) {
                 uint64_t pos = rb + S.doff[rel] + atomicAdd(&S.dfill[rel], 1u);
                 if (rec_ok) { o.rec_slot[pos] = g; o.rec_cnt[pos] = cnt; }
@@ -240,8 +198,7 @@ __device__ void k1_flush(K1Shared& S, const CorpusDev& c, const VocabDev& v, con
     for (int s = tid; s < TBL; s += NT) {
         S.tdoc[s] = DOC_NONE;
         S.tcnt[s] = 0;
-        S.khi[s] = KEY_EMPTY_HI;
-        S.klo[s] = 0;
+        S.key[s] = make_ulonglong2(0ull, KEY_EMPTY_HI);
     }
     if (tid < FDOCS) S.dsize[tid] = 0;
     if (tid == 0) {
@@ -264,7 +221,7 @@ __global__ __launch_bounds__(NT, 2) void k_tokcount(CorpusDev c, const uint64_t*
     uint32_t carry = chunk_doc[chunk]; /* document containing byte cs */
 
     for (int s = tid; s < TBL; s += NT) {
-        S.tdoc[s] = DOC_NONE; S.tcnt[s] = 0; S.khi[s] = KEY_EMPTY_HI; S.klo[s] = 0;
+        S.tdoc[s] = DOC_NONE; S.tcnt[s] = 0; S.key[s] = make_ulonglong2(0ull, KEY_EMPTY_HI);
     }
     if (tid < FDOCS) S.dsize[tid] = 0;
     if (tid == 0) {
@@ -460,15 +417,16 @@ __global__ __launch_bounds__(NT, 2) void k_tokcount(CorpusDev c, const uint64_t*
                 }
                 /* LDS (doc, key) table */
                 uint32_t h = (uint32_t)key_hash(klo ^ ((uint64_t)d * 0x9E3779B97F4A7C15ull), khi) & (TBL - 1);
+                /* claim-once slots, keys published by one 128-bit LDS write; a reader sees
+                 * the EMPTY sentinel (retry) or the final key (see tokcount_ws.hip) */
                 for (uint32_t guard = 0;; ++guard) {
-                    if (guard > (1u << 22)) { atomicOr(o.status, ST_VOCAB_SPIN); break; }
+                    if (guard > (1u << 16)) { atomicOr(o.status, ST_VOCAB_SPIN); break; }
+                    asm volatile("" ::: "memory");
                     uint32_t td = S.tdoc[h];
                     if (td == DOC_NONE) {
                         uint32_t old = atomicCAS(&S.tdoc[h], DOC_NONE, d);
                         if (old == DOC_NONE) {
-                            /* publish: klo, then khi with release (a reader that sees khi sees klo) */
-                            S.klo[h] = klo;
-                            __hip_atomic_store(&S.khi[h], khi, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            S.key[h] = make_ulonglong2(klo, khi);
                             atomicAdd(&S.tcnt[h], 1u);
                             atomicAdd(&S.fill, 1u);
                             break;
@@ -476,9 +434,9 @@ __global__ __launch_bounds__(NT, 2) void k_tokcount(CorpusDev c, const uint64_t*
                         td = old;
                     }
                     if (td == d) {
-                        uint64_t kh = __hip_atomic_load(&S.khi[h], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        if (kh == KEY_EMPTY_HI) continue;      /* claimer still publishing: retry */
-                        if (kh == khi && S.klo[h] == klo) { atomicAdd(&S.tcnt[h], 1u); break; }
+                        const ulonglong2 kk = S.key[h];
+                        if (kk.y == KEY_EMPTY_HI) { __builtin_amdgcn_s_sleep(1); continue; }
+                        if (kk.y == khi && kk.x == klo) { atomicAdd(&S.tcnt[h], 1u); break; }
                     }
                     h = (h + 1) & (TBL - 1);
                 }

@@ -12,7 +12,9 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libtfidf_hip.so")
+# TFIDF_LIB=stamps selects the diagnostic build (K1 phase stamps); never used for benches
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libtfidf_hip_stamps.so" if os.environ.get("TFIDF_LIB") == "stamps"
+                        else "libtfidf_hip.so")
 CLI_PATH = os.path.join(PKG_DIR, "bin", "tfidf")
 
 TFIDF_CORPUS_DEVICE = 1
@@ -51,7 +53,7 @@ class RunInfo(C.Structure):
         ("nbytes", C.c_uint64), ("ntokens", C.c_uint64), ("npairs", C.c_uint64), ("nterms", C.c_uint32),
         ("nterms_global", C.c_uint32), ("nchunks", C.c_uint64), ("partial_records", C.c_uint64),
         ("ndocs", C.c_uint32), ("vocab_capacity", C.c_uint32), ("ms_total", C.c_double),
-        ("ms_tokcount", C.c_double), ("ms_stage", C.c_double * 16), ("nstages", C.c_uint32), ("pad_", C.c_uint32),
+        ("ms_tokcount", C.c_double), ("ms_stage", C.c_double * 16), ("nstages", C.c_uint32), ("flags", C.c_uint32),
     ]
 
 
@@ -173,7 +175,7 @@ class Engine:
     def info(self) -> dict:
         r = RunInfo()
         _chk(lib().tfidf_last_run_info(self.h, C.byref(r)), "tfidf_last_run_info")
-        d = {k: getattr(r, k) for k, _ in RunInfo._fields_ if k not in ("ms_stage", "pad_")}
+        d = {k: getattr(r, k) for k, _ in RunInfo._fields_ if k != "ms_stage"}
         d["stages"] = {lib().tfidf_stage_name(i).decode(): r.ms_stage[i] for i in range(r.nstages)}
         return d
 

@@ -56,5 +56,31 @@ def rccl1():
     print("rccl1 equal:", res["output_txt"] == ora["output_txt"])
 
 
+def stamps():
+    """K1 phase breakdown (diagnostic build): TFIDF_LIB=stamps TFIDF_STAMPS=1"""
+    import ctypes as C
+    names = ["group setup", "stage", "compact+tokdoc", "docsize", "seg decide", "insert", "flush:enter",
+             "flush:A compact", "flush:B vocab", "flush:C alloc", "flush:D write", "kernel end"]
+    p = tfidf_configs.plan("c2", scale=float(os.environ.get("SCALE", "1.0")))
+    with tfidf_abi.Engine(0) as e:
+        c = e.synth_device(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"], p["ndocs_total"])
+        for _ in range(2):
+            e.run_corpus(c)
+        info = e.info()
+        buf = (C.c_uint64 * 17)()
+        L = tfidf_abi.lib()
+        L.tfidf_debug_k1_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        n = L.tfidf_debug_k1_stamps(e.h, buf, 17)
+        # the second run accumulated counters once (stamps are reset per run)
+        print("tokens", info["ntokens"], "segments", buf[13], "mid/clean flushes", buf[14],
+              "full-probe tokens", buf[15], "probe iterations", buf[16])
+    print("k1 ms", info["ms_tokcount"], "flags", info["flags"], "stamps", n)
+    wgs = buf[12]
+    tot = sum(buf[:12])
+    for k in range(12):
+        print("%-18s %12.0f cyc/WG  %5.1f%%" % (names[k], buf[k] / max(wgs, 1), 100.0 * buf[k] / max(tot, 1)))
+    print("WGs", wgs, "total cyc/WG", tot / max(wgs, 1))
+
+
 if __name__ == "__main__":
     globals()[sys.argv[1]]()

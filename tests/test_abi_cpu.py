@@ -32,9 +32,15 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_library_is_gfx950_code_object():
+    """The shared library embeds gfx950 code objects (objdump extracts the offload
+    bundles next to its input, so work on a copy in a scratch directory)."""
+    import shutil
     import subprocess
-    p = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", tfidf_abi.LIB_PATH],
-                       capture_output=True, text=True)
+    with tempfile.TemporaryDirectory() as td:
+        lib_copy = os.path.join(td, "lib.so")
+        shutil.copy(tfidf_abi.LIB_PATH, lib_copy)
+        p = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", lib_copy],
+                           capture_output=True, text=True, cwd=td)
     assert "gfx950" in (p.stdout + p.stderr)
 
 

@@ -216,3 +216,22 @@ def test_full_c2_properties():
     N = r["ndocs_total"]
     ref = (cnt / r["docsize"].astype(np.float64)) * np.log(N / r["df"].astype(np.float64))
     np.testing.assert_allclose(r["score"], ref, rtol=1e-12, atol=1e-300)
+
+
+@pytest.mark.parametrize("cfg,scale", [("c2", 0.002), ("c5", 0.0005)])
+def test_general_and_fast_k1_agree(cfg, scale):
+    """The whitespace-separated fast K1 and the general K1 give identical results."""
+    p = tfidf_configs.plan(cfg, scale=scale)
+    data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
+    outs = []
+    for mode in ("auto", "general"):
+        os.environ["TFIDF_K1"] = mode
+        try:
+            with tfidf_abi.Engine(0) as e:
+                e.run_host(data, off, p["doc_ids"], p["ndocs_total"])
+                assert bool(e.info()["flags"] & 1) == (mode == "auto")
+                outs.append(e.fetch())
+        finally:
+            os.environ.pop("TFIDF_K1", None)
+    assert_same_result(outs[0], outs[1])
+    assert_same_result(outs[0], oracle_py.run(data, off, p["doc_ids"], p["ndocs_total"]))
