@@ -127,7 +127,8 @@ typedef struct tfidf_run_info {
     uint32_t nstages;
     uint32_t flags;           /* TFIDF_RUN_* */
 } tfidf_run_info;
-#define TFIDF_RUN_K1_FAST 1u  /* whitespace-separated documents: fast tokenize+count kernel */
+#define TFIDF_RUN_K1_FAST 1u  /* whitespace-separated kernel (diagnostic, TFIDF_K1=ws) */
+#define TFIDF_RUN_K1_VS   2u  /* slot-keyed tokenize+count kernel (the default path) */
 int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info);
 const char* tfidf_stage_name(int stage);
 /* Enables per-stage HIP event timing (adds a few event records per run). */

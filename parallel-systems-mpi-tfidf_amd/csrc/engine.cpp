@@ -72,10 +72,11 @@ struct tfidf_ctx {
     ncclComm_t comm = nullptr;
     int rank = 0, nranks = 1;
     bool timing = true;
-    int k1_mode = 0;        /* 0 auto, 2 force the general K1 (env TFIDF_K1=general) */
+    int k1_mode = 0;        /* 0 auto, 2 general K1 (env TFIDF_K1=general), 3 ws K1 (TFIDF_K1=ws) */
     bool stamps_on = false; /* env TFIDF_STAMPS=1 with the diagnostic library build */
     DevBuf stamps;
-    bool k1_fast = false;   /* last run used the whitespace-separated fast path */
+    bool k1_fast = false;   /* last run used the whitespace-separated kernel (TFIDF_K1=ws) */
+    bool k1_vs = false;     /* last run used the slot-keyed kernel (default) */
     hipEvent_t ev[S_NSTAGES + 1];
     Arena arena;
     DevBuf arena_buf;
@@ -176,6 +177,7 @@ int tfidf_open(int device, tfidf_ctx** out) {
     ctx->device = device;
     const char* km = getenv("TFIDF_K1");
     if (km && !strcmp(km, "general")) ctx->k1_mode = 2;
+    if (km && !strcmp(km, "ws")) ctx->k1_mode = 3;
     const char* ks = getenv("TFIDF_STAMPS");
     ctx->stamps_on = ks && ks[0] == '1';
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
@@ -323,15 +325,19 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     HIPCHK(hipMemsetAsync(ctx->doc_size.p, 0, (size_t)N * 4 + 4, s));
     HIPCHK(hipMemsetAsync(ctx->doc_flags.p, 0, (size_t)N + 1, s));
     if (nchunks) LCHK(launch_plan_chunks(c, nchunks, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), s));
-    /* K1 variant: whitespace-separated documents take the fast path */
+    /* K1 variant: the slot-keyed kernel (tokcount_vs.hip) needs a 16-byte aligned corpus
+     * base; TFIDF_K1=general / =ws select the older kernels (cross-checks, diagnostics) */
     uint32_t not_ws_sep = 1;
-    if (nchunks && ctx->k1_mode != 2) {
+    if (nchunks && ctx->k1_mode == 3) {
         LCHK(launch_docs_ws_sep(c, (uint32_t*)(cnt + 4), s));
         HIPCHK(hipMemcpyAsync(&not_ws_sep, cnt + 4, 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
     }
-    /* the fast path's clamped 16-byte group loads need a 16-byte aligned corpus base */
-    ctx->k1_fast = (not_ws_sep == 0) && ctx->k1_mode != 2 && (((uintptr_t)c.bytes & 15u) == 0);
+    const bool aligned = (((uintptr_t)c.bytes & 15u) == 0);
+    ctx->k1_fast = false;
+    ctx->k1_vs = aligned && ctx->k1_mode == 0;
+    if (ctx->k1_mode == 3) ctx->k1_fast = (not_ws_sep == 0) && aligned;
+    if (ctx->k1_vs && ctx->vcap > K1_VS_MAX_CAP) return TFIDF_E_CAPACITY;
     /* ---- K1 ---- */
     mark(ctx, S_TOKCOUNT);
     VocabDev vd{ctx->vkeys.as<uint4>(), ctx->vrep.as<uint64_t>(), ctx->vcap - 1};
@@ -357,7 +363,9 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
         HIPCHK(hipMemsetAsync(ctx->stamps.p, 0, 8 * K1_STAMP_WORDS, s));
         o.stamps = ctx->stamps.as<unsigned long long>();
     }
-    if (nchunks && ctx->k1_fast)
+    if (nchunks && ctx->k1_vs)
+        LCHK(launch_tokcount_vs(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
+    else if (nchunks && ctx->k1_fast)
         LCHK(launch_tokcount_ws(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
     else if (nchunks)
         LCHK(launch_tokcount(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
@@ -372,6 +380,10 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     ctx->nrec_part = Q;
     if (st & ST_VOCAB_SPIN) return TFIDF_E_CAPACITY;
     bool retry = false;
+    if (st & ST_BOUNDS) {
+        fprintf(stderr, "tfidf: internal bounds check tripped in K1 (status 0x%x)\n", st);
+        return TFIDF_E_STATE;
+    }
     if (st & ST_VOCAB_FULL) { ctx->vcap *= 4; retry = true; }
     if (st & ST_REC_FULL) { ctx->rec_cap = R_main + R_main / 4 + 4096; retry = true; }
     if (st & ST_PART_FULL) { ctx->part_cap = Q + Q / 4 + 4096; retry = true; }
@@ -650,7 +662,7 @@ extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info) {
     info->ms_tokcount = ctx->ms_stage[S_TOKCOUNT];
     for (int i = 0; i < S_NSTAGES; ++i) info->ms_stage[i] = ctx->ms_stage[i];
     info->nstages = S_NSTAGES;
-    info->flags = ctx->k1_fast ? TFIDF_RUN_K1_FAST : 0u;
+    info->flags = (ctx->k1_fast ? TFIDF_RUN_K1_FAST : 0u) | (ctx->k1_vs ? TFIDF_RUN_K1_VS : 0u);
     return TFIDF_OK;
 }
 

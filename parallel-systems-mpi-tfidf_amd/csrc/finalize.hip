@@ -315,7 +315,7 @@ int launch_gather_npairs(const uint32_t* order, const uint32_t* doc_npairs, uint
 
 /* ------------------------------------------------------ score + order (K5) */
 
-constexpr int K5_MAX = 2048;
+constexpr int K5_MAX = K5_MAX_PAIRS;
 
 __device__ __forceinline__ void k5_emit(const K5Args& a, uint64_t o, uint32_t id, uint32_t ds, uint32_t rank,
                                         uint32_t cnt) {

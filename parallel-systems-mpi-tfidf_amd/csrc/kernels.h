@@ -12,6 +12,7 @@
 #define K1_WIN       (K1_NT * 16)        /* bytes per window: one 16-byte group per thread */
 #define CHUNK_BYTES  16384u              /* nominal chunk (work unit) size */
 #define BIG_DOC      65536u              /* documents longer than this are split across chunks */
+#define K5_MAX_PAIRS 2048                /* largest complete (unmerged) document K5 sorts in LDS */
 
 /* status bits (device word) */
 #define ST_VOCAB_FULL  1u
@@ -69,6 +70,12 @@ int launch_plan_chunks(const CorpusDev& c, uint64_t nchunks, uint64_t* chunk_sta
 /* K1: tokenize + per-document term counts for chunks [c0, c1) */
 int launch_tokcount(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc,
                     uint64_t c0, uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s);
+
+/* K1 main path (tokcount_vs.hip): 16-byte aligned corpus base; returns -3 when the
+ * vocabulary capacity exceeds the LDS entry's slot field */
+int launch_tokcount_vs(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc, uint64_t c0,
+                       uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s);
+#define K1_VS_MAX_CAP (1ull << 28)
 
 /* K1 fast path for whitespace-separated documents (tokcount_ws.hip) */
 int launch_docs_ws_sep(const CorpusDev& c, uint32_t* flag, hipStream_t s);

@@ -218,20 +218,70 @@ def test_full_c2_properties():
     np.testing.assert_allclose(r["score"], ref, rtol=1e-12, atol=1e-300)
 
 
-@pytest.mark.parametrize("cfg,scale", [("c2", 0.002), ("c5", 0.0005)])
-def test_general_and_fast_k1_agree(cfg, scale):
-    """The whitespace-separated fast K1 and the general K1 give identical results."""
+@pytest.mark.parametrize("cfg,scale", [("c2", 0.002), ("c5", 0.0005), ("c4", 0.001)])
+def test_k1_variants_agree(cfg, scale):
+    """The slot-keyed K1 (default), the general K1 and the whitespace-separated K1 give
+    identical results, equal to the oracle."""
     p = tfidf_configs.plan(cfg, scale=scale)
     data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
     outs = []
-    for mode in ("auto", "general"):
+    for mode, flag in (("auto", 2), ("general", 0), ("ws", 1)):
         os.environ["TFIDF_K1"] = mode
         try:
             with tfidf_abi.Engine(0) as e:
                 e.run_host(data, off, p["doc_ids"], p["ndocs_total"])
-                assert bool(e.info()["flags"] & 1) == (mode == "auto")
+                assert (e.info()["flags"] & 3) == flag
                 outs.append(e.fetch())
         finally:
             os.environ.pop("TFIDF_K1", None)
-    assert_same_result(outs[0], outs[1])
-    assert_same_result(outs[0], oracle_py.run(data, off, p["doc_ids"], p["ndocs_total"]))
+    ora = oracle_py.run(data, off, p["doc_ids"], p["ndocs_total"])
+    for o in outs:
+        assert_same_result(o, ora)
+
+
+def _distinct_words(n, rng, lo=2, hi=12):
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz", dtype=np.uint8)
+    words = set()
+    while len(words) < n:
+        L = int(rng.integers(lo, hi + 1))
+        words.add(bytes(alpha[rng.integers(0, 26, L)]))
+    return sorted(words)
+
+
+def test_doc_with_more_pairs_than_lds_table(engine):
+    """One ~60 KB document (a single chunk) with ~7000 distinct terms: the open document
+    overflows the LDS table (partial flushes) and exceeds K5's in-LDS sort size."""
+    rng = np.random.default_rng(11)
+    words = _distinct_words(7000, rng)
+    toks = [words[i] for i in rng.permutation(len(words))] + [words[i] for i in rng.integers(0, 300, 1500)]
+    docs = [b"x y z\n", b" ".join(toks)[:63000] + b"\n", b"x q\n"]
+    check_vs_oracle(engine, *docs_to_arrays(docs))
+
+
+def test_complete_doc_over_k5_limit(engine):
+    """~2500 distinct terms in a 25 KB document: complete inside one chunk but larger than
+    K5's in-LDS sort, so it is routed through the partial merge."""
+    rng = np.random.default_rng(12)
+    words = _distinct_words(2500, rng, 3, 8)
+    docs = [b" ".join(words[i] for i in rng.permutation(len(words))) + b"\n", b"a b\n"]
+    check_vs_oracle(engine, *docs_to_arrays(docs))
+
+
+def test_many_tiny_docs_without_separators(engine):
+    """Thousands of 0-6 byte documents, most with no trailing whitespace: document starts
+    are token boundaries, more documents per chunk than one LDS document group."""
+    rng = np.random.default_rng(13)
+    pool = [b"a", b"b", b"ab", b"ba", b"abc", b" ", b"", b"c\t", b"\nd", b"ee ee"]
+    docs = [pool[i] for i in rng.integers(0, len(pool), 5000)]
+    check_vs_oracle(engine, *docs_to_arrays(docs))
+
+
+def test_big_docs_split_across_chunks(engine):
+    """Documents far above BIG_DOC are split across work units mid-token; their partial
+    counts are merged."""
+    rng = np.random.default_rng(14)
+    words = _distinct_words(3000, rng, 1, 20)
+    z = rng.zipf(1.3, 60000) % len(words)
+    big = b" ".join(words[i] for i in z)
+    docs = [big, b"tail words here", big[:200000], b"", big[5:] + b"\n"]
+    check_vs_oracle(engine, *docs_to_arrays(docs))
