@@ -98,15 +98,36 @@ __device__ __forceinline__ void make_long_key(const uint8_t* p, uint64_t n, uint
 
 __device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
 
-/* ---- wave / block scans (wave64) ---- */
+/* ---- wave64 cross-lane primitives on DPP (GFX9-family data-parallel primitives:
+ * no LDS traffic and no lane-index registers, unlike ds_bpermute-based shuffles) ---- */
+#define DPP_ROW_SHR(n)   (0x110 + (n))
+#define DPP_WAVE_SHL1    0x130   /* lane i reads lane i+1 */
+#define DPP_WAVE_SHR1    0x138   /* lane i reads lane i-1 */
+#define DPP_ROW_BCAST15  0x142
+#define DPP_ROW_BCAST31  0x143
+
+/* value of lane+1 (lane 63 gets its own value) */
+__device__ __forceinline__ uint32_t lane_next(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, DPP_WAVE_SHL1, 0xF, 0xF, false);
+}
+/* value of lane-1 (lane 0 gets its own value) */
+__device__ __forceinline__ uint32_t lane_prev(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, DPP_WAVE_SHR1, 0xF, 0xF, false);
+}
+
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_SHR(1), 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_SHR(2), 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_SHR(4), 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_SHR(8), 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_BCAST15, 0xA, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_BCAST31, 0xC, 0xF, false);
     return v;
+}
+
+/* sum over the wave, uniform (scalar) result */
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(v), 63);
 }
 
 /* exclusive scan over the block (blockDim = NT, multiple of 64); wsum: NT/64 words LDS.

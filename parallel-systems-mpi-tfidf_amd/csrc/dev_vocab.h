@@ -14,11 +14,12 @@
  * carries its lo.  Plain loads may return stale EMPTY/PENDING lines from this XCD's L2;
  * those cases are re-read at the memory side with atomics (MI355X L2s are not coherent
  * across XCDs, device-scope atomics are). */
-__device__ __noinline__ uint32_t vocab_insert(const VocabDev v, uint64_t klo, uint64_t khi, uint64_t rep, uint32_t* status) {
-    uint64_t h = key_hash(klo, khi) & v.mask;
-    for (uint32_t probe = 0; probe < VOCAB_MAX_PROBE && probe <= v.mask; ++probe, h = (h + 1) & v.mask) {
-        unsigned long long* slot = reinterpret_cast<unsigned long long*>(&v.keys[h]);
-        uint4 s = v.keys[h];
+__device__ __forceinline__ uint32_t vocab_insert_s(uint4* __restrict__ keys, uint64_t* __restrict__ reps, uint64_t mask,
+                                                uint64_t klo, uint64_t khi, uint64_t rep, uint32_t* status) {
+    uint64_t h = key_hash(klo, khi) & mask;
+    for (uint32_t probe = 0; probe < VOCAB_MAX_PROBE && probe <= mask; ++probe, h = (h + 1) & mask) {
+        unsigned long long* slot = reinterpret_cast<unsigned long long*>(&keys[h]);
+        uint4 s = keys[h];
         uint64_t lo = ((uint64_t)s.y << 32) | s.x, hi = ((uint64_t)s.w << 32) | s.z;
         if (hi == khi && lo == klo) return (uint32_t)h;
         if (hi != KEY_EMPTY_HI && hi != KEY_PENDING_HI) continue;
@@ -27,7 +28,7 @@ __device__ __noinline__ uint32_t vocab_insert(const VocabDev v, uint64_t klo, ui
                                                (unsigned long long)KEY_PENDING_HI);
             if (old == KEY_EMPTY_HI) {
                 atomicExch(&slot[0], (unsigned long long)klo);
-                if ((khi >> 56) == 0xFFu) v.rep[h] = rep;
+                if ((khi >> 56) == 0xFFu) reps[h] = rep;
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 atomicExch(&slot[1], (unsigned long long)khi);
                 return (uint32_t)h;
@@ -47,6 +48,10 @@ __device__ __noinline__ uint32_t vocab_insert(const VocabDev v, uint64_t klo, ui
     }
     atomicOr(status, ST_VOCAB_FULL);
     return INVALID_SLOT;
+}
+__device__ __forceinline__ uint32_t vocab_insert(const VocabDev& v, uint64_t klo, uint64_t khi, uint64_t rep,
+                                                 uint32_t* status) {
+    return vocab_insert_s(v.keys, v.rep, v.mask, klo, khi, rep, status);
 }
 
 #endif

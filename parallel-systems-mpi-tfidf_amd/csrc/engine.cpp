@@ -74,6 +74,7 @@ struct tfidf_ctx {
     bool timing = true;
     int k1_mode = 0;        /* 0 auto, 2 general K1 (env TFIDF_K1=general), 3 ws K1 (TFIDF_K1=ws) */
     bool stamps_on = false; /* env TFIDF_STAMPS=1 with the diagnostic library build */
+    uint32_t ablate = 0;    /* env TFIDF_K1_ABLATE: K1 timing experiments, pipeline stops after K1 */
     DevBuf stamps;
     bool k1_fast = false;   /* last run used the whitespace-separated kernel (TFIDF_K1=ws) */
     bool k1_vs = false;     /* last run used the slot-keyed kernel (default) */
@@ -180,6 +181,8 @@ int tfidf_open(int device, tfidf_ctx** out) {
     if (km && !strcmp(km, "ws")) ctx->k1_mode = 3;
     const char* ks = getenv("TFIDF_STAMPS");
     ctx->stamps_on = ks && ks[0] == '1';
+    const char* ka = getenv("TFIDF_K1_ABLATE");
+    ctx->ablate = ka ? (uint32_t)strtoul(ka, nullptr, 0) : 0u;
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     for (int i = 0; i <= S_NSTAGES; ++i) HIPCHK(hipEventCreate(&ctx->ev[i]));
     if (arena_reset(ctx, 64ull << 20) != 0) { delete ctx; return TFIDF_E_NOMEM; }
@@ -358,6 +361,7 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     o.ntokens = cnt + 2;
     o.status = (uint32_t*)(cnt + 3);
     o.stamps = nullptr;
+    o.ablate = ctx->ablate;
     if (ctx->stamps_on) {
         ENSURE(ctx->stamps, 8 * K1_STAMP_WORDS);
         HIPCHK(hipMemsetAsync(ctx->stamps.p, 0, 8 * K1_STAMP_WORDS, s));
@@ -370,6 +374,13 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     else if (nchunks)
         LCHK(launch_tokcount(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
     mark(ctx, S_VOCAB);
+    if (ctx->ablate) { /* timing experiment: results are invalid, stop after K1 */
+        for (int st2 = S_MERGE; st2 <= S_NSTAGES; ++st2) mark(ctx, st2);
+        HIPCHK(hipStreamSynchronize(s));
+        ctx->V = 0;
+        ctx->npairs = 0;
+        return 0;
+    }
     unsigned long long hc[4];
     HIPCHK(hipMemcpyAsync(hc, cnt, sizeof hc, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));

@@ -57,6 +57,8 @@ struct K1Out {
     uint8_t* doc_flags;
     uint32_t* status;
     unsigned long long* ntokens;
+    uint32_t ablate;             /* timing experiments only (env TFIDF_K1_ABLATE; results invalid):
+                                    1 no vocabulary lookup, 2 no LDS counting, 4 no token walk */
     unsigned long long* stamps;  /* diagnostic build only: K1_NSTAMP phase cycle sums, WG count,
                                     then K1_NCOUNT event counters */
 };

@@ -15,7 +15,7 @@
  *             made once per step, identically in every thread, before any insert;
  *   resolve   each lane walks its own token starts: the 128-bit term key (dev_common.h;
  *             strcmp/NUL semantics) is cut from its 16 bytes plus its neighbour's
- *             (__shfl_down), hashed, and looked up in the HBM vocabulary (one 16-byte
+ *             (DPP lane shift), hashed, and looked up in the HBM vocabulary (one 16-byte
  *             load, L2-resident for Zipfian text; lock-free insert on a miss);
  *   insert    (document, slot) is counted in an LDS open-addressing table of u64
  *             entries  key(36 bits: doc-in-group 8 | slot 28) << 24 | count(24),
@@ -46,6 +46,35 @@ constexpr int GCAP = 256;                 /* documents per group (doc-in-group: 
 constexpr uint32_t SLOT_BITS = 28;
 constexpr uint32_t CNT_BITS = 24;
 constexpr uint64_t CNT_MASK = (1ull << CNT_BITS) - 1ull;
+constexpr int KB = 2;                     /* tokens per lane whose vocabulary loads fly together */
+
+/* Diagnostic build only (-DK1_STAMPS, lib/libtfidf_hip_stamps.so): thread 0 sums
+ * s_memtime cycles per phase and lane-level event counters; never in the measured
+ * library.  Phases: 0 group setup, 1 classify, 2 count+decide, 3 mid flush, 4 resolve+
+ * insert, 5 group flush, 6 docSize write.  Counters: tokens, first-probe misses,
+ * LDS probe iterations, wave token-loop iterations x 64. */
+#ifdef K1_STAMPS
+struct Stamps {
+    uint64_t prev;
+    uint64_t acc[K1_NSTAMP];
+};
+#define STAMP(st, k)                                                          \
+    do {                                                                      \
+        if (threadIdx.x == 0) {                                               \
+            __builtin_amdgcn_sched_barrier(0);                                \
+            uint64_t t_ = __builtin_amdgcn_s_memtime();                       \
+            __builtin_amdgcn_s_waitcnt(0xC07F);                               \
+            if ((st).prev) (st).acc[k] += t_ - (st).prev;                     \
+            (st).prev = t_;                                                   \
+            __builtin_amdgcn_sched_barrier(0);                                \
+        }                                                                     \
+    } while (0)
+#define CNT(k, n) (cnt_[k] += (n))
+#else
+struct Stamps {};
+#define STAMP(st, k) do { (void)(st); } while (0)
+#define CNT(k, n) ((void)0)
+#endif
 
 struct VsShared {
     unsigned long long T[TB];             /* (doc, slot) -> count */
@@ -63,9 +92,13 @@ struct VsShared {
     unsigned long long rec_base, part_base;
 };
 
+/* Streaming corpus load: clamped to the last 16-byte block holding corpus bytes, and
+ * non-temporal so the read-once corpus does not evict the vocabulary from L2. */
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 ld16c(const uint8_t* __restrict__ bytes, uint64_t last_blk, uint64_t pos) {
     const uint64_t p = pos < last_blk ? pos : last_blk;
-    return *reinterpret_cast<const uint4*>(bytes + p);
+    const u32x4 r = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(bytes + p));
+    return make_uint4(r.x, r.y, r.z, r.w);
 }
 
 /* bytes of [pos, pos+16) outside the shard's [lo, hi) read as whitespace */
@@ -107,9 +140,9 @@ __device__ __forceinline__ uint32_t tbl_hash(uint64_t key) {
     return (k * 0x85EBCA6Bu) >> (32 - 12);
 }
 
-/* counts (key, +n) into the table (entry claimed with count n or added to) */
-__device__ __forceinline__ bool tbl_add(VsShared& S, uint64_t key, uint32_t n, uint32_t* status) {
-    uint32_t h = tbl_hash(key) & (TB - 1);
+/* counts (key, +n) into the table probing from slot h (entry claimed with count n or
+ * added to); returns true when it claimed a new entry */
+__device__ __forceinline__ bool tbl_add_from(VsShared& S, uint64_t key, uint32_t h, uint32_t n, uint32_t* status) {
     const unsigned long long ent = (key << CNT_BITS) | n;
     for (int guard = 0; guard < TB; ++guard) {
         const unsigned long long old = atomicCAS(&S.T[h], 0ull, ent);
@@ -120,44 +153,34 @@ __device__ __forceinline__ bool tbl_add(VsShared& S, uint64_t key, uint32_t n, u
     atomicOr(status, ST_BOUNDS);
     return false;
 }
+__device__ __forceinline__ bool tbl_add(VsShared& S, uint64_t key, uint32_t n, uint32_t* status) {
+    return tbl_add_from(S, key, tbl_hash(key) & (TB - 1), n, status);
+}
 
 /* Term slot of a token whose term is >= 16 bytes or whose end lies past the 32 bytes a
  * lane holds: the token is re-read from HBM (rare for text). */
-__device__ __noinline__ uint32_t slow_slot(const CorpusDev& c, const VocabDev& v, uint64_t p0, uint64_t dend,
-                                           uint32_t* status) {
+__device__ __forceinline__ uint32_t slow_slot(const uint8_t* __restrict__ bytes, uint4* keys, uint64_t* reps,
+                                           uint64_t mask, uint64_t p0, uint64_t dend, uint32_t* status) {
+    const VocabDev v{keys, reps, mask};
     uint64_t p = p0;
-    while (p < dend && !is_ws(c.bytes[p])) ++p;
+    while (p < dend && !is_ws(bytes[p])) ++p;
     uint64_t n = 0;
-    while (p0 + n < p && c.bytes[p0 + n] != 0) ++n;
+    while (p0 + n < p && bytes[p0 + n] != 0) ++n;
     uint64_t klo, khi;
     if (n < 16) {
         uint64_t lo = 0, hi = 0;
         for (uint32_t k = 0; k < n; ++k) {
-            const uint64_t b = c.bytes[p0 + k];
+            const uint64_t b = bytes[p0 + k];
             if (k < 8) lo |= b << (8 * k); else hi |= b << (8 * (k - 8));
         }
         make_short_key(lo, hi, (uint32_t)n, &klo, &khi);
         return vocab_insert(v, klo, khi, 0, status);
     }
-    make_long_key(c.bytes + p0, n, &klo, &khi);
+    make_long_key(bytes + p0, n, &klo, &khi);
     const uint64_t rep = ((n < 0xFFFFFFull ? n : 0xFFFFFFull) << 40) | p0;
     return vocab_insert(v, klo, khi, rep, status);
 }
 
-/* Vocabulary slot of a short key: first probe inline, the rest in vocab_insert. */
-__device__ __forceinline__ uint32_t vocab_slot(const VocabDev& v, uint64_t klo, uint64_t khi, uint32_t* status) {
-    const uint64_t h = key_hash(klo, khi) & v.mask;
-    const uint4 s = v.keys[h];
-    if (s.x == (uint32_t)klo && s.y == (uint32_t)(klo >> 32) && s.z == (uint32_t)khi && s.w == (uint32_t)(khi >> 32))
-        return (uint32_t)h;
-    return vocab_insert(v, klo, khi, 0, status);
-}
-
-__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-    return x;
-}
 
 /* Writes table entries as records and clears the table.  Documents that ended at or
  * before `pos` (all of them when `final`) are emitted; the document open at `pos` is
@@ -203,8 +226,14 @@ __device__ uint32_t vs_flush(VsShared& S, const K1Out& o, uint32_t gd0, uint32_t
     if (tid < GCAP) S.doff[tid] = off;
     if (tid == 0) {
         const uint32_t nrec = tot & 0xFFFFu, npart = tot >> 16;
-        const unsigned long long rb = nrec ? atomicAdd(o.rec_alloc, (unsigned long long)nrec) : 0ull;
-        const unsigned long long pb = npart ? atomicAdd(o.part_alloc, (unsigned long long)npart) : 0ull;
+        unsigned long long rb = 0, pb = 0;
+        if (o.ablate & 8u) { /* timing experiment: no allocation atomics */
+            rb = ((unsigned long long)blockIdx.x * 4096ull) % (o.rec_cap > 8192 ? o.rec_cap - 8192 : 1);
+            pb = ((unsigned long long)blockIdx.x * 4096ull) % (o.part_cap > 8192 ? o.part_cap - 8192 : 1);
+        } else {
+            rb = nrec ? atomicAdd(o.rec_alloc, (unsigned long long)nrec) : 0ull;
+            pb = npart ? atomicAdd(o.part_alloc, (unsigned long long)npart) : 0ull;
+        }
         if (rb + nrec > o.rec_cap) atomicOr(o.status, ST_REC_FULL);
         if (pb + npart > o.part_cap) atomicOr(o.status, ST_PART_FULL);
         S.rec_base = rb;
@@ -222,28 +251,43 @@ __device__ uint32_t vs_flush(VsShared& S, const K1Out& o, uint32_t gd0, uint32_t
             o.doc_flags[gd0 + tid] = DF_PARTIAL;
         }
     }
-    /* pass 2: scatter emitted entries, clear the table, remember kept ones */
+    /* pass 2: stage emitted entries in the (already read) table in output order —
+     * complete records [0, nrec), partial records [nrec, nrec + npart) — so that the
+     * HBM writes below are coalesced; remember kept ones */
+    const uint32_t nrec = tot & 0xFFFFu, ntot = nrec + (tot >> 16);
     uint32_t keep = 0;
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
         if (!e[j]) continue;
         const uint32_t rel = (uint32_t)(e[j] >> (CNT_BITS + SLOT_BITS));
         const uint32_t slot = (uint32_t)(e[j] >> CNT_BITS) & ((1u << SLOT_BITS) - 1u);
-        const uint32_t cnt = (uint32_t)(e[j] & CNT_MASK);
+        const uint64_t cnt = e[j] & CNT_MASK;
         const uint8_t st = S.dstate[rel];
         if (st == 3) { keep |= 1u << j; continue; }
         const uint32_t k = atomicAdd(&S.drun[rel], 1u);
         const uint32_t dof = S.doff[rel];
-        if (st == 2) {
-            const uint64_t p = rb + (dof & 0xFFFFu) + k;
-            if (rec_ok) { o.rec_slot[p] = slot; o.rec_cnt[p] = cnt; }
-        } else {
-            const uint64_t p = pb + (dof >> 16) + k;
-            if (part_ok) { o.part_doc[p] = gd0 + rel; o.part_slot[p] = slot; o.part_cnt[p] = cnt; }
-        }
+        if (st == 2) S.T[(dof & 0xFFFFu) + k] = slot | (cnt << 32);
+        else S.T[nrec + (dof >> 16) + k] = slot | ((uint64_t)rel << SLOT_BITS) | (cnt << 36);
     }
+    __syncthreads();
+    /* coalesced write-out; each thread then clears exactly the entries it read */
 #pragma unroll
-    for (int j = 0; j < EPT; ++j) S.T[j * NT + tid] = 0ull;
+    for (int j = 0; j < EPT; ++j) {
+        const uint32_t i = j * NT + tid;
+        if (i < nrec) {
+            const unsigned long long w = S.T[i];
+            if (rec_ok) { o.rec_slot[rb + i] = (uint32_t)w; o.rec_cnt[rb + i] = (uint32_t)(w >> 32); }
+        } else if (i < ntot) {
+            const unsigned long long w = S.T[i];
+            const uint64_t q = pb + (i - nrec);
+            if (part_ok) {
+                o.part_doc[q] = gd0 + ((uint32_t)(w >> SLOT_BITS) & 0xFFu);
+                o.part_slot[q] = (uint32_t)w & ((1u << SLOT_BITS) - 1u);
+                o.part_cnt[q] = (uint32_t)(w >> 36);
+            }
+        }
+        S.T[i] = 0ull;
+    }
     __syncthreads();
     if (keep) {
 #pragma unroll
@@ -257,39 +301,65 @@ __device__ uint32_t vs_flush(VsShared& S, const K1Out& o, uint32_t gd0, uint32_t
 
 }  // namespace
 
+/* wave-uniform copy of a value the compiler keeps in VGPRs (LDS-loaded) */
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+}
+__device__ __forceinline__ uint32_t uni32(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+
+/* Persistent: a grid of (CUs x 4) workgroups walks the chunks [c0, c1) round-robin, so
+ * the per-workgroup setup (LDS table clear, kernel-argument state) is paid once. */
 __global__ __launch_bounds__(NT, 4) void k_tokcount_vs(CorpusDev c, const uint64_t* __restrict__ chunk_start,
                                                        const uint32_t* __restrict__ chunk_doc, uint64_t c0,
-                                                       VocabDev v, K1Out o) {
+                                                       uint64_t c1, VocabDev v, K1Out o) {
     __shared__ __attribute__((aligned(16))) VsShared S;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint64_t chunk = c0 + blockIdx.x;
-    const uint64_t cs = chunk_start[chunk], ce = chunk_start[chunk + 1];
-    if (cs >= ce) return;
-    const uint32_t dfirst = chunk_doc[chunk], dlast = chunk_doc[chunk + 1];
     const uint64_t last_blk = c.nbytes ? ((c.nbytes - 1) & ~(uint64_t)15) : 0;
 
 #pragma unroll
     for (int j = 0; j < EPT; ++j) S.T[j * NT + tid] = 0ull;
     unsigned long long tokens_chunk = 0;
     uint32_t step = 0;  /* global step counter: buffer parity */
+    Stamps st;
+#ifdef K1_STAMPS
+    st.prev = 0;
+    for (int k = 0; k < K1_NSTAMP; ++k) st.acc[k] = 0;
+    uint32_t cnt_[K1_NCOUNT] = {0, 0, 0, 0};
+#endif
+    STAMP(st, 0);
     if (tid < NT / 64) { S.wcl[0][tid] = 0; S.wcl[1][tid] = 0; }
 
+    for (uint64_t chunk = c0 + blockIdx.x; chunk < c1; chunk += gridDim.x) {
+    const uint64_t cs = chunk_start[chunk], ce = chunk_start[chunk + 1];
+    if (cs >= ce) continue;
+    const uint32_t dfirst = chunk_doc[chunk], dlast = chunk_doc[chunk + 1];
     for (uint32_t gd0 = dfirst; gd0 <= dlast; gd0 += GCAP) {
         const uint32_t ng = (dlast + 1 - gd0) < (uint32_t)GCAP ? (dlast + 1 - gd0) : (uint32_t)GCAP;
         for (uint32_t k = tid; k <= ng; k += NT) S.gdoc[k] = c.doc_off[gd0 + k];
         if (tid < GCAP) { S.dsz[tid] = 0; S.dpart[tid] = 0; }
         __syncthreads();
-        const uint64_t gs = S.gdoc[0] > cs ? S.gdoc[0] : cs;
-        const uint64_t ge = S.gdoc[ng] < ce ? S.gdoc[ng] : ce;
+        const uint64_t g0 = uni64(S.gdoc[0]), gn = uni64(S.gdoc[ng]);
+        const uint64_t gs = g0 > cs ? g0 : cs;
+        const uint64_t ge = gn < ce ? gn : ce;
+        STAMP(st, 0);
         uint32_t fill = 0; /* table entries, identical in every thread */
         if (gs < ge) {
             const uint64_t wbase0 = gs & ~(uint64_t)15;
+            /* lanes 0 and 63 also prefetch the group before / after their own (the byte
+             * before a wave's first group; the bytes a token runs into past its last) */
+            const bool edge_lane = lane == 0 || lane == 63;
+            const uint64_t eoff = lane == 0 ? (uint64_t)0 - 16ull : 16ull;
             uint4 pf = ld16c(c.bytes, last_blk, wbase0 + 16ull * tid);
+            uint4 pe = make_uint4(0, 0, 0, 0);
+            if (edge_lane) pe = ld16c(c.bytes, last_blk, wbase0 + 16ull * tid + eoff);
             for (uint64_t sbase = wbase0; sbase < ge; sbase += STEP, ++step) {
                 const uint32_t par = step & 1u;
                 const uint64_t gpos = sbase + 16ull * tid;
-                const uint4 cur = pf;
-                pf = ld16c(c.bytes, last_blk, gpos + STEP); /* next step, harmless past ge */
+                const uint4 cur = pf, edge = pe;
+                if (o.ablate & 16u) pf = make_uint4(0x20616161u ^ (uint32_t)gpos, 0x61612061u, 0x61206161u, 0x20616161u);
+                else pf = ld16c(c.bytes, last_blk, gpos + STEP); /* next step, harmless past ge */
+                if (edge_lane) pe = ld16c(c.bytes, last_blk, gpos + STEP + eoff);
                 /* ---- classify ---- */
                 const uint32_t ws = ws_mask16(cur) | bounds_ws(gpos, c.lo, c.hi);
                 const uint32_t r0 = doc_of(S, ng, gpos);
@@ -301,23 +371,21 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_vs(CorpusDev c, const uint64
                     const uint32_t b = gpos + 16 > ge ? (uint32_t)(ge - gpos) : 16u;
                     own = ((1u << b) - 1u) & ~((1u << a) - 1u);
                 }
-                uint32_t prev = __shfl_up(ws >> 15, 1, 64) & 1u;
-                if (lane == 0) {
-                    prev = 1u;
-                    if (gpos > c.lo && gpos - 1 < c.hi) prev = is_ws(c.bytes[gpos - 1]) ? 1u : 0u;
-                }
+                uint32_t prev = (lane_prev(ws) >> 15) & 1u;
+                if (lane == 0) prev = (gpos > c.lo && gpos - 1 < c.hi) ? (is_ws(edge.w >> 24) ? 1u : 0u) : 1u;
                 const uint32_t starts = ~ws & (((ws << 1) | prev) | ds) & own & 0xFFFFu;
                 /* the neighbour's 16 bytes and stop mask (tokens running into it) */
                 uint4 nxt;
-                nxt.x = __shfl_down(cur.x, 1, 64);
-                nxt.y = __shfl_down(cur.y, 1, 64);
-                nxt.z = __shfl_down(cur.z, 1, 64);
-                nxt.w = __shfl_down(cur.w, 1, 64);
-                uint32_t nstop = __shfl_down(stop, 1, 64);
+                nxt.x = lane_next(cur.x);
+                nxt.y = lane_next(cur.y);
+                nxt.z = lane_next(cur.z);
+                nxt.w = lane_next(cur.w);
+                uint32_t nstop = lane_next(stop);
                 if (lane == 63 && starts) {
-                    nxt = ld16c(c.bytes, last_blk, gpos + 16);
+                    nxt = edge;
                     nstop = ws_mask16(nxt) | bounds_ws(gpos + 16, c.lo, c.hi) | doc_start_bits(S, ng, r0, gpos + 16);
                 }
+                STAMP(st, 1);
                 /* ---- step token count -> flush decision (identical in every thread) ---- */
                 const uint32_t wt = wave_sum((uint32_t)__popc(starts));
                 if (lane == 0) S.wtok[par][wid] = wt;
@@ -327,10 +395,12 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_vs(CorpusDev c, const uint64
                 for (int q = 0; q < NT / 64; ++q) { ntok += S.wtok[par][q]; ncl += S.wcl[par ^ 1u][q]; }
                 fill += ncl;
                 tokens_chunk += ntok;
+                STAMP(st, 2);
                 if (fill + ntok > SOFT) fill = vs_flush(S, o, gd0, ng, cs, ce, sbase, false, ntok);
+                STAMP(st, 3);
                 /* ---- resolve + insert this lane's tokens ---- */
                 uint32_t claims = 0;
-                if (starts) {
+                if (starts && !(o.ablate & 4u)) {
                     const uint64_t q0 = ((uint64_t)cur.y << 32) | cur.x, q1 = ((uint64_t)cur.w << 32) | cur.z;
                     const uint64_t q2 = ((uint64_t)nxt.y << 32) | nxt.x, q3 = ((uint64_t)nxt.w << 32) | nxt.z;
                     const uint32_t s32 = stop | (nstop << 16);
@@ -338,40 +408,88 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_vs(CorpusDev c, const uint64
                     uint64_t nstart = S.gdoc[rel + 1];
                     uint32_t run_rel = rel, run_n = 0;
                     uint32_t sm = starts;
+                    CNT(0, __popc(starts));
                     while (sm) {
-                        const uint32_t i = __builtin_ctz(sm);
-                        sm &= sm - 1;
-                        const uint64_t ap = gpos + i;
-                        while (nstart <= ap) { ++rel; nstart = S.gdoc[rel + 1]; }
-                        const uint32_t m = s32 >> (i + 1);
-                        const uint32_t len = m ? (uint32_t)__builtin_ctz(m) + 1u : 32u;
-                        const uint32_t sh = (i & 7u) * 8u;
-                        const uint64_t a = i < 8 ? q0 : q1, b = i < 8 ? q1 : q2, cc = i < 8 ? q2 : q3;
-                        const uint64_t lo = sh ? (a >> sh) | (b << (64 - sh)) : a;
-                        const uint64_t hi = sh ? (b >> sh) | (cc << (64 - sh)) : b;
-                        uint64_t klo, khi;
-                        uint32_t slot;
-                        if (make_short_key(lo, hi, len, &klo, &khi) < 16u)
-                            slot = vocab_slot(v, klo, khi, o.status);
-                        else
-                            slot = slow_slot(c, v, ap, nstart, o.status);
-                        if (rel != run_rel) {
-                            if (run_n) atomicAdd(&S.dsz[run_rel], run_n);
-                            run_rel = rel;
-                            run_n = 0;
+                        CNT(3, 1);
+                        /* batch of KB tokens: keys, then every first vocabulary probe in
+                         * flight together, then the LDS counting */
+                        uint64_t klo[KB], khi[KB];
+                        uint32_t hv[KB], relk[KB], ipos[KB], kind[KB];
+                        uint4 s4[KB];
+#pragma unroll
+                        for (int k = 0; k < KB; ++k) {
+                            kind[k] = 0;
+                            ipos[k] = 0;
+                            klo[k] = khi[k] = 0;
+                            if (sm) {
+                                const uint32_t i = __builtin_ctz(sm);
+                                sm &= sm - 1;
+                                const uint64_t ap = gpos + i;
+                                while (nstart <= ap) { ++rel; nstart = S.gdoc[rel + 1]; }
+                                const uint32_t m = s32 >> (i + 1);
+                                const uint32_t len = m ? (uint32_t)__builtin_ctz(m) + 1u : 32u;
+                                const uint32_t sh = (i & 7u) * 8u;
+                                const uint64_t a = i < 8 ? q0 : q1, b = i < 8 ? q1 : q2, cc = i < 8 ? q2 : q3;
+                                const uint64_t lo = sh ? (a >> sh) | (b << (64 - sh)) : a;
+                                const uint64_t hi = sh ? (b >> sh) | (cc << (64 - sh)) : b;
+                                kind[k] = make_short_key(lo, hi, len, &klo[k], &khi[k]) < 16u ? 1u : 2u;
+                                ipos[k] = i;
+                            }
+                            relk[k] = rel;
+                            hv[k] = kind[k] == 1u ? (uint32_t)(key_hash(klo[k], khi[k]) & v.mask) : 0u;
+                            if (o.ablate & 1u) { s4[k] = make_uint4((uint32_t)klo[k], (uint32_t)(klo[k] >> 32), (uint32_t)khi[k], (uint32_t)(khi[k] >> 32)); if (kind[k] == 2u) kind[k] = 1u; }
+                            else s4[k] = v.keys[hv[k]];
                         }
-                        ++run_n;
-                        if (slot == INVALID_SLOT) continue; /* status flagged: the run is retried */
-                        if (tbl_add(S, ((uint64_t)rel << SLOT_BITS) | slot, 1u, o.status)) ++claims;
+                        uint64_t key[KB];
+                        uint32_t hl[KB];
+#pragma unroll
+                        for (int k = 0; k < KB; ++k) {
+                            uint32_t slot = INVALID_SLOT;
+                            if (kind[k] == 1u) {
+                                const bool hit = s4[k].x == (uint32_t)klo[k] && s4[k].y == (uint32_t)(klo[k] >> 32) &&
+                                                 s4[k].z == (uint32_t)khi[k] && s4[k].w == (uint32_t)(khi[k] >> 32);
+                                CNT(1, hit ? 0 : 1);
+                                slot = hit ? hv[k] : vocab_insert(v, klo[k], khi[k], 0, o.status);
+                            } else if (kind[k] == 2u) {
+                                slot = slow_slot(c.bytes, v.keys, v.rep, v.mask, gpos + ipos[k], S.gdoc[relk[k] + 1], o.status);
+                            }
+                            if (kind[k]) {
+                                if (relk[k] != run_rel) {
+                                    if (run_n) atomicAdd(&S.dsz[run_rel], run_n);
+                                    run_rel = relk[k];
+                                    run_n = 0;
+                                }
+                                ++run_n;
+                            }
+                            /* invalid slot: status flagged, the run is retried */
+                            key[k] = slot == INVALID_SLOT ? ~0ull : (((uint64_t)relk[k] << SLOT_BITS) | slot);
+                            hl[k] = tbl_hash(key[k]) & (TB - 1);
+                        }
+                        /* first LDS probes of the batch issued together (one lane's LDS
+                         * operations execute in order, so a repeated key sees its claim) */
+                        unsigned long long old[KB];
+                        if (o.ablate & 2u) continue;
+#pragma unroll
+                        for (int k = 0; k < KB; ++k)
+                            old[k] = key[k] != ~0ull ? atomicCAS(&S.T[hl[k]], 0ull, (key[k] << CNT_BITS) | 1ull) : 1ull;
+#pragma unroll
+                        for (int k = 0; k < KB; ++k) {
+                            if (key[k] == ~0ull) continue;
+                            if (old[k] == 0ull) { ++claims; continue; }
+                            if ((old[k] >> CNT_BITS) == key[k]) { atomicAdd(&S.T[hl[k]], 1ull); continue; }
+                            if (tbl_add_from(S, key[k], (hl[k] + 1) & (TB - 1), 1u, o.status)) ++claims;
+                        }
                     }
                     if (run_n) atomicAdd(&S.dsz[run_rel], run_n);
                 }
                 const uint32_t wc = wave_sum(claims);
                 if (lane == 0) S.wcl[par][wid] = wc;
+                STAMP(st, 4);
             }
         }
         /* group end is a document boundary (or the chunk end): emit everything */
-        vs_flush(S, o, gd0, ng, cs, ce, ge, true, 0);
+        if (!(o.ablate & 32u)) vs_flush(S, o, gd0, ng, cs, ce, ge, true, 0);
+        STAMP(st, 5);
         if ((uint32_t)tid < ng) {
             const uint32_t n = S.dsz[tid];
             if (n) {
@@ -382,15 +500,34 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_vs(CorpusDev c, const uint64
         }
         if (tid < NT / 64) { S.wcl[0][tid] = 0; S.wcl[1][tid] = 0; }
         __syncthreads();
+        STAMP(st, 6);
         if (gd0 + GCAP < gd0) break; /* overflow guard */
     }
-    if (tid == 0) atomicAdd(o.ntokens, tokens_chunk);
+    }  /* chunk loop */
+    if (tid == 0 && !(o.ablate & 8u)) atomicAdd(o.ntokens, tokens_chunk);
+#ifdef K1_STAMPS
+    if (tid == 0 && o.stamps) {
+        for (int k = 0; k < K1_NSTAMP; ++k) atomicAdd(&o.stamps[k], (unsigned long long)st.acc[k]);
+        atomicAdd(&o.stamps[K1_NSTAMP], 1ull);
+    }
+    if (o.stamps)
+        for (int k = 0; k < K1_NCOUNT; ++k)
+            if (cnt_[k]) atomicAdd(&o.stamps[K1_NSTAMP + 1 + k], (unsigned long long)cnt_[k]);
+#endif
 }
 
 int launch_tokcount_vs(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc, uint64_t c0,
                        uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s) {
     if (c1 <= c0) return 0;
     if (v.mask >= (1ull << SLOT_BITS)) return -3; /* slot must fit the LDS entry */
-    k_tokcount_vs<<<(unsigned)(c1 - c0), NT, 0, s>>>(c, chunk_start, chunk_doc, c0, v, o);
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+    }
+    const uint64_t grid = (c1 - c0) < (uint64_t)ncu * 4 ? (c1 - c0) : (uint64_t)ncu * 4;
+    k_tokcount_vs<<<(unsigned)grid, NT, 0, s>>>(c, chunk_start, chunk_doc, c0, c1, v, o);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

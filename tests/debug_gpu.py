@@ -59,8 +59,8 @@ def rccl1():
 def stamps():
     """K1 phase breakdown (diagnostic build): TFIDF_LIB=stamps TFIDF_STAMPS=1"""
     import ctypes as C
-    names = ["group setup", "stage", "compact+tokdoc", "docsize", "seg decide", "insert", "flush:enter",
-             "flush:A compact", "flush:B vocab", "flush:C alloc", "flush:D write", "kernel end"]
+    names = ["group setup", "classify", "count+decide", "mid flush", "resolve+insert", "group flush",
+             "docsize write", "-", "-", "-", "-", "-"]
     p = tfidf_configs.plan("c2", scale=float(os.environ.get("SCALE", "1.0")))
     with tfidf_abi.Engine(0) as e:
         c = e.synth_device(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"], p["ndocs_total"])
@@ -72,8 +72,8 @@ def stamps():
         L.tfidf_debug_k1_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
         n = L.tfidf_debug_k1_stamps(e.h, buf, 17)
         # the second run accumulated counters once (stamps are reset per run)
-        print("tokens", info["ntokens"], "segments", buf[13], "mid/clean flushes", buf[14],
-              "full-probe tokens", buf[15], "probe iterations", buf[16])
+        print("tokens", info["ntokens"], "counted", buf[13], "vocab first-probe misses", buf[14],
+              "-", buf[15], "lane token-loop iterations", buf[16])
     print("k1 ms", info["ms_tokcount"], "flags", info["flags"], "stamps", n)
     wgs = buf[12]
     tot = sum(buf[:12])
