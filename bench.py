@@ -76,6 +76,7 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--cpu-sample-docs", type=int, default=12000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--vocab", type=int, default=0, help="diagnostics only: override the config's vocabulary size")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -96,7 +97,7 @@ def main():
         dist.broadcast(uid, 0)
         eng.comm_init(bytes(uid.numpy().tobytes()), rank, world)
 
-    p = tfidf_configs.plan(args.config, scale=args.scale, rank=rank, nranks=world, weak=True)
+    p = tfidf_configs.plan(args.config, scale=args.scale, rank=rank, nranks=world, weak=True, vocab=args.vocab)
     corpus = eng.synth_device(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"], p["ndocs_total"])
     eng.set_timing(True)
 

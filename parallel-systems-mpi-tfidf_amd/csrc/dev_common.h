@@ -29,6 +29,24 @@
 /* C-locale isspace(): the byte set fscanf("%s") stops at (TFIDF.c:142,147) */
 __device__ __forceinline__ bool is_ws(uint32_t c) { return c == 0x20u || (c - 0x09u) <= 4u; }
 
+/* 4-bit mask of the C-locale whitespace bytes {0x20, 0x09..0x0D} of a 32-bit word,
+ * SWAR: every per-byte sum below stays inside its byte, so the tests are exact. */
+__device__ __forceinline__ uint32_t ws_mask4(uint32_t x) {
+    const uint32_t lo7 = x & 0x7F7F7F7Fu;
+    const uint32_t t = x ^ 0x20202020u;
+    const uint32_t ne20 = ((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t;   /* bit 7: byte != 0x20 */
+    const uint32_t ge9 = lo7 + 0x77777777u;                         /* bit 7: low7 >= 0x09 */
+    const uint32_t ge14 = lo7 + 0x72727272u;                        /* bit 7: low7 >= 0x0E */
+    uint32_t m = (~ne20 | (ge9 & ~ge14)) & ~x & 0x80808080u;        /* bit 7 of each ws byte */
+    m >>= 7;                                                        /* bits 0, 8, 16, 24 */
+    m |= m >> 7;                                                    /* bits 0-1, 16-17 */
+    m |= m >> 14;                                                   /* bits 0-3 */
+    return m & 0xFu;
+}
+__device__ __forceinline__ uint32_t ws_mask16_swar(uint4 v) {
+    return ws_mask4(v.x) | (ws_mask4(v.y) << 4) | (ws_mask4(v.z) << 8) | (ws_mask4(v.w) << 12);
+}
+
 /* 16-bit mask of whitespace bytes in a 16-byte group (bit i = byte i) */
 __device__ __forceinline__ uint32_t ws_mask16(uint4 v) {
     uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -50,8 +68,17 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 
+/* Vocabulary hash of a 128-bit term key: 32-bit multiplies only (a 64-bit multiply is
+ * four quarter-rate v_mul on CDNA), finalised murmur-style; tables are < 2^32 slots. */
 __device__ __forceinline__ uint64_t key_hash(uint64_t lo, uint64_t hi) {
-    return mix64(lo * 0x9E3779B97F4A7C15ull ^ (hi + 0x632BE59BD9B4E019ull) * 0xC2B2AE3D27D4EB4Full);
+    const uint32_t a = (uint32_t)lo, b = (uint32_t)(lo >> 32), c = (uint32_t)hi, d = (uint32_t)(hi >> 32);
+    uint32_t h = (a ^ __builtin_rotateleft32(c, 16)) * 0x9E3779B1u + (b ^ __builtin_rotateleft32(d, 8)) * 0x85EBCA77u;
+    h ^= h >> 15;
+    h *= 0x2C1B3C6Du;
+    h ^= h >> 12;
+    h *= 0x297A2D39u;
+    h ^= h >> 15;
+    return h;
 }
 
 /* first zero byte index in a u64 (8 if none) */

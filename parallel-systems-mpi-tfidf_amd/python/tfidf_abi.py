@@ -12,9 +12,10 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# TFIDF_LIB=stamps selects the diagnostic build (K1 phase stamps); never used for benches
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libtfidf_hip_stamps.so" if os.environ.get("TFIDF_LIB") == "stamps"
-                        else "libtfidf_hip.so")
+# TFIDF_LIB=<variant> selects a diagnostic build lib/libtfidf_hip_<variant>.so (K1 phase
+# stamps, K1 ablations); never used for benches or tests
+_VARIANT = os.environ.get("TFIDF_LIB", "")
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libtfidf_hip_%s.so" % _VARIANT if _VARIANT else "libtfidf_hip.so")
 CLI_PATH = os.path.join(PKG_DIR, "bin", "tfidf")
 
 TFIDF_CORPUS_DEVICE = 1

@@ -65,7 +65,7 @@ def doc_name_key(ids: np.ndarray) -> np.ndarray:
     return key
 
 
-def plan(name: str, scale: float = 1.0, rank: int = 0, nranks: int = 1, weak: bool = False):
+def plan(name: str, scale: float = 1.0, rank: int = 0, nranks: int = 1, weak: bool = False, vocab: int = 0):
     """Returns dict(doc_ids, ntok, cdf, V, mode, seed, ndocs_total).
 
     nranks > 1: documents are sharded in contiguous "docN" strcmp-order ranges, so the
@@ -74,7 +74,7 @@ def plan(name: str, scale: float = 1.0, rank: int = 0, nranks: int = 1, weak: bo
     """
     cfg = dict(CONFIGS[name])
     seed = cfg["seed"]
-    V = cfg["V"]
+    V = vocab or cfg["V"]   # vocab: diagnostic override of the vocabulary size
     if cfg.get("mode") == MODE_C1:
         N = cfg["N"] * (nranks if weak else 1)
         ids = np.arange(1, N + 1, dtype=np.uint32)

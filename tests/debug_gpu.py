@@ -59,8 +59,9 @@ def rccl1():
 def stamps():
     """K1 phase breakdown (diagnostic build): TFIDF_LIB=stamps TFIDF_STAMPS=1"""
     import ctypes as C
-    names = ["group setup", "classify", "count+decide", "mid flush", "resolve+insert", "group flush",
-             "docsize write", "-", "-", "-", "-", "-"]
+    names = ["group setup", "walk tail", "flush", "docsize write", "classify", "compact",
+             "round: keys+loads", "round: compare+miss", "round: docsize", "round: LDS count",
+             "round: claims", "step loop top"]
     p = tfidf_configs.plan("c2", scale=float(os.environ.get("SCALE", "1.0")))
     with tfidf_abi.Engine(0) as e:
         c = e.synth_device(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"], p["ndocs_total"])
