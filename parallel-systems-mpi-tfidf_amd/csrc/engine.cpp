@@ -99,7 +99,7 @@ struct tfidf_ctx {
     DevBuf pkey0, pkey1, pseq0, pseq1, phead;
     DevBuf df_local, df_global, present, idf_vals;
     DevBuf dkey0, dkey1, dseq0, dseq1, npairs_ord, out_off;
-    DevBuf out_doc, out_term, out_cnt, out_docsize, out_df, out_score;
+    DevBuf out_term, out_cnt, out_score, idf_rank, large_list;
     DevBuf x_mine, x_send, x_recv, x_recv2, x_seq0, x_seq1, x_head, x_grank, x_dfv, x_cnt;
     uint32_t* sorted_dense = nullptr; /* points into seq0/seq1 */
     uint4* sorted_skey = nullptr;
@@ -204,8 +204,8 @@ void tfidf_close(tfidf_ctx* ctx) {
                       &ctx->skey1, &ctx->seq0, &ctx->seq1, &ctx->rank_of_slot, &ctx->slot_of_rank, &ctx->pkey0,
                       &ctx->pkey1, &ctx->pseq0, &ctx->pseq1, &ctx->phead, &ctx->df_local, &ctx->df_global,
                       &ctx->present, &ctx->idf_vals, &ctx->dkey0, &ctx->dkey1, &ctx->dseq0, &ctx->dseq1,
-                      &ctx->npairs_ord, &ctx->out_off, &ctx->out_doc, &ctx->out_term, &ctx->out_cnt,
-                      &ctx->out_docsize, &ctx->out_df, &ctx->out_score, &ctx->x_mine, &ctx->x_send, &ctx->x_recv,
+                      &ctx->npairs_ord, &ctx->out_off, &ctx->out_term, &ctx->out_cnt,
+                      &ctx->out_score, &ctx->idf_rank, &ctx->large_list, &ctx->x_mine, &ctx->x_send, &ctx->x_recv,
                       &ctx->x_recv2, &ctx->x_seq0, &ctx->x_seq1, &ctx->x_head, &ctx->x_grank, &ctx->x_dfv,
                       &ctx->x_cnt, &ctx->stamps};
     for (DevBuf* b : bufs) b->release();
@@ -520,12 +520,11 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     ctx->npairs = P;
     /* ---- score + per-document term order ---- */
     mark(ctx, S_SCORE);
-    ENSURE(ctx->out_doc, P * 4 + 4);
     ENSURE(ctx->out_term, P * 4 + 4);
     ENSURE(ctx->out_cnt, P * 4 + 4);
-    ENSURE(ctx->out_docsize, P * 4 + 4);
-    ENSURE(ctx->out_df, P * 4 + 4);
     ENSURE(ctx->out_score, P * 8 + 8);
+    ENSURE(ctx->idf_rank, (size_t)V * 8 + 8);
+    ENSURE(ctx->large_list, (size_t)N * 4 + 8);
     K5Args a{};
     a.order = ctx->order;
     a.out_off = ctx->out_off.as<uint64_t>();
@@ -533,23 +532,23 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     a.doc_npairs = ctx->doc_npairs.as<uint32_t>();
     a.doc_size = ctx->doc_size.as<uint32_t>();
     a.doc_flags = ctx->doc_flags.as<uint8_t>();
-    a.doc_ids = dev_ids;
     a.rec_slot = ctx->rec_slot.as<uint32_t>();
     a.rec_cnt = ctx->rec_cnt.as<uint32_t>();
     a.rank_of_slot = ctx->rank_of_slot.as<uint32_t>();
     a.df_of_rank = ctx->df_global.as<uint32_t>();
     a.idf_idx = ctx->present.as<uint32_t>();
     a.idf = ctx->idf_vals.as<double>();
+    a.idf_rank = ctx->idf_rank.as<double>();
+    a.large_list = ctx->large_list.as<uint32_t>() + 1;
+    a.large_count = ctx->large_list.as<uint32_t>();
     a.ndocs = N;
+    a.nterms = V;
     a.rank_bits = V > 1 ? 32u - (uint32_t)__builtin_clz(V - 1) : 1u;
     a.rec_total = R_total;
     a.slot_cap = cap;
     a.status = (uint32_t*)(cnt + 3);
-    a.out_doc = ctx->out_doc.as<uint32_t>();
     a.out_term = ctx->out_term.as<uint32_t>();
     a.out_cnt = ctx->out_cnt.as<uint32_t>();
-    a.out_docsize = ctx->out_docsize.as<uint32_t>();
-    a.out_df = ctx->out_df.as<uint32_t>();
     a.out_score = ctx->out_score.as<double>();
     LCHK(launch_score_order(a, s));
     mark(ctx, S_NSTAGES);
@@ -715,15 +714,18 @@ extern "C" int tfidf_fetch(tfidf_ctx* ctx, tfidf_result* r) {
         tfidf_result_free(r);
         return TFIDF_E_NOMEM;
     }
+    std::vector<uint32_t> order(N);
+    std::vector<uint64_t> ooff((size_t)N + 1);
     if (P) {
-        HIPCHK(hipMemcpyAsync(r->pair_doc, ctx->out_doc.p, P * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(r->pair_term, ctx->out_term.p, P * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(r->pair_count, ctx->out_cnt.p, P * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(r->pair_docsize, ctx->out_docsize.p, P * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(r->pair_df, ctx->out_df.p, P * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(r->pair_score, ctx->out_score.p, P * 8, hipMemcpyDeviceToHost, s));
     }
-    if (N) HIPCHK(hipMemcpyAsync(r->doc_size, ctx->doc_size.p, (size_t)N * 4, hipMemcpyDeviceToHost, s));
+    if (N) {
+        HIPCHK(hipMemcpyAsync(r->doc_size, ctx->doc_size.p, (size_t)N * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(order.data(), ctx->order, (size_t)N * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(ooff.data(), ctx->out_off.p, ((size_t)N + 1) * 8, hipMemcpyDeviceToHost, s));
+    }
     if (V) HIPCHK(hipMemcpyAsync(r->term_df, ctx->df_global.p, (size_t)V * 4, hipMemcpyDeviceToHost, s));
     /* term strings in rank order */
     std::vector<uint4> keys(V);
@@ -744,6 +746,17 @@ extern "C" int tfidf_fetch(tfidf_ctx* ctx, tfidf_result* r) {
     } else {
         for (uint32_t i = 0; i < N; ++i) r->doc_id[i] = i + 1;
     }
+    /* per-pair document, docSize and df: expanded from the per-document output order
+     * (K5 writes 16 bytes per pair) */
+    for (uint32_t j = 0; j < N; ++j) {
+        const uint32_t d = order[j];
+        const uint32_t id = r->doc_id[d], dsz = r->doc_size[d];
+        for (uint64_t q = ooff[j]; q < ooff[j + 1] && q < P; ++q) {
+            r->pair_doc[q] = id;
+            r->pair_docsize[q] = dsz;
+        }
+    }
+    for (uint64_t q = 0; q < P; ++q) r->pair_df[q] = r->pair_term[q] < V ? r->term_df[r->pair_term[q]] : 0u;
     std::string pool;
     pool.reserve((size_t)V * 8);
     for (uint32_t t = 0; t < V; ++t) {

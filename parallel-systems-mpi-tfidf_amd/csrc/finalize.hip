@@ -208,22 +208,34 @@ int launch_part_merge(const uint64_t* keys, const uint32_t* seq, const uint32_t*
 constexpr uint32_t DFH_RECS = 65535;      /* records per workgroup: u16 bins cannot overflow */
 constexpr uint32_t DFH_MAXV = 65536;
 
-__global__ __launch_bounds__(NT) void k_df_hist_lds(const uint32_t* __restrict__ rec_slot, uint64_t nrec,
-                                                    const uint32_t* __restrict__ rank_of_slot, uint32_t V,
-                                                    uint32_t* __restrict__ part /* [grid][V/2 words] */) {
+/* LDS-privatised DF histogram: 1024 threads (16 waves, the 100 KB bin array allows one
+ * workgroup per CU), four record gathers in flight per thread. */
+constexpr int DFH_NT = 1024;
+__global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(const uint32_t* __restrict__ rec_slot, uint64_t nrec,
+                                                        const uint32_t* __restrict__ rank_of_slot, uint32_t V,
+                                                        uint32_t* __restrict__ part /* [grid][V/2 words] */) {
     extern __shared__ __attribute__((aligned(16))) uint32_t bins[]; /* V/2 words of two u16 counters */
     const uint32_t W = (V + 1) / 2;
-    for (uint32_t k = threadIdx.x; k < W; k += NT) bins[k] = 0;
+    for (uint32_t k = threadIdx.x; k < W; k += DFH_NT) bins[k] = 0;
     __syncthreads();
-    uint64_t r0 = (uint64_t)blockIdx.x * DFH_RECS;
-    uint64_t r1 = r0 + DFH_RECS < nrec ? r0 + DFH_RECS : nrec;
-    for (uint64_t i = r0 + threadIdx.x; i < r1; i += NT) {
-        uint32_t r = rank_of_slot[rec_slot[i]];
-        atomicAdd(&bins[r >> 1], 1u << (16 * (r & 1)));
+    const uint64_t r0 = (uint64_t)blockIdx.x * DFH_RECS;
+    const uint64_t r1 = r0 + DFH_RECS < nrec ? r0 + DFH_RECS : nrec;
+    for (uint64_t i = r0 + threadIdx.x; i < r1; i += 4 * DFH_NT) {
+        uint32_t sl[4], r[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint64_t k = i + (uint64_t)q * DFH_NT;
+            sl[q] = k < r1 ? rec_slot[k] : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) r[q] = rank_of_slot[sl[q]];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (i + (uint64_t)q * DFH_NT < r1) atomicAdd(&bins[r[q] >> 1], 1u << (16 * (r[q] & 1)));
     }
     __syncthreads();
     uint32_t* out = part + (uint64_t)blockIdx.x * W;
-    for (uint32_t k = threadIdx.x; k < W; k += NT) out[k] = bins[k];
+    for (uint32_t k = threadIdx.x; k < W; k += DFH_NT) out[k] = bins[k];
 }
 __global__ void k_df_colsum(const uint32_t* __restrict__ part, uint32_t nparts, uint32_t V, uint32_t* __restrict__ df) {
     uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -248,7 +260,7 @@ int launch_df_hist(const uint32_t* rec_slot, uint64_t nrec, const uint32_t* rank
         size_t m = ar.mark();
         uint32_t* part = (uint32_t*)ar.get((size_t)nparts * W * 4);
         if (!part) return -2;
-        k_df_hist_lds<<<nparts, NT, (size_t)W * 4, s>>>(rec_slot, nrec, rank_of_slot, V, part);
+        k_df_hist_lds<<<nparts, DFH_NT, (size_t)W * 4, s>>>(rec_slot, nrec, rank_of_slot, V, part);
         k_df_colsum<<<grid_for(V), NT, 0, s>>>(part, nparts, V, df);
         ar.release(m);
         return ok();
@@ -316,57 +328,171 @@ int launch_gather_npairs(const uint32_t* order, const uint32_t* doc_npairs, uint
 /* ------------------------------------------------------ score + order (K5) */
 
 constexpr int K5_MAX = K5_MAX_PAIRS;
+constexpr uint32_t K5_SMALL = 64;     /* one wave, bitonic across the lanes */
+constexpr uint32_t K5_WAVE = 1024;    /* one wave, LDS radix sort of packed (rank, index) keys */
+constexpr uint32_t K5_IDX_BITS = 11;  /* index bits of a packed key (n <= 2048) */
+constexpr int K5_BATCH = 8;           /* gathers per lane in flight together */
 
-__device__ __forceinline__ void k5_emit(const K5Args& a, uint64_t o, uint32_t id, uint32_t ds, uint32_t rank,
-                                        uint32_t cnt) {
-    uint32_t df = a.df_of_rank[rank];
-    double idf = a.idf[a.idf_idx[df]];
-    double tf = (double)cnt / (double)ds;  /* TFIDF.c:202 */
-    a.out_doc[o] = id;
-    a.out_term[o] = rank;
-    a.out_cnt[o] = cnt;
-    a.out_docsize[o] = ds;
-    a.out_df[o] = df;
-    a.out_score[o] = tf * idf;             /* TFIDF.c:244 */
+/* idf of every term rank: one gather per pair in K5 instead of three dependent ones */
+__global__ void k_idf_of_rank(const uint32_t* __restrict__ df_of_rank, const uint32_t* __restrict__ idf_idx,
+                              const double* __restrict__ idf, uint32_t V, double* __restrict__ out) {
+    uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < V) out[r] = idf[idf_idx[df_of_rank[r]]];
 }
 
-constexpr uint32_t K5_SMALL = 64;
+/* The output is 16 bytes per pair (term rank, count, score): the document, docSize and
+ * df of a pair are per-document / per-term values the fetch expands on the host. */
+__device__ __forceinline__ void k5_emit(const K5Args& a, uint64_t o, double ds, uint32_t rank, uint32_t cnt) {
+    const double tf = (double)cnt / ds;   /* TFIDF.c:202 */
+    a.out_term[o] = rank;
+    a.out_cnt[o] = cnt;
+    a.out_score[o] = tf * a.idf_rank[rank]; /* TFIDF.c:243-244 (idf from the host-libm LUT) */
+}
 
 __device__ __forceinline__ uint32_t k5_rank(const K5Args& a, uint32_t sl) {
     if (sl >= a.slot_cap) { atomicOr(a.status, ST_BOUNDS); sl = 0; }
     return a.rank_of_slot[sl];
 }
 
-/* Documents with <= 64 pairs: one wave each, bitonic sort of (rank, count) across the
- * 64 lanes with __shfl_xor; four documents per workgroup, no barriers. */
-__global__ __launch_bounds__(NT) void k_score_small(K5Args a) {
+/* which kernel sorts a document of n pairs */
+__device__ __forceinline__ bool k5_by_wave(const K5Args& a, uint32_t n, bool presorted) {
+    if (presorted) return n <= K5_WAVE;
+    return n <= K5_SMALL || (n <= K5_WAVE && a.rank_bits + K5_IDX_BITS <= 32);
+}
+
+/* One wave per document, four documents per workgroup, no block barriers:
+ *   n <= 64      bitonic sort of (rank, count) across the lanes (__shfl_xor);
+ *   n <= 1024    LSD radix sort by rank, 8-bit digits, of packed (rank << 11 | index) keys
+ *                in a wave-private LDS ping-pong: a wave-private histogram, a DPP scan of the
+ *                256 bins and a stable multisplit scatter (8 ballots) per round of 64 keys;
+ *   presorted    merged runs (finalize's partial merge) are emitted as they are. */
+__global__ __launch_bounds__(NT) void k_score_wave(K5Args a) {
+    __shared__ uint32_t kb[NT / 64][2][K5_WAVE];
+    __shared__ uint32_t hist[NT / 64][256];
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t i = blockIdx.x * (NT / 64) + w;
     if (i >= a.ndocs) return;
     const uint32_t d = a.order[i];
     const uint32_t n = a.doc_npairs[d];
-    if (n == 0 || n > K5_SMALL) return;
+    const bool presorted = (a.doc_flags[d] & DF_PRESORTED) != 0;
+    if (n == 0) return;
+    if (!k5_by_wave(a, n, presorted)) { /* hand the document to k_score_large's list */
+        if (lane == 0) a.large_list[atomicAdd(a.large_count, 1u)] = i;
+        return;
+    }
     const uint64_t ob = a.out_off[i], rb = a.doc_recoff[d];
     if (rb + n > a.rec_total) { if (lane == 0) atomicOr(a.status, ST_BOUNDS); return; }
-    uint32_t key = 0xFFFFFFFFu, val = 0;
-    if (lane < n) { key = k5_rank(a, a.rec_slot[rb + lane]); val = a.rec_cnt[rb + lane]; }
+    const double ds = (double)a.doc_size[d];
+    if (presorted) {
+        for (uint32_t j = lane; j < n; j += 64) k5_emit(a, ob + j, ds, k5_rank(a, a.rec_slot[rb + j]), a.rec_cnt[rb + j]);
+        return;
+    }
+    if (n <= K5_SMALL) {
+        uint32_t key = 0xFFFFFFFFu, val = 0;
+        if (lane < n) { key = k5_rank(a, a.rec_slot[rb + lane]); val = a.rec_cnt[rb + lane]; }
 #pragma unroll
-    for (uint32_t k = 2; k <= 64; k <<= 1) {
+        for (uint32_t k = 2; k <= 64; k <<= 1) {
 #pragma unroll
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            uint32_t pk = __shfl_xor(key, j, 64), pv = __shfl_xor(val, j, 64);
-            bool take_min = ((lane & k) == 0) == ((lane & j) == 0);
-            if (take_min ? (pk < key) : (pk > key)) { key = pk; val = pv; }
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                uint32_t pk = __shfl_xor(key, j, 64), pv = __shfl_xor(val, j, 64);
+                bool take_min = ((lane & k) == 0) == ((lane & j) == 0);
+                if (take_min ? (pk < key) : (pk > key)) { key = pk; val = pv; }
+            }
+        }
+        if (lane < n) k5_emit(a, ob + lane, ds, key, val);
+        return;
+    }
+    uint32_t* buf0 = kb[w][0];
+    uint32_t* buf1 = kb[w][1];
+    uint32_t* h = hist[w];
+    /* keys: every slot load of a batch in flight, then every rank gather */
+    for (uint32_t j0 = 0; j0 < n; j0 += 64 * K5_BATCH) {
+        uint32_t sl[K5_BATCH];
+#pragma unroll
+        for (int q = 0; q < K5_BATCH; ++q) {
+            const uint32_t j = j0 + 64 * q + lane;
+            sl[q] = j < n ? a.rec_slot[rb + j] : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < K5_BATCH; ++q) {
+            const uint32_t j = j0 + 64 * q + lane;
+            const uint32_t r = k5_rank(a, sl[q]);
+            if (j < n) buf0[j] = (r << K5_IDX_BITS) | j;
         }
     }
-    if (lane < n) {
-        const uint32_t id = a.doc_ids ? a.doc_ids[d] : d + 1;
-        k5_emit(a, ob + lane, id, a.doc_size[d], key, val);
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint32_t cur = 0;
+    for (uint32_t sh = K5_IDX_BITS; sh < K5_IDX_BITS + a.rank_bits; sh += 8) {
+        const uint32_t* src = cur ? buf1 : buf0;
+        uint32_t* dst = cur ? buf0 : buf1;
+        h[4 * lane] = 0; h[4 * lane + 1] = 0; h[4 * lane + 2] = 0; h[4 * lane + 3] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t j = lane; j < n; j += 64) atomicAdd(&h[(src[j] >> sh) & 0xFFu], 1u);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        {
+            const uint32_t v0 = h[4 * lane], v1 = h[4 * lane + 1], v2 = h[4 * lane + 2], v3 = h[4 * lane + 3];
+            const uint32_t tot = v0 + v1 + v2 + v3;
+            const uint32_t ex = wave_incl_scan(tot) - tot;
+            h[4 * lane] = ex; h[4 * lane + 1] = ex + v0; h[4 * lane + 2] = ex + v0 + v1; h[4 * lane + 3] = ex + v0 + v1 + v2;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t r0 = 0; r0 < n; r0 += 64) {
+            const uint32_t j = r0 + lane;
+            const bool valid = j < n;
+            const uint32_t key = valid ? src[j] : 0u;
+            const uint32_t dg = (key >> sh) & 0xFFu;
+            uint64_t m = __ballot(valid);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const bool bit = (dg >> b) & 1u;
+                const uint64_t bb = __ballot(valid && bit);
+                m &= bit ? bb : ~bb;
+            }
+            const uint32_t lrank = (uint32_t)__popcll(m & below);
+            const uint32_t cnt = (uint32_t)__popcll(m);
+            const uint32_t base = valid ? h[dg] : 0u;   /* every lane reads before any lane writes */
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (valid) {
+                dst[base + lrank] = key;
+                if (lrank == cnt - 1u) h[dg] = base + cnt;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        cur ^= 1u;
+    }
+    const uint32_t* fin = cur ? buf1 : buf0;
+    for (uint32_t j0 = 0; j0 < n; j0 += 64 * K5_BATCH) {
+        uint32_t key[K5_BATCH], cnt[K5_BATCH];
+        double idf[K5_BATCH];
+#pragma unroll
+        for (int q = 0; q < K5_BATCH; ++q) {
+            const uint32_t j = j0 + 64 * q + lane;
+            key[q] = j < n ? fin[j] : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < K5_BATCH; ++q) {
+            cnt[q] = a.rec_cnt[rb + (key[q] & ((1u << K5_IDX_BITS) - 1u))];
+            idf[q] = a.idf_rank[key[q] >> K5_IDX_BITS];
+        }
+#pragma unroll
+        for (int q = 0; q < K5_BATCH; ++q) {
+            const uint32_t j = j0 + 64 * q + lane;
+            if (j < n) {
+                a.out_term[ob + j] = key[q] >> K5_IDX_BITS;
+                a.out_cnt[ob + j] = cnt[q];
+                a.out_score[ob + j] = ((double)cnt[q] / ds) * idf[q]; /* TFIDF.c:202,243-244 */
+            }
+        }
     }
 }
 
-/* Documents with > 64 pairs: one workgroup each.  Presorted (merged) runs are scored
- * straight through; others are LSD radix-sorted by rank in LDS, 8-bit digits, with a
+/* Documents the wave kernel leaves: one workgroup each.  Presorted (merged) runs are
+ * scored straight through; others are LSD radix-sorted by rank in LDS, 8-bit digits, with a
  * stable wave64 multisplit (8 ballots) per round of 256 elements. */
 __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
     __shared__ uint32_t kbuf[2][K5_MAX];
@@ -375,21 +501,22 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
     __shared__ uint32_t wcnt[NT / 64][256];
     __shared__ uint32_t wsum[NT / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint32_t i = blockIdx.x;
+    const uint32_t nlarge = *a.large_count;
+    for (uint32_t li = blockIdx.x; li < nlarge; li += gridDim.x) {
+    const uint32_t i = a.large_list[li];
     const uint32_t d = a.order[i];
     const uint32_t n = a.doc_npairs[d];
-    if (n <= K5_SMALL) return;
+    const bool presorted = (a.doc_flags[d] & DF_PRESORTED) != 0;
     const uint64_t ob = a.out_off[i], rb = a.doc_recoff[d];
-    const uint32_t ds = a.doc_size[d];
-    const uint32_t id = a.doc_ids ? a.doc_ids[d] : d + 1;
+    const double ds = (double)a.doc_size[d];
     if (rb + n > a.rec_total) { /* never expected: report instead of reading past the records */
         if (tid == 0) atomicOr(a.status, ST_BOUNDS);
-        return;
+        continue;
     }
-    if ((a.doc_flags[d] & DF_PRESORTED) || n > (uint32_t)K5_MAX) {
-        if (n > (uint32_t)K5_MAX && !(a.doc_flags[d] & DF_PRESORTED)) { if (tid == 0) atomicOr(a.status, ST_BOUNDS); return; }
-        for (uint32_t j = tid; j < n; j += NT) k5_emit(a, ob + j, id, ds, k5_rank(a, a.rec_slot[rb + j]), a.rec_cnt[rb + j]);
-        return;
+    if (presorted || n > (uint32_t)K5_MAX) {
+        if (n > (uint32_t)K5_MAX && !presorted) { if (tid == 0) atomicOr(a.status, ST_BOUNDS); continue; }
+        for (uint32_t j = tid; j < n; j += NT) k5_emit(a, ob + j, ds, k5_rank(a, a.rec_slot[rb + j]), a.rec_cnt[rb + j]);
+        continue;
     }
     for (uint32_t j = tid; j < n; j += NT) {
         kbuf[0][j] = k5_rank(a, a.rec_slot[rb + j]);
@@ -439,12 +566,18 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
         }
         cur ^= 1;
     }
-    for (uint32_t j = tid; j < n; j += NT) k5_emit(a, ob + j, id, ds, kbuf[cur][j], vbuf[cur][j]);
+    for (uint32_t j = tid; j < n; j += NT) k5_emit(a, ob + j, ds, kbuf[cur][j], vbuf[cur][j]);
+    __syncthreads(); /* the next document reuses the LDS buffers */
+    }
 }
 int launch_score_order(const K5Args& a, hipStream_t s) {
     if (!a.ndocs) return 0;
-    k_score_small<<<(a.ndocs + NT / 64 - 1) / (NT / 64), NT, 0, s>>>(a);
-    k_score_large<<<a.ndocs, NT, 0, s>>>(a);
+    if (hipMemsetAsync(a.large_count, 0, 4, s) != hipSuccess) return -1;
+    k_idf_of_rank<<<grid_for(a.nterms ? a.nterms : 1), NT, 0, s>>>(a.df_of_rank, a.idf_idx, a.idf, a.nterms,
+                                                                  a.idf_rank);
+    k_score_wave<<<(a.ndocs + NT / 64 - 1) / (NT / 64), NT, 0, s>>>(a);
+    const uint32_t grid = a.ndocs < 2048u ? a.ndocs : 2048u; /* persistent over the handed-off list */
+    k_score_large<<<grid, NT, 0, s>>>(a);
     return ok();
 }
 

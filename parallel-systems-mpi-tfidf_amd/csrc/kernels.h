@@ -119,24 +119,24 @@ struct K5Args {
     const uint32_t* doc_npairs;
     const uint32_t* doc_size;
     const uint8_t* doc_flags;
-    const uint32_t* doc_ids;     /* NULL: 1..ndocs */
     const uint32_t* rec_slot;
     const uint32_t* rec_cnt;
     const uint32_t* rank_of_slot;
     const uint32_t* df_of_rank;  /* global df */
     const uint32_t* idf_idx;     /* df value -> index into idf */
     const double* idf;
+    double* idf_rank;            /* [nterms] scratch: idf of each term rank */
+    uint32_t* large_list;        /* [ndocs] scratch: output positions left to k_score_large */
+    uint32_t* large_count;
     uint32_t ndocs;
+    uint32_t nterms;
     uint32_t rank_bits;          /* bits of the largest term rank (radix passes) */
     uint64_t rec_total;          /* bounds guard: records in rec_slot/rec_cnt */
     uint64_t slot_cap;           /* bounds guard: vocabulary capacity */
     uint32_t* status;            /* ST_BOUNDS set instead of faulting */
-    uint32_t* out_doc;
-    uint32_t* out_term;
-    uint32_t* out_cnt;
-    uint32_t* out_docsize;
-    uint32_t* out_df;
-    double* out_score;
+    uint32_t* out_term;          /* output order: term rank */
+    uint32_t* out_cnt;           /*               wordCount */
+    double* out_score;           /*               tf * idf */
 };
 int launch_score_order(const K5Args& a, hipStream_t s);
 

@@ -197,7 +197,10 @@ int radix_sort_t(K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t n, uint32_t 
     return hipGetLastError() == hipSuccess ? cur : -1;
 }
 
-__global__ void k_orand_u64(const uint64_t* __restrict__ k, uint64_t n, unsigned long long* acc) {
+/* AND / OR of all keys (which bytes vary): wave reduce, then one LDS combine per block and
+ * one global atomic per block and word (thousands of same-address atomics serialise). */
+__global__ __launch_bounds__(256) void k_orand_u64(const uint64_t* __restrict__ k, uint64_t n, unsigned long long* acc) {
+    __shared__ unsigned long long sa[4], so[4];
     uint64_t a = ~0ull, o = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         a &= k[i];
@@ -207,10 +210,17 @@ __global__ void k_orand_u64(const uint64_t* __restrict__ k, uint64_t n, unsigned
         a &= __shfl_xor(a, off, 64);
         o |= __shfl_xor(o, off, 64);
     }
-    if ((threadIdx.x & 63) == 0) { atomicAnd(&acc[0], a); atomicOr(&acc[1], o); }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sa[w] = a; so[w] = o; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAnd(&acc[0], sa[0] & sa[1] & sa[2] & sa[3]);
+        atomicOr(&acc[1], so[0] | so[1] | so[2] | so[3]);
+    }
 }
 
-__global__ void k_orand_u128(const uint4* __restrict__ k, uint64_t n, unsigned long long* acc) {
+__global__ __launch_bounds__(256) void k_orand_u128(const uint4* __restrict__ k, uint64_t n, unsigned long long* acc) {
+    __shared__ unsigned long long s4[4][4];
     uint64_t a0 = ~0ull, a1 = ~0ull, o0 = 0, o1 = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         uint4 v = k[i];
@@ -221,9 +231,14 @@ __global__ void k_orand_u128(const uint4* __restrict__ k, uint64_t n, unsigned l
         a0 &= __shfl_xor(a0, off, 64); a1 &= __shfl_xor(a1, off, 64);
         o0 |= __shfl_xor(o0, off, 64); o1 |= __shfl_xor(o1, off, 64);
     }
-    if ((threadIdx.x & 63) == 0) {
-        atomicAnd(&acc[0], a0); atomicAnd(&acc[1], a1);
-        atomicOr(&acc[2], o0); atomicOr(&acc[3], o1);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { s4[w][0] = a0; s4[w][1] = a1; s4[w][2] = o0; s4[w][3] = o1; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAnd(&acc[0], s4[0][0] & s4[1][0] & s4[2][0] & s4[3][0]);
+        atomicAnd(&acc[1], s4[0][1] & s4[1][1] & s4[2][1] & s4[3][1]);
+        atomicOr(&acc[2], s4[0][2] | s4[1][2] | s4[2][2] | s4[3][2]);
+        atomicOr(&acc[3], s4[0][3] | s4[1][3] | s4[2][3] | s4[3][3]);
     }
 }
 
@@ -252,7 +267,7 @@ static int varying_common(int words, const void* k, uint64_t n, uint32_t* mask, 
     if (words == 1) { init[1] = 0ull; }
     if (hipMemcpyAsync(acc, init, sizeof init, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
     unsigned grid = (unsigned)((n + 255) / 256);
-    if (grid > 1024) grid = 1024;
+    if (grid > 512) grid = 512;
     if (grid == 0) grid = 1;
     if (words == 1) k_orand_u64<<<grid, 256, 0, s>>>((const uint64_t*)k, n, acc);
     else k_orand_u128<<<grid, 256, 0, s>>>((const uint4*)k, n, acc);
