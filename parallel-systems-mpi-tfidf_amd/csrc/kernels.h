@@ -11,7 +11,9 @@
 #define K1_NT        256                 /* threads per tokenize+count workgroup */
 #define K1_WIN       (K1_NT * 16)        /* bytes per window: one 16-byte group per thread */
 #define CHUNK_BYTES  16384u              /* nominal chunk (work unit) size */
-#define BIG_DOC      24576u              /* documents longer than this are split across chunks */
+#ifndef BIG_DOC
+#define BIG_DOC      49152u              /* documents longer than this are split across chunks */
+#endif
 #define K5_MAX_PAIRS 2048                /* largest complete (unmerged) document K5 sorts in LDS */
 
 /* status bits (device word) */
