@@ -161,6 +161,8 @@ def main():
             "tokens_per_s": round(T_all * args.steps / elapsed, 1),
             "device_ms_per_step": round(float(np.mean(tot_ms)), 4),
             "stage_ms": {k: round(v, 4) for k, v in info["stages"].items()},
+            "k1_work": {"chunks": int(info["nchunks"]), "partial_records": int(info["partial_records"]),
+                        "vocab_capacity": int(info["vocab_capacity"]), "terms": int(info["nterms"])},
             "roofline": {"bound": "hbm", "kernel": "k_tokcount_vs (K1)", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "alg_bytes_per_launch": int(alg_bytes),

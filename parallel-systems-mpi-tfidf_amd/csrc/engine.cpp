@@ -98,7 +98,7 @@ struct tfidf_ctx {
     DevBuf dense, vslot, skey0, skey1, seq0, seq1, rank_of_slot, slot_of_rank;
     DevBuf pkey0, pkey1, pseq0, pseq1, phead;
     DevBuf df_local, df_global, present, idf_vals;
-    DevBuf dkey0, dkey1, dseq0, dseq1, npairs_ord, out_off;
+    DevBuf dkey0, dkey1, dseq0, dseq1, npairs_ord, out_off, doc_meta;
     DevBuf out_term, out_cnt, out_score, idf_rank, large_list;
     DevBuf x_mine, x_send, x_recv, x_recv2, x_seq0, x_seq1, x_head, x_grank, x_dfv, x_cnt;
     uint32_t* sorted_dense = nullptr; /* points into seq0/seq1 */
@@ -204,7 +204,7 @@ void tfidf_close(tfidf_ctx* ctx) {
                       &ctx->skey1, &ctx->seq0, &ctx->seq1, &ctx->rank_of_slot, &ctx->slot_of_rank, &ctx->pkey0,
                       &ctx->pkey1, &ctx->pseq0, &ctx->pseq1, &ctx->phead, &ctx->df_local, &ctx->df_global,
                       &ctx->present, &ctx->idf_vals, &ctx->dkey0, &ctx->dkey1, &ctx->dseq0, &ctx->dseq1,
-                      &ctx->npairs_ord, &ctx->out_off, &ctx->out_term, &ctx->out_cnt,
+                      &ctx->npairs_ord, &ctx->out_off, &ctx->doc_meta, &ctx->out_term, &ctx->out_cnt,
                       &ctx->out_score, &ctx->idf_rank, &ctx->large_list, &ctx->x_mine, &ctx->x_send, &ctx->x_recv,
                       &ctx->x_recv2, &ctx->x_seq0, &ctx->x_seq1, &ctx->x_head, &ctx->x_grank, &ctx->x_dfv,
                       &ctx->x_cnt, &ctx->stamps};
@@ -440,7 +440,14 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
         LCHK(launch_part_keys(ctx->part_doc.as<uint32_t>(), ctx->part_slot.as<uint32_t>(), ctx->rank_of_slot.as<uint32_t>(),
                               Q, ctx->pkey0.as<uint64_t>(), ctx->pseq0.as<uint32_t>(), s));
         uint32_t pm = 0;
-        LCHK(key_varying_bytes_u64(ctx->pkey0.as<uint64_t>(), Q, &pm, ar, s));
+        /* key = (local doc << 32) | rank: the varying bytes follow from N and V (no probe,
+         * no host sync) */
+        {
+            const uint32_t rb = V > 1 ? 32u - (uint32_t)__builtin_clz(V - 1) : 1u;
+            const uint32_t db = N > 1 ? 32u - (uint32_t)__builtin_clz(N - 1) : 1u;
+            for (uint32_t b = 0; b < (rb + 7) / 8; ++b) pm |= 1u << b;
+            for (uint32_t b = 0; b < (db + 7) / 8; ++b) pm |= 1u << (4 + b);
+        }
         int pc = radix_sort_u64(ctx->pkey0.as<uint64_t>(), ctx->pseq0.as<uint32_t>(), ctx->pkey1.as<uint64_t>(),
                                 ctx->pseq1.as<uint32_t>(), Q, pm, ar, s);
         LCHK(pc);
@@ -507,12 +514,15 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     ENSURE(ctx->out_off, (size_t)N * 8 + 8);
     LCHK(launch_doc_keys(dev_ids, N, ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), s));
     uint32_t dm = 0;
-    LCHK(key_varying_bytes_u64(ctx->dkey0.as<uint64_t>(), N, &dm, ar, s));
+    dm = 0x1Fu; /* base-11 keys of 10 digits are < 11^10 < 2^35: five bytes, no probe */
     int dc = radix_sort_u64(ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), ctx->dkey1.as<uint64_t>(),
                             ctx->dseq1.as<uint32_t>(), N, dm, ar, s);
     LCHK(dc);
     ctx->order = dc ? ctx->dseq1.as<uint32_t>() : ctx->dseq0.as<uint32_t>();
-    LCHK(launch_gather_npairs(ctx->order, ctx->doc_npairs.as<uint32_t>(), N, ctx->npairs_ord.as<uint64_t>(), s));
+    ENSURE(ctx->doc_meta, (size_t)N * 16 + 16);
+    LCHK(launch_gather_meta(ctx->order, ctx->doc_npairs.as<uint32_t>(), ctx->doc_recoff.as<uint64_t>(),
+                            ctx->doc_size.as<uint32_t>(), ctx->doc_flags.as<uint8_t>(), N,
+                            ctx->npairs_ord.as<uint64_t>(), ctx->doc_meta.as<uint4>(), s));
     LCHK(scan_excl_u64(ctx->npairs_ord.as<uint64_t>(), ctx->out_off.as<uint64_t>(), N, ar, s));
     uint64_t P = 0;
     HIPCHK(hipMemcpyAsync(&P, ctx->out_off.as<uint64_t>() + N, 8, hipMemcpyDeviceToHost, s));
@@ -527,6 +537,7 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     ENSURE(ctx->large_list, (size_t)N * 4 + 8);
     K5Args a{};
     a.order = ctx->order;
+    a.meta = ctx->doc_meta.as<uint4>();
     a.out_off = ctx->out_off.as<uint64_t>();
     a.doc_recoff = ctx->doc_recoff.as<uint64_t>();
     a.doc_npairs = ctx->doc_npairs.as<uint32_t>();

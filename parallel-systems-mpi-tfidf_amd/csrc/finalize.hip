@@ -313,15 +313,27 @@ int launch_doc_keys(const uint32_t* doc_ids, uint32_t ndocs, uint64_t* keys, uin
     k_doc_keys<<<grid_for(ndocs), NT, 0, s>>>(doc_ids, ndocs, keys, seq);
     return ok();
 }
-__global__ void k_gather_npairs(const uint32_t* __restrict__ order, const uint32_t* __restrict__ np, uint32_t n,
-                                uint64_t* __restrict__ out) {
+/* per output position i (document order[i]): its pair count for the offsets scan, and
+ * the packed K5 metadata {record offset lo, hi, npairs | flags << 30, docSize} so that
+ * K5 reads one coalesced 16-byte word per document instead of a dependent chain */
+__global__ void k_gather_meta(const uint32_t* __restrict__ order, const uint32_t* __restrict__ np,
+                              const uint64_t* __restrict__ recoff, const uint32_t* __restrict__ dsize,
+                              const uint8_t* __restrict__ flags, uint32_t n, uint64_t* __restrict__ out,
+                              uint4* __restrict__ meta) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = np[order[i]];
+    if (i >= n) return;
+    const uint32_t d = order[i];
+    const uint32_t c = np[d];
+    const uint64_t rb = c ? recoff[d] : 0ull;
+    out[i] = c;
+    meta[i] = make_uint4((uint32_t)rb, (uint32_t)(rb >> 32), (c & 0x3FFFFFFFu) | ((uint32_t)(flags[d] & 3u) << 30), dsize[d]);
 }
-int launch_gather_npairs(const uint32_t* order, const uint32_t* doc_npairs, uint32_t ndocs, uint64_t* out,
-                         hipStream_t s) {
+int launch_gather_meta(const uint32_t* order, const uint32_t* doc_npairs, const uint64_t* doc_recoff,
+                       const uint32_t* doc_size, const uint8_t* doc_flags, uint32_t ndocs, uint64_t* npairs_ord,
+                       uint4* meta, hipStream_t s) {
     if (!ndocs) return 0;
-    k_gather_npairs<<<grid_for(ndocs), NT, 0, s>>>(order, doc_npairs, ndocs, out);
+    k_gather_meta<<<grid_for(ndocs), NT, 0, s>>>(order, doc_npairs, doc_recoff, doc_size, doc_flags, ndocs,
+                                                npairs_ord, meta);
     return ok();
 }
 
@@ -370,22 +382,27 @@ __global__ __launch_bounds__(NT) void k_score_wave(K5Args a) {
     __shared__ uint32_t kb[NT / 64][2][K5_WAVE];
     __shared__ uint32_t hist[NT / 64][256];
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t i = blockIdx.x * (NT / 64) + w;
-    if (i >= a.ndocs) return;
-    const uint32_t d = a.order[i];
-    const uint32_t n = a.doc_npairs[d];
-    const bool presorted = (a.doc_flags[d] & DF_PRESORTED) != 0;
-    if (n == 0) return;
+    const uint32_t stride = gridDim.x * (NT / 64);
+    /* persistent waves: each wave walks output positions i, i + stride, ...; the next
+     * position's metadata word is loaded while the current document is sorted */
+    uint32_t i = blockIdx.x * (NT / 64) + w;
+    uint4 mnext = i < a.ndocs ? a.meta[i] : make_uint4(0, 0, 0, 0);
+    for (; i < a.ndocs; i += stride) {
+    const uint4 mc = mnext;
+    if (i + stride < a.ndocs) mnext = a.meta[i + stride];
+    const uint32_t n = mc.z & 0x3FFFFFFFu;
+    const bool presorted = ((mc.z >> 30) & DF_PRESORTED) != 0;
+    if (n == 0) continue;
     if (!k5_by_wave(a, n, presorted)) { /* hand the document to k_score_large's list */
         if (lane == 0) a.large_list[atomicAdd(a.large_count, 1u)] = i;
-        return;
+        continue;
     }
-    const uint64_t ob = a.out_off[i], rb = a.doc_recoff[d];
-    if (rb + n > a.rec_total) { if (lane == 0) atomicOr(a.status, ST_BOUNDS); return; }
-    const double ds = (double)a.doc_size[d];
+    const uint64_t ob = a.out_off[i], rb = ((uint64_t)mc.y << 32) | mc.x;
+    if (rb + n > a.rec_total) { if (lane == 0) atomicOr(a.status, ST_BOUNDS); continue; }
+    const double ds = (double)mc.w;
     if (presorted) {
         for (uint32_t j = lane; j < n; j += 64) k5_emit(a, ob + j, ds, k5_rank(a, a.rec_slot[rb + j]), a.rec_cnt[rb + j]);
-        return;
+        continue;
     }
     if (n <= K5_SMALL) {
         uint32_t key = 0xFFFFFFFFu, val = 0;
@@ -400,7 +417,7 @@ __global__ __launch_bounds__(NT) void k_score_wave(K5Args a) {
             }
         }
         if (lane < n) k5_emit(a, ob + lane, ds, key, val);
-        return;
+        continue;
     }
     uint32_t* buf0 = kb[w][0];
     uint32_t* buf1 = kb[w][1];
@@ -489,6 +506,9 @@ __global__ __launch_bounds__(NT) void k_score_wave(K5Args a) {
             }
         }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }  /* persistent loop */
 }
 
 /* Documents the wave kernel leaves: one workgroup each.  Presorted (merged) runs are
@@ -575,7 +595,16 @@ int launch_score_order(const K5Args& a, hipStream_t s) {
     if (hipMemsetAsync(a.large_count, 0, 4, s) != hipSuccess) return -1;
     k_idf_of_rank<<<grid_for(a.nterms ? a.nterms : 1), NT, 0, s>>>(a.df_of_rank, a.idf_idx, a.idf, a.nterms,
                                                                   a.idf_rank);
-    k_score_wave<<<(a.ndocs + NT / 64 - 1) / (NT / 64), NT, 0, s>>>(a);
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+    }
+    const uint32_t wg_need = (a.ndocs + NT / 64 - 1) / (NT / 64);
+    const uint32_t wg = wg_need < (uint32_t)ncu * 4u ? wg_need : (uint32_t)ncu * 4u; /* 36 KB LDS: 4 per CU */
+    k_score_wave<<<wg, NT, 0, s>>>(a);
     const uint32_t grid = a.ndocs < 2048u ? a.ndocs : 2048u; /* persistent over the handed-off list */
     k_score_large<<<grid, NT, 0, s>>>(a);
     return ok();

@@ -10,7 +10,9 @@
 /* chunking (K0/K1) */
 #define K1_NT        256                 /* threads per tokenize+count workgroup */
 #define K1_WIN       (K1_NT * 16)        /* bytes per window: one 16-byte group per thread */
+#ifndef CHUNK_BYTES
 #define CHUNK_BYTES  16384u              /* nominal chunk (work unit) size */
+#endif
 #ifndef BIG_DOC
 #define BIG_DOC      49152u              /* documents longer than this are split across chunks */
 #endif
@@ -112,10 +114,12 @@ int launch_df_list(const uint32_t* present_scan, uint64_t nvals, uint32_t* vals,
 
 /* documents: name order key and output */
 int launch_doc_keys(const uint32_t* doc_ids, uint32_t ndocs, uint64_t* keys, uint32_t* seq, hipStream_t s);
-int launch_gather_npairs(const uint32_t* order, const uint32_t* doc_npairs, uint32_t ndocs, uint64_t* out,
-                         hipStream_t s);
+int launch_gather_meta(const uint32_t* order, const uint32_t* doc_npairs, const uint64_t* doc_recoff,
+                       const uint32_t* doc_size, const uint8_t* doc_flags, uint32_t ndocs, uint64_t* npairs_ord,
+                       uint4* meta, hipStream_t s);
 struct K5Args {
     const uint32_t* order;       /* docs in output order */
+    const uint4* meta;           /* per output position: {recoff lo, hi, npairs | flags << 30, docSize} */
     const uint64_t* out_off;     /* per output position */
     const uint64_t* doc_recoff;
     const uint32_t* doc_npairs;

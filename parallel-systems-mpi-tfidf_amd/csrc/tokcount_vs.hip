@@ -38,7 +38,8 @@
 #include "kernels.h"
 
 /* timing-only ablation builds (make abl): 1 no vocabulary load, 2 no LDS counting,
- * 4 no token rounds, 8 no token-list writes, 16 no docSize adds, 32 no corpus loads */
+ * 4 no token rounds, 8 no token-list writes, 16 no docSize adds, 32 no corpus loads,
+ * 64 no claim accounting, 128 first LDS probe only */
 #ifndef K1_ABL
 #define K1_ABL 0
 #endif
@@ -48,17 +49,17 @@ namespace {
 constexpr int NT = 256;
 constexpr int NWAVE = NT / 64;
 constexpr int WSTEP = 1024;               /* bytes per wave step: one 16-byte group per lane */
-constexpr int TB = 4096;                  /* LDS table entries (u64) */
+#ifndef K1_TB
+#define K1_TB 4096
+#endif
+constexpr int TB = K1_TB;                 /* LDS table entries (u64), a power of two */
 constexpr int EPT = TB / NT;              /* table entries per thread in a flush */
 constexpr uint32_t FILL_LIMIT = TB - NT * 2 - 64; /* claims after which overflow mode starts */
 constexpr int GCAP = 256;                 /* documents per group (doc-in-group: 8 bits) */
 constexpr uint32_t SLOT_BITS = 28;
 constexpr uint32_t CNT_BITS = 24;
 constexpr uint64_t CNT_MASK = (1ull << CNT_BITS) - 1ull;
-#ifndef K1_KB
-#define K1_KB 2
-#endif
-constexpr int KB = K1_KB;                 /* tokens per lane whose vocabulary loads fly together */
+
 constexpr int TLW = 2 * GCAP * 4 / 2 / NWAVE; /* token-list entries per wave (shares dcnt/doff) */
 
 /* Diagnostic build only (-DK1_STAMPS, lib/libtfidf_hip_stamps.so): thread 0 sums
@@ -126,7 +127,7 @@ __device__ __forceinline__ uint32_t bounds_ws(uint64_t pos, uint64_t lo, uint64_
 
 __device__ __forceinline__ uint32_t tbl_hash(uint64_t key) {
     const uint32_t k = (uint32_t)key ^ (uint32_t)(key >> 28) * 0x9E3779B1u;
-    return (k * 0x85EBCA6Bu) >> (32 - 12);
+    return (k * 0x85EBCA6Bu) >> (32 - 13);   /* & (TB - 1) by the callers */
 }
 
 /* wave-uniform copy of a value the compiler keeps in VGPRs (LDS-loaded) */
@@ -176,15 +177,24 @@ __device__ __forceinline__ void overflow_pair(VsShared& S, const K1Out& o, uint6
 }
 
 /* Counts `key` into the table from slot h (the first probe already returned `old`: a
- * CAS, or a plain read in overflow mode).  Returns 1 when this call claimed an entry.
+ * CAS, or a plain read in overflow mode; `nx` is a plain read of slot h+1 issued in the
+ * same LDS batch, so the common collision costs no extra round trip before the second
+ * probe decision).  Returns 1 when this call claimed an entry.
  * A probe sequence longer than PMAX also goes to the partial stream: a pair counted
  * partly in the table and partly as partial records is still summed exactly by the
  * merge, so the table can never fill up or loop. */
 constexpr int PMAX = 64;
 __device__ __forceinline__ uint32_t tbl_count(VsShared& S, const K1Out& o, uint64_t key, uint32_t h,
-                                              unsigned long long old, bool over, uint32_t gd0) {
+                                              unsigned long long old, unsigned long long nx, bool over,
+                                              uint32_t gd0) {
     const unsigned long long ent = (key << CNT_BITS) | 1ull;
-    for (int probe = 1;; ++probe) {
+    if (old != 0ull && (old >> CNT_BITS) != key) {
+        /* collision at h: the read-ahead of h+1 decides without a dependent probe */
+        h = (h + 1) & (TB - 1);
+        if ((nx >> CNT_BITS) == key && nx != 0ull) { atomicAdd(&S.T[h], 1ull); return 0u; }
+        old = (nx == 0ull && !over) ? atomicCAS(&S.T[h], 0ull, ent) : nx;
+    }
+    for (int probe = 2;; ++probe) {
         if (old == 0ull) {
             if (!over) return 1u;
             break;
@@ -282,7 +292,10 @@ __device__ void vs_flush(VsShared& S, const K1Out& o, uint32_t gd0, uint32_t ng,
 }  // namespace
 
 /* Persistent: a grid of (CUs x 4) workgroups walks the chunks [c0, c1) round-robin. */
-__global__ __launch_bounds__(NT, 4) void k_tokcount_vs(CorpusDev c, const uint64_t* __restrict__ chunk_start,
+#ifndef K1_WAVES_PER_SIMD
+#define K1_WAVES_PER_SIMD 4
+#endif
+__global__ __launch_bounds__(NT, K1_WAVES_PER_SIMD) void k_tokcount_vs(CorpusDev c, const uint64_t* __restrict__ chunk_start,
                                                        const uint32_t* __restrict__ chunk_doc, uint64_t c0,
                                                        uint64_t c1, VocabDev v, K1Out o) {
     __shared__ __attribute__((aligned(16))) VsShared S;
@@ -302,11 +315,78 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_vs(CorpusDev c, const uint64
 #endif
     STAMP(st, 0);
 
+    /* one token round of the wave (one token per lane): its key, document, vocabulary
+     * hash and the two vocabulary slots loaded for it */
+    struct Round {
+        uint64_t klo, khi, ap;
+        uint32_t hv, rel, kind;
+        uint4 s4, t4;
+    };
+    Round pend{};
+    bool pending = false;
+    uint32_t gd0_cur = 0;
+    /* finish a round: vocabulary slot (miss path: lock-free insert / long term), docSize,
+     * LDS (doc, slot) count, overflow accounting */
+    auto claims_finish = [&](const Round& r) {
+        uint32_t slot = INVALID_SLOT;
+        if (r.kind == 1u) {
+            const bool hit0 = r.s4.x == (uint32_t)r.klo && r.s4.y == (uint32_t)(r.klo >> 32) &&
+                              r.s4.z == (uint32_t)r.khi && r.s4.w == (uint32_t)(r.khi >> 32);
+            const bool hit1 = r.t4.x == (uint32_t)r.klo && r.t4.y == (uint32_t)(r.klo >> 32) &&
+                              r.t4.z == (uint32_t)r.khi && r.t4.w == (uint32_t)(r.khi >> 32);
+            CNT(1, (hit0 || hit1) ? 0 : 1);
+            slot = hit0 ? r.hv : hit1 ? ((r.hv + 1) & (uint32_t)v.mask) : vocab_insert(v, r.klo, r.khi, 0, o.status);
+        } else if (r.kind == 2u) {
+            slot = slow_slot(c.bytes, v, r.ap, S.gdoc[r.rel + 1], o.status);
+        }
+        STAMP(st, 7);
+        /* docSize: one LDS add per wave when the round's tokens share a document */
+        if (!(K1_ABL & 16)) {
+            const uint64_t vm = __ballot(r.kind != 0u);
+            if (vm) {
+                const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.rel);
+                if (__ballot(r.kind != 0u && r.rel != r0) == 0ull) {
+                    if (lane == 0) atomicAdd(&S.dsz[r0], (uint32_t)__popcll(vm));
+                } else if (r.kind) {
+                    atomicAdd(&S.dsz[r.rel], 1u);
+                }
+            }
+        }
+        STAMP(st, 8);
+        if (K1_ABL & 2) return;
+        /* invalid slot: status flagged, the run is retried */
+        const uint64_t key = slot == INVALID_SLOT ? ~0ull : (((uint64_t)r.rel << SLOT_BITS) | slot);
+        const uint32_t hl = tbl_hash(key) & (TB - 1);
+        /* first LDS probe: a CAS claim, or a plain read in overflow mode */
+        const bool over = S.over != 0;
+        uint32_t claims = 0;
+        if (key != ~0ull) {
+            const unsigned long long old = over ? S.T[hl] : atomicCAS(&S.T[hl], 0ull, (key << CNT_BITS) | 1ull);
+            const unsigned long long nx = S.T[(hl + 1) & (TB - 1)];
+#if K1_ABL & 128
+            claims = old == 0ull ? 1u : 0u;
+            (void)nx;
+#else
+            claims = tbl_count(S, o, key, hl, old, nx, over, gd0_cur);
+#endif
+        }
+        STAMP(st, 9);
+        if (K1_ABL & 64) return;
+        /* claims -> overflow mode: one LDS add per wave and round */
+        const uint32_t wc = wave_sum(claims);
+        if (wc && lane == 0) {
+            const uint32_t f = atomicAdd(&S.fill, wc);
+            if (f + wc >= FILL_LIMIT) S.over = 1;
+        }
+        STAMP(st, 10);
+    };
+
     for (uint64_t chunk = c0 + blockIdx.x; chunk < c1; chunk += gridDim.x) {
         const uint64_t cs = chunk_start[chunk], ce = chunk_start[chunk + 1];
         if (cs >= ce) continue;
         const uint32_t dfirst = chunk_doc[chunk], dlast = chunk_doc[chunk + 1];
         for (uint32_t gd0 = dfirst; gd0 <= dlast; gd0 += GCAP) {
+            gd0_cur = gd0;
             const uint32_t ng = (dlast + 1 - gd0) < (uint32_t)GCAP ? (dlast + 1 - gd0) : (uint32_t)GCAP;
             for (uint32_t k = tid; k <= ng; k += NT) S.gdoc[k] = c.doc_off[gd0 + k];
             if (tid < GCAP) { S.dsz[tid] = 0; S.dpart[tid] = 0; S.drun[tid] = 0; }
@@ -413,14 +493,13 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_vs(CorpusDev c, const uint64
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                         const uint32_t cnt = (ntok - base) < (uint32_t)TLW ? (ntok - base) : (uint32_t)TLW;
                         STAMP(st, 5);
-                        /* ---- resolve + count, KB tokens per lane per round, all lanes busy ---- */
-                        for (uint32_t t0 = 0; t0 < cnt && !(K1_ABL & 4); t0 += 64 * KB) {
-                            uint64_t klo[KB], khi[KB];
-                            uint32_t hv[KB], relk[KB], posk[KB], kind[KB];
-                            uint4 s4[KB], t4[KB];
-#pragma unroll
-                            for (int k = 0; k < KB; ++k) {
-                                const uint32_t t = t0 + 64 * k + lane;
+                        /* ---- resolve + count, 64 tokens per round, all lanes busy; the
+                         * vocabulary loads of round r+1 are issued before round r is
+                         * counted (one round in flight, also across steps) ---- */
+                        for (uint32_t t0 = 0; t0 < cnt && !(K1_ABL & 4); t0 += 64) {
+                            Round q;
+                            {
+                                const uint32_t t = t0 + lane;
                                 const bool val = t < cnt;
                                 const uint32_t pos = val ? (uint32_t)tl[t] : 0u;
                                 const uint32_t src = pos >> 4, i = pos & 15u;
@@ -438,84 +517,28 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_vs(CorpusDev c, const uint64
                                 const uint64_t a = i < 8 ? q0 : q1, b = i < 8 ? q1 : q2, cc = i < 8 ? q2 : q3;
                                 const uint64_t lo = sh ? (a >> sh) | (b << (64 - sh)) : a;
                                 const uint64_t hi = sh ? (b >> sh) | (cc << (64 - sh)) : b;
-                                kind[k] = val ? (make_short_key(lo, hi, len, &klo[k], &khi[k]) < 16u ? 1u : 2u) : 0u;
-                                posk[k] = pos;
+                                q.kind = val ? (make_short_key(lo, hi, len, &q.klo, &q.khi) < 16u ? 1u : 2u) : 0u;
+                                q.ap = sb + pos;
                                 /* document: wr plus the step's document starts at or before the token */
-                                const uint64_t ap = sb + pos;
                                 uint32_t rel = wr;
-                                for (uint32_t q = wr + 1; q < kend; ++q) rel += uni64(S.gdoc[q]) <= ap ? 1u : 0u;
-                                relk[k] = rel;
-                                hv[k] = kind[k] == 1u ? (uint32_t)(key_hash(klo[k], khi[k]) & v.mask) : 0u;
+                                for (uint32_t k = wr + 1; k < kend; ++k) rel += uni64(S.gdoc[k]) <= q.ap ? 1u : 0u;
+                                q.rel = rel;
+                                q.hv = q.kind == 1u ? (uint32_t)(key_hash(q.klo, q.khi) & v.mask) : 0u;
 #if K1_ABL & 1
-                                s4[k] = make_uint4((uint32_t)klo[k], (uint32_t)(klo[k] >> 32), (uint32_t)khi[k], (uint32_t)(khi[k] >> 32));
-                                t4[k] = s4[k];
-                                if (kind[k] == 2u) kind[k] = 1u;
+                                q.s4 = make_uint4((uint32_t)q.klo, (uint32_t)(q.klo >> 32), (uint32_t)q.khi, (uint32_t)(q.khi >> 32));
+                                q.t4 = q.s4;
+                                if (q.kind == 2u) q.kind = 1u;
 #else
                                 /* the home slot and the next one: a key displaced by one slot
                                  * (linear probing) still resolves without a dependent load */
-                                s4[k] = v.keys[hv[k]];
-                                t4[k] = v.keys[(hv[k] + 1) & (uint32_t)v.mask];
+                                q.s4 = v.keys[q.hv];
+                                q.t4 = v.keys[(q.hv + 1) & (uint32_t)v.mask];
 #endif
                             }
                             STAMP(st, 6);
-                            uint64_t key[KB];
-                            uint32_t hl[KB];
-#pragma unroll
-                            for (int k = 0; k < KB; ++k) {
-                                uint32_t slot = INVALID_SLOT;
-                                if (kind[k] == 1u) {
-                                    const bool hit0 = s4[k].x == (uint32_t)klo[k] && s4[k].y == (uint32_t)(klo[k] >> 32) &&
-                                                      s4[k].z == (uint32_t)khi[k] && s4[k].w == (uint32_t)(khi[k] >> 32);
-                                    const bool hit1 = t4[k].x == (uint32_t)klo[k] && t4[k].y == (uint32_t)(klo[k] >> 32) &&
-                                                      t4[k].z == (uint32_t)khi[k] && t4[k].w == (uint32_t)(khi[k] >> 32);
-                                    CNT(1, (hit0 || hit1) ? 0 : 1);
-                                    slot = hit0 ? hv[k] : hit1 ? ((hv[k] + 1) & (uint32_t)v.mask)
-                                                               : vocab_insert(v, klo[k], khi[k], 0, o.status);
-                                } else if (kind[k] == 2u) {
-                                    slot = slow_slot(c.bytes, v, sb + posk[k], S.gdoc[relk[k] + 1], o.status);
-                                }
-                                /* invalid slot: status flagged, the run is retried */
-                                key[k] = slot == INVALID_SLOT ? ~0ull : (((uint64_t)relk[k] << SLOT_BITS) | slot);
-                                hl[k] = tbl_hash(key[k]) & (TB - 1);
-                            }
-                            STAMP(st, 7);
-                            /* docSize: one LDS add per wave when the round's tokens share a document */
-#pragma unroll
-                            for (int k = 0; k < KB && !(K1_ABL & 16); ++k) {
-                                const uint64_t vm = __ballot(kind[k] != 0u);
-                                if (!vm) continue;
-                                const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)relk[k]);
-                                if (__ballot(kind[k] != 0u && relk[k] != r0) == 0ull) {
-                                    if (lane == 0) atomicAdd(&S.dsz[r0], (uint32_t)__popcll(vm));
-                                } else if (kind[k]) {
-                                    atomicAdd(&S.dsz[relk[k]], 1u);
-                                }
-                            }
-                            /* first LDS probes issued together (one lane's LDS operations execute
-                             * in order, so a repeated key sees its claim); in overflow mode the
-                             * first probe is a plain read */
-                            STAMP(st, 8);
-                            if (K1_ABL & 2) continue;
-                            const bool over = S.over != 0;
-                            unsigned long long old[KB];
-#pragma unroll
-                            for (int k = 0; k < KB; ++k) {
-                                old[k] = 1ull;
-                                if (key[k] != ~0ull)
-                                    old[k] = over ? S.T[hl[k]] : atomicCAS(&S.T[hl[k]], 0ull, (key[k] << CNT_BITS) | 1ull);
-                            }
-                            uint32_t claims = 0;
-#pragma unroll
-                            for (int k = 0; k < KB; ++k)
-                                if (key[k] != ~0ull) claims += tbl_count(S, o, key[k], hl[k], old[k], over, gd0);
-                            STAMP(st, 9);
-                            /* claims -> overflow mode: one LDS add per wave and round */
-                            const uint32_t wc = wave_sum(claims);
-                            if (wc && lane == 0) {
-                                const uint32_t f = atomicAdd(&S.fill, wc);
-                                if (f + wc >= FILL_LIMIT) S.over = 1;
-                            }
-                            STAMP(st, 10);
+                            if (pending) claims_finish(pend);
+                            pend = q;
+                            pending = true;
                         }
                         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                         __builtin_amdgcn_wave_barrier();
@@ -523,6 +546,7 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_vs(CorpusDev c, const uint64
                     }
                 }
             }
+            if (pending) { claims_finish(pend); pending = false; }
             STAMP(st, 1);
             /* group end is a document boundary (or the chunk end): emit everything */
             vs_flush(S, o, gd0, ng, cs, ce);
