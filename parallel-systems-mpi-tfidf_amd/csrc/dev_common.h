@@ -157,14 +157,23 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(v), 63);
 }
 
+/* Workgroup barrier that orders LDS only.  __syncthreads() is a release/acquire fence over
+ * all address spaces, so it also waits for every outstanding global store of the wave
+ * (vmcnt(0)); kernels whose barriers only publish LDS data use this one. */
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 /* exclusive scan over the block (blockDim = NT, multiple of 64); wsum: NT/64 words LDS.
- * Returns exclusive prefix; *total = block sum.  Contains two __syncthreads(). */
-template <int NT>
+ * Returns exclusive prefix; *total = block sum.  Contains two barriers. */
+template <int NT, bool LDS_ONLY = false>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* total) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t inc = wave_incl_scan(v);
     if (lane == 63) wsum[w] = inc;
-    __syncthreads();
+    if (LDS_ONLY) lds_barrier(); else __syncthreads();
     uint32_t base = 0, tot = 0;
 #pragma unroll
     for (int k = 0; k < NT / 64; ++k) {
@@ -173,7 +182,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
         tot += s;
     }
     *total = tot;
-    __syncthreads();
+    if (LDS_ONLY) lds_barrier(); else __syncthreads();
     return base + inc - v;
 }
 

@@ -208,20 +208,53 @@ __device__ __forceinline__ uint32_t tbl_count(VsShared& S, const K1Out& o, uint6
     return 0u;
 }
 
+/* ctr[idx] += 1 for every active lane.  Most table entries of a flush belong to one
+ * document, so a per-lane atomic would serialise up to 64 same-address LDS updates per
+ * instruction: when the active lanes agree on idx one lane adds the popcount. */
+__device__ __forceinline__ void wave_agg_add(uint32_t* ctr, uint32_t idx) {
+    const uint32_t i0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);
+    const uint64_t am = __ballot(1);
+    if (__ballot(idx != i0) == 0ull) {
+        if (__builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u)) == 0u)
+            atomicAdd(&ctr[i0], (uint32_t)__popcll(am));
+    } else {
+        atomicAdd(&ctr[idx], 1u);
+    }
+}
+/* as wave_agg_add, returning this lane's old value (distinct per lane: a running rank) */
+__device__ __forceinline__ uint32_t wave_agg_add_rtn(uint32_t* ctr, uint32_t idx) {
+    const uint32_t i0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);
+    const uint64_t am = __ballot(1);
+    uint32_t k;
+    if (__ballot(idx != i0) == 0ull) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u));
+        uint32_t b = 0;
+        if (rank == 0u) b = atomicAdd(&ctr[i0], (uint32_t)__popcll(am));
+        k = (uint32_t)__builtin_amdgcn_readfirstlane((int)b) + rank;
+    } else {
+        k = atomicAdd(&ctr[idx], 1u);
+    }
+    return k;
+}
+
 /* Emits every table entry of the group as records and clears the table. */
 __device__ void vs_flush(VsShared& S, const K1Out& o, uint32_t gd0, uint32_t ng, uint64_t cs, uint64_t ce) {
-    const int tid = threadIdx.x;
-    __syncthreads();   /* every wave's walk is done (the token lists alias dcnt/doff) */
+    /* opaque copy of the thread index: keeps the per-entry indices (j * NT + tid) from being
+     * hoisted out of the chunk loop and spilled — reloading them from scratch in the
+     * write-out loop waited on every outstanding record store (vmcnt(0)) per iteration */
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    lds_barrier();   /* every wave's walk is done (the token lists alias dcnt/doff) */
     if (tid < GCAP) S.dcnt[tid] = 0;
-    __syncthreads();
+    lds_barrier();
     /* pass 1: entries into registers (lane-consecutive, conflict-free), per-document counts */
     unsigned long long e[EPT];
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
         e[j] = S.T[j * NT + tid];
-        if (e[j]) atomicAdd(&S.dcnt[(uint32_t)(e[j] >> (CNT_BITS + SLOT_BITS))], 1u);
+        if (e[j]) wave_agg_add(&S.dcnt[0], (uint32_t)(e[j] >> (CNT_BITS + SLOT_BITS)));
     }
-    __syncthreads();
+    lds_barrier();
     /* per-document decision, one thread per document */
     uint32_t packed = 0;
     if ((uint32_t)tid < ng) {
@@ -237,18 +270,20 @@ __device__ void vs_flush(VsShared& S, const K1Out& o, uint32_t gd0, uint32_t ng,
         S.dstate[tid] = st;
     }
     uint32_t tot;
-    const uint32_t off = block_excl_scan<NT>(packed, S.wsum, &tot);
+    const uint32_t off = block_excl_scan<NT, true>(packed, S.wsum, &tot);
     if ((uint32_t)tid < ng) S.doff[tid] = off;
     const uint32_t nrec = tot & 0xFFFFu, npart = tot >> 16, ntot = nrec + npart;
+    /* the two allocations in different waves, so their L2 round trips overlap */
     if (tid == 0) {
         const unsigned long long rb = nrec ? atomicAdd(o.rec_alloc, (unsigned long long)nrec) : 0ull;
-        const unsigned long long pb = npart ? atomicAdd(o.part_alloc, (unsigned long long)npart) : 0ull;
         if (rb + nrec > o.rec_cap) atomicOr(o.status, ST_REC_FULL);
-        if (pb + npart > o.part_cap) atomicOr(o.status, ST_PART_FULL);
         S.rec_base = rb;
+    } else if (tid == 64) {
+        const unsigned long long pb = npart ? atomicAdd(o.part_alloc, (unsigned long long)npart) : 0ull;
+        if (pb + npart > o.part_cap) atomicOr(o.status, ST_PART_FULL);
         S.part_base = pb;
     }
-    __syncthreads();
+    lds_barrier();
     const unsigned long long rb = S.rec_base, pb = S.part_base;
     const bool rec_ok = rb + nrec <= o.rec_cap, part_ok = pb + npart <= o.part_cap;
     if ((uint32_t)tid < ng && S.dstate[tid] == 2) {
@@ -259,16 +294,17 @@ __device__ void vs_flush(VsShared& S, const K1Out& o, uint32_t gd0, uint32_t ng,
      * records [0, nrec), partial records [nrec, ntot) — for coalesced HBM writes */
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
-        if (!e[j]) continue;
-        const uint32_t rel = (uint32_t)(e[j] >> (CNT_BITS + SLOT_BITS));
-        const uint32_t slot = (uint32_t)(e[j] >> CNT_BITS) & ((1u << SLOT_BITS) - 1u);
-        const uint64_t cnt = e[j] & CNT_MASK;
-        const uint32_t k = atomicAdd(&S.drun[rel], 1u);
-        const uint32_t dof = S.doff[rel];
-        if (S.dstate[rel] == 2) S.T[(dof & 0xFFFFu) + k] = slot | (cnt << 32);
-        else S.T[nrec + (dof >> 16) + k] = slot | ((uint64_t)rel << SLOT_BITS) | (cnt << 36);
+        if (e[j]) {
+            const uint32_t rel = (uint32_t)(e[j] >> (CNT_BITS + SLOT_BITS));
+            const uint32_t slot = (uint32_t)(e[j] >> CNT_BITS) & ((1u << SLOT_BITS) - 1u);
+            const uint64_t cnt = e[j] & CNT_MASK;
+            const uint32_t k = wave_agg_add_rtn(&S.drun[0], rel);
+            const uint32_t dof = S.doff[rel];
+            if (S.dstate[rel] == 2) S.T[(dof & 0xFFFFu) + k] = slot | (cnt << 32);
+            else S.T[nrec + (dof >> 16) + k] = slot | ((uint64_t)rel << SLOT_BITS) | (cnt << 36);
+        }
     }
-    __syncthreads();
+    lds_barrier();
     /* coalesced write-out; each thread then clears exactly the entries it read */
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
@@ -391,7 +427,7 @@ __global__ __launch_bounds__(NT, K1_WAVES_PER_SIMD) void k_tokcount_vs(CorpusDev
             for (uint32_t k = tid; k <= ng; k += NT) S.gdoc[k] = c.doc_off[gd0 + k];
             if (tid < GCAP) { S.dsz[tid] = 0; S.dpart[tid] = 0; S.drun[tid] = 0; }
             if (tid == 0) { S.fill = 0; S.over = 0; }
-            __syncthreads();
+            lds_barrier();
             const uint64_t g0 = uni64(S.gdoc[0]), gn = uni64(S.gdoc[ng]);
             const uint64_t gs = g0 > cs ? g0 : cs;
             const uint64_t ge = gn < ce ? gn : ce;
@@ -547,6 +583,10 @@ __global__ __launch_bounds__(NT, K1_WAVES_PER_SIMD) void k_tokcount_vs(CorpusDev
                 }
             }
             if (pending) { claims_finish(pend); pending = false; }
+#ifdef K1_STAMPS
+            STAMP(st, 10);
+            lds_barrier();   /* diagnostic: separates the wait for the other waves */
+#endif
             STAMP(st, 1);
             /* group end is a document boundary (or the chunk end): emit everything */
             vs_flush(S, o, gd0, ng, cs, ce);
@@ -559,7 +599,7 @@ __global__ __launch_bounds__(NT, K1_WAVES_PER_SIMD) void k_tokcount_vs(CorpusDev
                     else atomicAdd(&o.doc_size[d], n);
                 }
             }
-            __syncthreads();
+            lds_barrier();
             STAMP(st, 3);
             if (gd0 + GCAP < gd0) break; /* overflow guard */
         }

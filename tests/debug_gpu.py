@@ -62,6 +62,7 @@ def stamps():
     names = ["group setup", "walk tail", "flush", "docsize write", "classify", "compact",
              "round: keys+loads", "round: compare+miss", "round: docsize", "round: LDS count",
              "round: claims", "step loop top"]
+    names[1] = "barrier wait (walk imbalance)"
     p = tfidf_configs.plan("c2", scale=float(os.environ.get("SCALE", "1.0")))
     with tfidf_abi.Engine(0) as e:
         c = e.synth_device(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"], p["ndocs_total"])
