@@ -152,6 +152,16 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
+/* max over the wave, uniform (scalar) result */
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t t = (uint32_t)__shfl_xor((int)v, o, 64);
+        v = t > v ? t : v;
+    }
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
 /* sum over the wave, uniform (scalar) result */
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(v), 63);

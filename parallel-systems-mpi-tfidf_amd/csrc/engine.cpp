@@ -418,10 +418,16 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     ENSURE(ctx->slot_of_rank, (size_t)V * 4 + 4);
     LCHK(launch_vocab_compact(vd, cap, ctx->dense.as<uint32_t>(), c, ctx->vslot.as<uint32_t>(), ctx->skey0.as<uint4>(),
                               ctx->seq0.as<uint32_t>(), s));
-    uint32_t vm = 0;
-    LCHK(key_varying_bytes_u128(ctx->skey0.as<uint4>(), V, &vm, ar, s));
-    int cur = radix_sort_u128(ctx->skey0.as<uint4>(), ctx->seq0.as<uint32_t>(), ctx->skey1.as<uint4>(),
+    int cur;
+    if (V <= SORT_TILE_MAXN) { /* two launches, no varying-byte probe (no host sync) */
+        cur = tile_sort_u128(ctx->skey0.as<uint4>(), ctx->seq0.as<uint32_t>(), ctx->skey1.as<uint4>(),
+                             ctx->seq1.as<uint32_t>(), V, ar, s);
+    } else {
+        uint32_t vm = 0;
+        LCHK(key_varying_bytes_u128(ctx->skey0.as<uint4>(), V, &vm, ar, s));
+        cur = radix_sort_u128(ctx->skey0.as<uint4>(), ctx->seq0.as<uint32_t>(), ctx->skey1.as<uint4>(),
                               ctx->seq1.as<uint32_t>(), V, vm, ar, s);
+    }
     LCHK(cur);
     ctx->sorted_skey = cur ? ctx->skey1.as<uint4>() : ctx->skey0.as<uint4>();
     ctx->sorted_dense = cur ? ctx->seq1.as<uint32_t>() : ctx->seq0.as<uint32_t>();
@@ -475,8 +481,9 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     mark(ctx, S_DF);
     ENSURE(ctx->df_local, (size_t)V * 4 + 4);
     ENSURE(ctx->df_global, (size_t)V * 4 + 4);
-    LCHK(launch_df_hist(ctx->rec_slot.as<uint32_t>(), R_total, ctx->rank_of_slot.as<uint32_t>(), V,
-                        ctx->df_local.as<uint32_t>(), ar, s));
+    /* also rewrites every record's slot as its term rank (K5 then needs no rank gather) */
+    LCHK(launch_df_hist(ctx->rec_slot.as<uint32_t>(), R_total, ctx->rank_of_slot.as<uint32_t>(), V, cap,
+                        (uint32_t*)(cnt + 3), ctx->df_local.as<uint32_t>(), ar, s));
     mark(ctx, S_EXCHANGE);
     if (ctx->comm && ctx->nranks > 1) {
         int rc = exchange_df(ctx, V);
@@ -515,6 +522,7 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     LCHK(launch_doc_keys(dev_ids, N, ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), s));
     uint32_t dm = 0;
     dm = 0x1Fu; /* base-11 keys of 10 digits are < 11^10 < 2^35: five bytes, no probe */
+    /* five known digit bytes: the radix sort beats the tile sort's 49-tile rank search here */
     int dc = radix_sort_u64(ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), ctx->dkey1.as<uint64_t>(),
                             ctx->dseq1.as<uint32_t>(), N, dm, ar, s);
     LCHK(dc);

@@ -209,10 +209,14 @@ constexpr uint32_t DFH_RECS = 65535;      /* records per workgroup: u16 bins can
 constexpr uint32_t DFH_MAXV = 65536;
 
 /* LDS-privatised DF histogram: 1024 threads (16 waves, the 100 KB bin array allows one
- * workgroup per CU), four record gathers in flight per thread. */
+ * workgroup per CU).  Each thread owns 64 records of the workgroup's range and keeps
+ * DFH_B of them in flight at once (slot loads, then rank gathers, then LDS adds): the
+ * loop is latency-bound, so the number of dependent round trips is what matters. */
 constexpr int DFH_NT = 1024;
-__global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(const uint32_t* __restrict__ rec_slot, uint64_t nrec,
+constexpr int DFH_B = 16;
+__global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ rec_slot, uint64_t nrec,
                                                         const uint32_t* __restrict__ rank_of_slot, uint32_t V,
+                                                        uint64_t slot_cap, uint32_t* __restrict__ status,
                                                         uint32_t* __restrict__ part /* [grid][V/2 words] */) {
     extern __shared__ __attribute__((aligned(16))) uint32_t bins[]; /* V/2 words of two u16 counters */
     const uint32_t W = (V + 1) / 2;
@@ -220,38 +224,60 @@ __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(const uint32_t* __restri
     __syncthreads();
     const uint64_t r0 = (uint64_t)blockIdx.x * DFH_RECS;
     const uint64_t r1 = r0 + DFH_RECS < nrec ? r0 + DFH_RECS : nrec;
-    for (uint64_t i = r0 + threadIdx.x; i < r1; i += 4 * DFH_NT) {
-        uint32_t sl[4], r[4];
+    for (uint64_t i = r0 + threadIdx.x; i < r1; i += (uint64_t)DFH_B * DFH_NT) {
+        uint32_t sl[DFH_B], r[DFH_B];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < DFH_B; ++q) {
             const uint64_t k = i + (uint64_t)q * DFH_NT;
-            sl[q] = k < r1 ? rec_slot[k] : 0u;
+            sl[q] = k < r1 ? __builtin_nontemporal_load(&rec_slot[k]) : 0xFFFFFFFFu;
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) r[q] = rank_of_slot[sl[q]];
+        for (int q = 0; q < DFH_B; ++q) {
+            if (sl[q] != 0xFFFFFFFFu && sl[q] >= slot_cap) { atomicOr(status, ST_BOUNDS); sl[q] = 0xFFFFFFFFu; }
+            r[q] = sl[q] != 0xFFFFFFFFu ? rank_of_slot[sl[q]] : 0u;
+        }
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (i + (uint64_t)q * DFH_NT < r1) atomicAdd(&bins[r[q] >> 1], 1u << (16 * (r[q] & 1)));
+        for (int q = 0; q < DFH_B; ++q) {
+            if (sl[q] == 0xFFFFFFFFu) continue;
+            atomicAdd(&bins[r[q] >> 1], 1u << (16 * (r[q] & 1)));
+            /* records carry term ranks from here on: K5 reads them without a gather */
+            __builtin_nontemporal_store(r[q], &rec_slot[i + (uint64_t)q * DFH_NT]);
+        }
     }
     __syncthreads();
     uint32_t* out = part + (uint64_t)blockIdx.x * W;
     for (uint32_t k = threadIdx.x; k < W; k += DFH_NT) out[k] = bins[k];
 }
+/* df[r] += sum over DFC_G partial histograms (blockIdx.y picks the group): all of a
+ * thread's column loads are in flight at once, one atomic per (rank, group) */
+constexpr uint32_t DFC_G = 32;
 __global__ void k_df_colsum(const uint32_t* __restrict__ part, uint32_t nparts, uint32_t V, uint32_t* __restrict__ df) {
-    uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= V) return;
-    const uint32_t W = (V + 1) / 2;
-    uint32_t sum = 0, sh = 16 * (r & 1);
-    for (uint32_t p = 0; p < nparts; ++p) sum += (part[(uint64_t)p * W + (r >> 1)] >> sh) & 0xFFFFu;
-    df[r] = sum;
+    const uint32_t W = (V + 1) / 2, sh = 16 * (r & 1);
+    const uint32_t p0 = blockIdx.y * DFC_G;
+    uint32_t v[DFC_G];
+#pragma unroll
+    for (uint32_t q = 0; q < DFC_G; ++q)
+        v[q] = p0 + q < nparts ? part[(uint64_t)(p0 + q) * W + (r >> 1)] : 0u;
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < DFC_G; ++q) sum += (v[q] >> sh) & 0xFFFFu;
+    if (sum) atomicAdd(&df[r], sum);
 }
-__global__ void k_df_hist_atomic(const uint32_t* __restrict__ rec_slot, uint64_t nrec,
-                                 const uint32_t* __restrict__ rank_of_slot, uint32_t* __restrict__ df) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nrec; i += (uint64_t)gridDim.x * blockDim.x)
-        atomicAdd(&df[rank_of_slot[rec_slot[i]]], 1u);
+__global__ void k_df_hist_atomic(uint32_t* __restrict__ rec_slot, uint64_t nrec,
+                                 const uint32_t* __restrict__ rank_of_slot, uint64_t slot_cap,
+                                 uint32_t* __restrict__ status, uint32_t* __restrict__ df) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nrec; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t sl = rec_slot[i];
+        if (sl >= slot_cap) { atomicOr(status, ST_BOUNDS); continue; }
+        const uint32_t r = rank_of_slot[sl];
+        atomicAdd(&df[r], 1u);
+        rec_slot[i] = r;
+    }
 }
-int launch_df_hist(const uint32_t* rec_slot, uint64_t nrec, const uint32_t* rank_of_slot, uint32_t V, uint32_t* df,
-                   Arena& ar, hipStream_t s) {
+int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* rank_of_slot, uint32_t V, uint64_t slot_cap,
+                   uint32_t* status, uint32_t* df, Arena& ar, hipStream_t s) {
     if (V == 0) return 0;
     if (nrec == 0) return hipMemsetAsync(df, 0, (size_t)V * 4, s) == hipSuccess ? 0 : -1;
     if (V <= DFH_MAXV) {
@@ -260,13 +286,14 @@ int launch_df_hist(const uint32_t* rec_slot, uint64_t nrec, const uint32_t* rank
         size_t m = ar.mark();
         uint32_t* part = (uint32_t*)ar.get((size_t)nparts * W * 4);
         if (!part) return -2;
-        k_df_hist_lds<<<nparts, DFH_NT, (size_t)W * 4, s>>>(rec_slot, nrec, rank_of_slot, V, part);
-        k_df_colsum<<<grid_for(V), NT, 0, s>>>(part, nparts, V, df);
+        if (hipMemsetAsync(df, 0, (size_t)V * 4, s) != hipSuccess) return -1;
+        k_df_hist_lds<<<nparts, DFH_NT, (size_t)W * 4, s>>>(rec_slot, nrec, rank_of_slot, V, slot_cap, status, part);
+        k_df_colsum<<<dim3(grid_for(V), (nparts + DFC_G - 1) / DFC_G), NT, 0, s>>>(part, nparts, V, df);
         ar.release(m);
         return ok();
     }
     if (hipMemsetAsync(df, 0, (size_t)V * 4, s) != hipSuccess) return -1;
-    k_df_hist_atomic<<<2048, NT, 0, s>>>(rec_slot, nrec, rank_of_slot, df);
+    k_df_hist_atomic<<<2048, NT, 0, s>>>(rec_slot, nrec, rank_of_slot, slot_cap, status, df);
     return ok();
 }
 
@@ -344,6 +371,9 @@ constexpr uint32_t K5_SMALL = 64;     /* one wave, bitonic across the lanes */
 constexpr uint32_t K5_WAVE = 1024;    /* one wave, LDS radix sort of packed (rank, index) keys */
 constexpr uint32_t K5_IDX_BITS = 11;  /* index bits of a packed key (n <= 2048) */
 constexpr int K5_BATCH = 8;           /* gathers per lane in flight together */
+constexpr uint32_t K5_NB_BITS = 9;    /* bucket sort: 512 buckets by the rank's top bits */
+constexpr uint32_t K5_NB = 1u << K5_NB_BITS;
+constexpr uint32_t K5_GROUP_MAX = 48; /* larger buckets (skewed ranks): the radix path */
 
 /* idf of every term rank: one gather per pair in K5 instead of three dependent ones */
 __global__ void k_idf_of_rank(const uint32_t* __restrict__ df_of_rank, const uint32_t* __restrict__ idf_idx,
@@ -361,9 +391,10 @@ __device__ __forceinline__ void k5_emit(const K5Args& a, uint64_t o, double ds, 
     a.out_score[o] = tf * a.idf_rank[rank]; /* TFIDF.c:243-244 (idf from the host-libm LUT) */
 }
 
-__device__ __forceinline__ uint32_t k5_rank(const K5Args& a, uint32_t sl) {
-    if (sl >= a.slot_cap) { atomicOr(a.status, ST_BOUNDS); sl = 0; }
-    return a.rank_of_slot[sl];
+/* records hold term ranks once the DF pass has run (k_df_hist_* rewrite them in place) */
+__device__ __forceinline__ uint32_t k5_rank(const K5Args& a, uint32_t r) {
+    if (r >= a.nterms) { atomicOr(a.status, ST_BOUNDS); r = 0; }
+    return r;
 }
 
 /* which kernel sorts a document of n pairs */
@@ -372,71 +403,12 @@ __device__ __forceinline__ bool k5_by_wave(const K5Args& a, uint32_t n, bool pre
     return n <= K5_SMALL || (n <= K5_WAVE && a.rank_bits + K5_IDX_BITS <= 32);
 }
 
-/* One wave per document, four documents per workgroup, no block barriers:
- *   n <= 64      bitonic sort of (rank, count) across the lanes (__shfl_xor);
- *   n <= 1024    LSD radix sort by rank, 8-bit digits, of packed (rank << 11 | index) keys
- *                in a wave-private LDS ping-pong: a wave-private histogram, a DPP scan of the
- *                256 bins and a stable multisplit scatter (8 ballots) per round of 64 keys;
- *   presorted    merged runs (finalize's partial merge) are emitted as they are. */
-__global__ __launch_bounds__(NT) void k_score_wave(K5Args a) {
-    __shared__ uint32_t kb[NT / 64][2][K5_WAVE];
-    __shared__ uint32_t hist[NT / 64][256];
-    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t stride = gridDim.x * (NT / 64);
-    /* persistent waves: each wave walks output positions i, i + stride, ...; the next
-     * position's metadata word is loaded while the current document is sorted */
-    uint32_t i = blockIdx.x * (NT / 64) + w;
-    uint4 mnext = i < a.ndocs ? a.meta[i] : make_uint4(0, 0, 0, 0);
-    for (; i < a.ndocs; i += stride) {
-    const uint4 mc = mnext;
-    if (i + stride < a.ndocs) mnext = a.meta[i + stride];
-    const uint32_t n = mc.z & 0x3FFFFFFFu;
-    const bool presorted = ((mc.z >> 30) & DF_PRESORTED) != 0;
-    if (n == 0) continue;
-    if (!k5_by_wave(a, n, presorted)) { /* hand the document to k_score_large's list */
-        if (lane == 0) a.large_list[atomicAdd(a.large_count, 1u)] = i;
-        continue;
-    }
-    const uint64_t ob = a.out_off[i], rb = ((uint64_t)mc.y << 32) | mc.x;
-    if (rb + n > a.rec_total) { if (lane == 0) atomicOr(a.status, ST_BOUNDS); continue; }
-    const double ds = (double)mc.w;
-    if (presorted) {
-        for (uint32_t j = lane; j < n; j += 64) k5_emit(a, ob + j, ds, k5_rank(a, a.rec_slot[rb + j]), a.rec_cnt[rb + j]);
-        continue;
-    }
-    if (n <= K5_SMALL) {
-        uint32_t key = 0xFFFFFFFFu, val = 0;
-        if (lane < n) { key = k5_rank(a, a.rec_slot[rb + lane]); val = a.rec_cnt[rb + lane]; }
-#pragma unroll
-        for (uint32_t k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                uint32_t pk = __shfl_xor(key, j, 64), pv = __shfl_xor(val, j, 64);
-                bool take_min = ((lane & k) == 0) == ((lane & j) == 0);
-                if (take_min ? (pk < key) : (pk > key)) { key = pk; val = pv; }
-            }
-        }
-        if (lane < n) k5_emit(a, ob + lane, ds, key, val);
-        continue;
-    }
-    uint32_t* buf0 = kb[w][0];
-    uint32_t* buf1 = kb[w][1];
-    uint32_t* h = hist[w];
-    /* keys: every slot load of a batch in flight, then every rank gather */
-    for (uint32_t j0 = 0; j0 < n; j0 += 64 * K5_BATCH) {
-        uint32_t sl[K5_BATCH];
-#pragma unroll
-        for (int q = 0; q < K5_BATCH; ++q) {
-            const uint32_t j = j0 + 64 * q + lane;
-            sl[q] = j < n ? a.rec_slot[rb + j] : 0u;
-        }
-#pragma unroll
-        for (int q = 0; q < K5_BATCH; ++q) {
-            const uint32_t j = j0 + 64 * q + lane;
-            const uint32_t r = k5_rank(a, sl[q]);
-            if (j < n) buf0[j] = (r << K5_IDX_BITS) | j;
-        }
-    }
+/* Skewed documents (a bucket of the bucket sort above K5_GROUP_MAX keys): LSD radix sort
+ * by rank, 8-bit digits, of the packed keys in buf0 — a wave-private histogram, a DPP scan
+ * of the 256 bins and a stable multisplit scatter (8 ballots) per round of 64 keys. */
+__device__ __noinline__ void k5_radix(const K5Args& a, uint32_t* buf0, uint32_t* buf1, uint32_t* h, uint32_t n,
+                                      uint64_t rb, uint64_t ob, double ds) {
+    const uint32_t lane = threadIdx.x & 63;
     const uint64_t below = (1ull << lane) - 1ull;
     uint32_t cur = 0;
     for (uint32_t sh = K5_IDX_BITS; sh < K5_IDX_BITS + a.rank_bits; sh += 8) {
@@ -506,8 +478,211 @@ __global__ __launch_bounds__(NT) void k_score_wave(K5Args a) {
             }
         }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+/* One wave per document, four documents per workgroup, no block barriers.  The wave's
+ * next document is prefetched while the current one is sorted: its metadata two documents
+ * ahead, its output offset, and up to K5_PF x 64 (slot, count) records one document
+ * ahead, so a document costs two dependent global round trips (rank gathers, idf
+ * gathers) instead of five.
+ *   n <= 64      bitonic sort of (rank, count) across the lanes (__shfl_xor);
+ *   n <= 1024    bucket sort of packed (rank << 11 | index) keys by the rank's top 9 bits
+ *                (counts kept in LDS by index), k5_radix for skewed documents;
+ *   presorted    merged runs (finalize's partial merge) are emitted as they are. */
+constexpr int K5_PF = 8;                 /* records prefetched per lane: documents up to 512 pairs */
+constexpr int K5_RQ = K5_WAVE / 64;      /* rank registers per lane: documents up to K5_WAVE pairs */
+__device__ __forceinline__ void k5_prefetch(const K5Args& a, const uint4& m, uint32_t lane, uint32_t (&s)[K5_PF],
+                                            uint32_t (&c)[K5_PF]) {
+    const uint32_t n = m.z & 0x3FFFFFFFu;
+    const uint64_t rb = ((uint64_t)m.y << 32) | m.x;
+    const bool ok = n != 0u && n <= K5_WAVE && rb + n <= a.rec_total;
+#pragma unroll
+    for (int q = 0; q < K5_PF; ++q) {
+        const uint32_t j = 64u * q + lane;
+        const bool v = ok && j < n;
+        s[q] = v ? a.rec_slot[rb + j] : 0u;
+        c[q] = v ? a.rec_cnt[rb + j] : 0u;
+    }
+}
+
+__global__ __launch_bounds__(NT, 4) void k_score_wave(K5Args a) {
+    __shared__ uint32_t kb[NT / 64][2][K5_WAVE];
+    __shared__ uint32_t hist[NT / 64][K5_NB];
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t stride = gridDim.x * (NT / 64);
+    uint32_t* buf0 = kb[w][0];
+    uint32_t* buf1 = kb[w][1];
+    uint32_t* h = hist[w];
+    uint32_t i = blockIdx.x * (NT / 64) + w;
+    uint4 m_cur = i < a.ndocs ? a.meta[i] : make_uint4(0, 0, 0, 0);
+    uint4 m_nxt = i + stride < a.ndocs ? a.meta[i + stride] : make_uint4(0, 0, 0, 0);
+    uint64_t ob_cur = i < a.ndocs ? a.out_off[i] : 0ull;
+    uint32_t s_cur[K5_PF], c_cur[K5_PF];
+    k5_prefetch(a, m_cur, lane, s_cur, c_cur);
+    for (; i < a.ndocs; i += stride) {
+        const uint4 mc = m_cur;
+        const uint64_t ob = ob_cur;
+        const uint32_t n = mc.z & 0x3FFFFFFFu;
+        const bool presorted = ((mc.z >> 30) & DF_PRESORTED) != 0;
+        const uint64_t rb = ((uint64_t)mc.y << 32) | mc.x;
+        const double ds = (double)mc.w;
+        const bool small_doc = n != 0u && k5_by_wave(a, n, presorted) && rb + n <= a.rec_total;
+        /* this document's rank gathers first, then the next document's prefetch: the
+         * waits for the ranks leave the prefetch loads in flight */
+        uint32_t r[K5_RQ];
+#pragma unroll
+        for (int q = 0; q < K5_PF; ++q) {
+            const uint32_t j = 64u * q + lane;
+            r[q] = (small_doc && j < n) ? k5_rank(a, s_cur[q]) : 0xFFFFFFFFu;
+            if (small_doc && j < n) buf0[j] = c_cur[q]; /* counts by record index */
+        }
+        if (small_doc && n > 64u * K5_PF) { /* beyond the prefetch: loaded here */
+            uint32_t sx[K5_RQ - K5_PF];
+#pragma unroll
+            for (int q = K5_PF; q < K5_RQ; ++q) {
+                const uint32_t j = 64u * q + lane;
+                sx[q - K5_PF] = j < n ? a.rec_slot[rb + j] : 0u;
+                if (j < n) buf0[j] = a.rec_cnt[rb + j];
+            }
+#pragma unroll
+            for (int q = K5_PF; q < K5_RQ; ++q) {
+                const uint32_t j = 64u * q + lane;
+                r[q] = j < n ? k5_rank(a, sx[q - K5_PF]) : 0xFFFFFFFFu;
+            }
+        } else {
+#pragma unroll
+            for (int q = K5_PF; q < K5_RQ; ++q) r[q] = 0xFFFFFFFFu;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        {
+            const uint32_t inx = i + stride;
+            m_cur = m_nxt;
+            ob_cur = inx < a.ndocs ? a.out_off[inx] : 0ull;
+            m_nxt = inx + stride < a.ndocs ? a.meta[inx + stride] : make_uint4(0, 0, 0, 0);
+            k5_prefetch(a, m_cur, lane, s_cur, c_cur);
+        }
+        if (n == 0) continue;
+        if (!k5_by_wave(a, n, presorted)) { /* hand the document to k_score_large's list */
+            if (lane == 0) a.large_list[atomicAdd(a.large_count, 1u)] = i;
+            continue;
+        }
+        if (rb + n > a.rec_total) { if (lane == 0) atomicOr(a.status, ST_BOUNDS); continue; }
+        if (presorted) {
+#pragma unroll
+            for (int q = 0; q < K5_RQ; ++q) {
+                const uint32_t j = 64u * q + lane;
+                if (j < n) k5_emit(a, ob + j, ds, r[q], buf0[j]);
+            }
+            continue;
+        }
+        if (n <= K5_SMALL) {
+            uint32_t key = r[0], val = lane < n ? buf0[lane] : 0u;
+#pragma unroll
+            for (uint32_t k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                    uint32_t pk = __shfl_xor(key, j, 64), pv = __shfl_xor(val, j, 64);
+                    bool take_min = ((lane & k) == 0) == ((lane & j) == 0);
+                    if (take_min ? (pk < key) : (pk > key)) { key = pk; val = pv; }
+                }
+            }
+            if (lane < n) k5_emit(a, ob + lane, ds, key, val);
+            continue;
+        }
+        /* ---- bucket sort: ranks are distinct within a document, so an element's position
+         * is its bucket's start plus the number of smaller keys in its bucket.  Buckets by
+         * the rank's top K5_NB_BITS bits hold ~n/512 keys each. ---- */
+        const uint32_t hsh = a.rank_bits > K5_NB_BITS ? a.rank_bits - K5_NB_BITS : 0u;
+#pragma unroll
+        for (uint32_t q = 0; q < K5_NB / 64; ++q) h[q * 64 + lane] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int q = 0; q < K5_RQ; ++q)
+            if (64u * q + lane < n) atomicAdd(&h[r[q] >> hsh], 1u);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t gmax;
+        {
+            constexpr uint32_t PER = K5_NB / 64;
+            uint32_t v[PER], tot = 0, mx = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < PER; ++q) { v[q] = h[lane * PER + q]; tot += v[q]; mx = v[q] > mx ? v[q] : mx; }
+            uint32_t run = wave_incl_scan(tot) - tot;
+#pragma unroll
+            for (uint32_t q = 0; q < PER; ++q) { h[lane * PER + q] = run; run += v[q]; }
+            gmax = wave_max(mx);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (gmax > K5_GROUP_MAX) { /* skewed ranks: stable radix passes over buf0 */
+#pragma unroll
+            for (int q = 0; q < K5_RQ; ++q) {
+                const uint32_t j = 64u * q + lane;
+                if (j < n) buf0[j] = (r[q] << K5_IDX_BITS) | j;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            k5_radix(a, buf0, buf1, h, n, rb, ob, ds);
+            continue;
+        }
+#pragma unroll
+        for (int q = 0; q < K5_RQ; ++q) {
+            const uint32_t j = 64u * q + lane;
+            if (j < n) buf1[atomicAdd(&h[r[q] >> hsh], 1u)] = (r[q] << K5_IDX_BITS) | j;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        /* h[d] is now bucket d's end (= bucket d+1's start).  Every position is computed
+         * before any key moves (buf1 is read by the in-bucket counts), then the keys are
+         * placed in order and emitted with coalesced stores. */
+        uint32_t pk[K5_RQ], pp[K5_RQ];
+#pragma unroll
+        for (int q = 0; q < K5_RQ; ++q) {
+            const uint32_t j = 64u * q + lane;
+            pk[q] = 0u;
+            pp[q] = 0u;
+            if (j < n) {
+                const uint32_t k = buf1[j], d = (k >> K5_IDX_BITS) >> hsh;
+                const uint32_t gs = d ? h[d - 1] : 0u, ge = h[d];
+                uint32_t less = 0;
+                for (uint32_t f = gs; f < ge; ++f) less += buf1[f] < k ? 1u : 0u;
+                pk[q] = k;
+                pp[q] = gs + less;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int q = 0; q < K5_RQ; ++q)
+            if (64u * q + lane < n) buf1[pp[q]] = pk[q];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        constexpr int EB = 4;
+        for (uint32_t j0 = 0; j0 < n; j0 += 64 * EB) {
+            uint32_t key[EB], cnt[EB];
+            double idf[EB];
+#pragma unroll
+            for (int q = 0; q < EB; ++q) {
+                const uint32_t j = j0 + 64 * q + lane;
+                key[q] = j < n ? buf1[j] : 0u;
+                cnt[q] = j < n ? buf0[key[q] & ((1u << K5_IDX_BITS) - 1u)] : 0u;
+            }
+#pragma unroll
+            for (int q = 0; q < EB; ++q) idf[q] = a.idf_rank[key[q] >> K5_IDX_BITS];
+#pragma unroll
+            for (int q = 0; q < EB; ++q) {
+                const uint32_t j = j0 + 64 * q + lane;
+                if (j < n) {
+                    a.out_term[ob + j] = key[q] >> K5_IDX_BITS;
+                    a.out_cnt[ob + j] = cnt[q];
+                    a.out_score[ob + j] = ((double)cnt[q] / ds) * idf[q]; /* TFIDF.c:202,243-244 */
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }  /* persistent loop */
 }
 

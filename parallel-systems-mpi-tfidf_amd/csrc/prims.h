@@ -36,6 +36,15 @@ int radix_sort_u64(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, uint6
 int radix_sort_u128(uint4* k0, uint32_t* v0, uint4* k1, uint32_t* v1, uint64_t n,
                     uint32_t byte_mask, Arena& ar, hipStream_t s);
 
+/* Stable sort of (key, u32 value) pairs for n <= SORT_TILE_MAXN in two launches (tile
+ * bitonic sort + rank by binary search); same result as the radix sort over all bytes.
+ * The result is always in (k1, v1): returns 1, or <0 on error. */
+constexpr uint64_t SORT_TILE_MAXN = 64ull * 2048ull;
+int tile_sort_u64(const uint64_t* k0, const uint32_t* v0, uint64_t* k1, uint32_t* v1, uint64_t n, Arena& ar,
+                  hipStream_t s);
+int tile_sort_u128(const uint4* k0, const uint32_t* v0, uint4* k1, uint32_t* v1, uint64_t n, Arena& ar,
+                   hipStream_t s);
+
 /* Bitwise AND and OR over n keys of KB bytes -> varying-byte mask (synchronises). */
 int key_varying_bytes_u64(const uint64_t* k, uint64_t n, uint32_t* mask, Arena& ar, hipStream_t s);
 int key_varying_bytes_u128(const uint4* k, uint64_t n, uint32_t* mask, Arena& ar, hipStream_t s);

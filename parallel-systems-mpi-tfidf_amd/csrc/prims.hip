@@ -100,6 +100,7 @@ int scan_excl_t(const T* in, T* out, uint64_t n, Arena& ar, hipStream_t s) {
 constexpr int RS_NT = 256;
 constexpr int RS_IT = 8;
 constexpr int RS_TILE = RS_NT * RS_IT;
+constexpr uint32_t RS_FUSED_MAXNB = 1024; /* up to 2M keys: each scatter block reads nb histogram words per digit */
 
 __device__ __forceinline__ uint32_t digit_of(uint64_t k, int p) { return (uint32_t)(k >> (8 * p)) & 0xFFu; }
 __device__ __forceinline__ uint32_t digit_of(uint4 k, int p) {
@@ -123,7 +124,7 @@ __global__ __launch_bounds__(RS_NT) void k_rs_hist(const K* __restrict__ keys, u
     hist[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
 }
 
-template <typename K>
+template <typename K, bool FUSED>
 __global__ __launch_bounds__(RS_NT) void k_rs_scatter(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                      K* __restrict__ kout, uint32_t* __restrict__ vout,
                                                      uint64_t n, int p, const uint32_t* __restrict__ offs,
@@ -133,7 +134,29 @@ __global__ __launch_bounds__(RS_NT) void k_rs_scatter(const K* __restrict__ kin,
     __shared__ uint32_t wcnt[RS_NT / 64][256];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     run[tid] = 0;
-    boff[tid] = offs[(uint64_t)tid * nblocks + blockIdx.x];
+    if (FUSED) {
+        /* offs is the raw digit-major histogram: this block's base for digit tid is the
+         * count of smaller digits everywhere plus digit tid in earlier blocks */
+        const uint32_t* row = offs + (uint64_t)tid * nblocks;
+        uint32_t pre = 0, tot = 0;
+        uint32_t b = 0;
+        for (; b + 16 <= nblocks; b += 16) { /* 16 loads in flight per step */
+            uint32_t c[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) c[q] = row[b + q];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) { pre += b + q < blockIdx.x ? c[q] : 0u; tot += c[q]; }
+        }
+        for (; b < nblocks; ++b) {
+            const uint32_t c = row[b];
+            pre += b < blockIdx.x ? c : 0u;
+            tot += c;
+        }
+        uint32_t all;
+        boff[tid] = block_excl_scan<RS_NT>(tot, &wcnt[0][0], &all) + pre;
+    } else {
+        boff[tid] = offs[(uint64_t)tid * nblocks + blockIdx.x];
+    }
 #pragma unroll
     for (int q = 0; q < RS_NT / 64; ++q) wcnt[q][tid] = 0;
     __syncthreads();
@@ -188,13 +211,135 @@ int radix_sort_t(K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t n, uint32_t 
         K* ko = cur ? k0 : k1;
         uint32_t* vo = cur ? v0 : v1;
         k_rs_hist<K><<<nb, RS_NT, 0, s>>>(ki, n, p, hist, nb);
-        int rc = scan_excl_t<uint32_t>(hist, hist, (uint64_t)256 * nb, ar, s);
-        if (rc) return rc;
-        k_rs_scatter<K><<<nb, RS_NT, 0, s>>>(ki, vi, ko, vo, n, p, hist, nb);
+        if (nb <= RS_FUSED_MAXNB) { /* two launches per digit: the scatter scans the histogram itself */
+            k_rs_scatter<K, true><<<nb, RS_NT, 0, s>>>(ki, vi, ko, vo, n, p, hist, nb);
+        } else {
+            int rc = scan_excl_t<uint32_t>(hist, hist, (uint64_t)256 * nb, ar, s);
+            if (rc) return rc;
+            k_rs_scatter<K, false><<<nb, RS_NT, 0, s>>>(ki, vi, ko, vo, n, p, hist, nb);
+        }
         cur ^= 1;
     }
     ar.release(m);
     return hipGetLastError() == hipSuccess ? cur : -1;
+}
+
+/* ------------------------------------------------- small sorts (n <= SORT_TILE_MAXN) ----
+ * Two launches, no digit passes: (1) each 1024-thread block bitonic-sorts a tile of 2048
+ * (key, input index) pairs in LDS; (2) every element's output position is its index in
+ * its own tile plus, for every other tile, the number of that tile's elements ordered
+ * before it (a binary search) — its global rank, since (key, input index) pairs are
+ * distinct.  Ties on the key keep input order, so the result equals the stable LSD radix
+ * sort's.  Replaces 4-5 launches per 8-bit digit for the vocabulary, document-order and
+ * partial-record sorts, which are all a few 10^5 elements. */
+constexpr int TS_NT = 1024;
+constexpr uint32_t TS_T = 2048;
+
+__device__ __forceinline__ bool key_lt(uint64_t a, uint64_t b) { return a < b; }
+__device__ __forceinline__ bool key_eq(uint64_t a, uint64_t b) { return a == b; }
+__device__ __forceinline__ bool key_lt(uint4 a, uint4 b) {
+    if (a.w != b.w) return a.w < b.w;
+    if (a.z != b.z) return a.z < b.z;
+    if (a.y != b.y) return a.y < b.y;
+    return a.x < b.x;
+}
+__device__ __forceinline__ bool key_eq(uint4 a, uint4 b) { return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w; }
+__device__ __forceinline__ void key_max(uint64_t& k) { k = ~0ull; }
+__device__ __forceinline__ void key_max(uint4& k) { k = make_uint4(~0u, ~0u, ~0u, ~0u); }
+
+template <typename K>
+__global__ __launch_bounds__(TS_NT) void k_tile_sort(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                    uint64_t n, K* __restrict__ tk, uint32_t* __restrict__ tv,
+                                                    uint32_t* __restrict__ ti) {
+    __shared__ K sk[TS_T];
+    __shared__ uint32_t sv[TS_T], si[TS_T];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * TS_T;
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {
+        const uint32_t e = tid + h * TS_NT;
+        const uint64_t g = t0 + e;
+        if (g < n) { sk[e] = kin[g]; sv[e] = vin[g]; si[e] = (uint32_t)g; }
+        else { K m; key_max(m); sk[e] = m; sv[e] = 0u; si[e] = 0xFFFFFFFFu; }
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= TS_T; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            const uint32_t i = 2u * tid - (tid & (j - 1u)), l = i + j;
+            const bool asc = (i & k) == 0u;
+            const K a = sk[i], b = sk[l];
+            const uint32_t ia = si[i], ib = si[l];
+            const bool b_first = key_lt(b, a) || (key_eq(a, b) && ib < ia);
+            if (b_first == asc) {
+                sk[i] = b; sk[l] = a;
+                si[i] = ib; si[l] = ia;
+                const uint32_t x = sv[i]; sv[i] = sv[l]; sv[l] = x;
+            }
+            __syncthreads();
+        }
+    }
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {
+        const uint32_t e = tid + h * TS_NT;
+        const uint64_t g = t0 + e;
+        if (g < n) { tk[g] = sk[e]; tv[g] = sv[e]; ti[g] = si[e]; }
+    }
+}
+
+/* An element's rank: the searches over the other tiles advance in lockstep, TS_LB at a
+ * time, so a thread has TS_LB independent loads in flight per step instead of one
+ * dependent chain per tile. */
+constexpr uint32_t TS_LB = 8;
+template <typename K>
+__global__ __launch_bounds__(256) void k_tile_rank(const K* __restrict__ tk, const uint32_t* __restrict__ tv,
+                                                  const uint32_t* __restrict__ ti, uint64_t n, K* __restrict__ kout,
+                                                  uint32_t* __restrict__ vout) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n) return;
+    const uint32_t t = (uint32_t)(g / TS_T), nt = (uint32_t)((n + TS_T - 1) / TS_T);
+    const K key = tk[g];
+    const uint32_t idx = ti[g];
+    uint64_t pos = g - (uint64_t)t * TS_T;
+    for (uint32_t b0 = 0; b0 < nt; b0 += TS_LB) {
+        uint32_t lo[TS_LB], len[TS_LB];
+#pragma unroll
+        for (uint32_t q = 0; q < TS_LB; ++q) {
+            const uint32_t b = b0 + q;
+            const uint64_t st = (uint64_t)b * TS_T;
+            lo[q] = 0;
+            len[q] = (b < nt && b != t) ? (uint32_t)((n - st) < TS_T ? (n - st) : TS_T) : 0u;
+        }
+        for (uint32_t it = 0; it < 12; ++it) {  /* ceil(log2(TS_T + 1)) steps */
+#pragma unroll
+            for (uint32_t q = 0; q < TS_LB; ++q) {
+                if (len[q] == 0u) continue;
+                const uint32_t half = len[q] >> 1, mid = lo[q] + half;
+                const uint64_t e = (uint64_t)(b0 + q) * TS_T + mid;
+                const K m = tk[e];
+                const bool before = key_lt(m, key) || (key_eq(m, key) && ti[e] < idx);
+                if (before) { lo[q] = mid + 1u; len[q] -= half + 1u; }
+                else len[q] = half;
+            }
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < TS_LB; ++q) pos += lo[q];
+    }
+    kout[pos] = key;
+    vout[pos] = tv[g];
+}
+
+template <typename K>
+int tile_sort_t(const K* k0, const uint32_t* v0, K* k1, uint32_t* v1, uint64_t n, Arena& ar, hipStream_t s) {
+    const uint32_t nt = (uint32_t)((n + TS_T - 1) / TS_T);
+    size_t m = ar.mark();
+    K* tk = (K*)ar.get(n * sizeof(K));
+    uint32_t* tv = (uint32_t*)ar.get(n * 4);
+    uint32_t* ti = (uint32_t*)ar.get(n * 4);
+    if (!tk || !tv || !ti) return -2;
+    k_tile_sort<K><<<nt, TS_NT, 0, s>>>(k0, v0, n, tk, tv, ti);
+    k_tile_rank<K><<<(unsigned)((n + 255) / 256), 256, 0, s>>>(tk, tv, ti, n, k1, v1);
+    ar.release(m);
+    return hipGetLastError() == hipSuccess ? 1 : -1;
 }
 
 /* AND / OR of all keys (which bytes vary): wave reduce, then one LDS combine per block and
@@ -249,6 +394,26 @@ int scan_excl_u32(const uint32_t* in, uint32_t* out, uint64_t n, Arena& ar, hipS
 }
 int scan_excl_u64(const uint64_t* in, uint64_t* out, uint64_t n, Arena& ar, hipStream_t s) {
     return scan_excl_t<uint64_t>(in, out, n, ar, s);
+}
+int tile_sort_u64(const uint64_t* k0, const uint32_t* v0, uint64_t* k1, uint32_t* v1, uint64_t n, Arena& ar,
+                  hipStream_t s) {
+    if (n > SORT_TILE_MAXN) return -3;
+    if (n <= 1) {
+        if (n == 1 && (hipMemcpyAsync(k1, k0, 8, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+                       hipMemcpyAsync(v1, v0, 4, hipMemcpyDeviceToDevice, s) != hipSuccess)) return -1;
+        return 1;
+    }
+    return tile_sort_t<uint64_t>(k0, v0, k1, v1, n, ar, s);
+}
+int tile_sort_u128(const uint4* k0, const uint32_t* v0, uint4* k1, uint32_t* v1, uint64_t n, Arena& ar,
+                   hipStream_t s) {
+    if (n > SORT_TILE_MAXN) return -3;
+    if (n <= 1) {
+        if (n == 1 && (hipMemcpyAsync(k1, k0, 16, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+                       hipMemcpyAsync(v1, v0, 4, hipMemcpyDeviceToDevice, s) != hipSuccess)) return -1;
+        return 1;
+    }
+    return tile_sort_t<uint4>(k0, v0, k1, v1, n, ar, s);
 }
 int radix_sort_u64(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, uint64_t n, uint32_t byte_mask,
                    Arena& ar, hipStream_t s) {
