@@ -88,7 +88,10 @@ struct tfidf_ctx {
     /* stage buffers */
     DevBuf chunk_start, chunk_doc;
     DevBuf vkeys, vrep;
-    uint64_t vcap = 1ull << 16;
+    /* vocabulary table: K1 is measurably faster at low load (fewer displaced keys behind
+     * the two slots it loads per token): 1M slots (16 MB) to start, x4 past 12 % load */
+    uint64_t vcap = 1ull << 20;
+    uint32_t vload_pct = 12;
     DevBuf rec_slot, rec_cnt;
     uint64_t rec_cap = 0;
     DevBuf part_doc, part_slot, part_cnt;
@@ -183,6 +186,18 @@ int tfidf_open(int device, tfidf_ctx** out) {
     ctx->stamps_on = ks && ks[0] == '1';
     const char* ka = getenv("TFIDF_K1_ABLATE");
     ctx->ablate = ka ? (uint32_t)strtoul(ka, nullptr, 0) : 0u;
+    /* diagnostics: initial vocabulary capacity (power of two) and the load it may reach
+     * before the run is repeated with a larger table (TFIDF_VLOAD percent, default 50) */
+    const char* kv = getenv("TFIDF_VCAP");
+    if (kv) {
+        uint64_t c = strtoull(kv, nullptr, 0);
+        if (c >= 1024 && (c & (c - 1)) == 0) ctx->vcap = c;
+    }
+    const char* kl = getenv("TFIDF_VLOAD");
+    if (kl) {
+        uint32_t l = (uint32_t)strtoul(kl, nullptr, 0);
+        if (l >= 10 && l <= 90) ctx->vload_pct = l;
+    }
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     for (int i = 0; i <= S_NSTAGES; ++i) HIPCHK(hipEventCreate(&ctx->ev[i]));
     if (arena_reset(ctx, 64ull << 20) != 0) { delete ctx; return TFIDF_E_NOMEM; }
@@ -408,7 +423,7 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     HIPCHK(hipMemcpyAsync(&V, ctx->dense.as<uint32_t>() + cap, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     ctx->V = V;
-    if ((uint64_t)V * 2 > cap) { ctx->vcap *= 4; return 1; } /* keep probes short */
+    if ((uint64_t)V * 100 > cap * ctx->vload_pct) { ctx->vcap *= 4; return 1; } /* keep probes short */
     ENSURE(ctx->vslot, (size_t)V * 4 + 4);
     ENSURE(ctx->skey0, (size_t)V * 16 + 16);
     ENSURE(ctx->skey1, (size_t)V * 16 + 16);

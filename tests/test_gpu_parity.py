@@ -285,3 +285,18 @@ def test_big_docs_split_across_chunks(engine):
     big = b" ".join(words[i] for i in z)
     docs = [big, b"tail words here", big[:200000], b"", big[5:] + b"\n"]
     check_vs_oracle(engine, *docs_to_arrays(docs))
+
+
+@pytest.mark.parametrize("cap,load", [("1024", "50"), ("4096", "12")])
+def test_vocabulary_table_growth(monkeypatch, cap, load):
+    """A vocabulary table that starts too small: K1 flags the overflow (or the load check
+    fires) and the run repeats with a larger table — results unchanged."""
+    monkeypatch.setenv("TFIDF_VCAP", cap)
+    monkeypatch.setenv("TFIDF_VLOAD", load)
+    p = tfidf_configs.plan("c2", scale=0.002)
+    data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
+    with tfidf_abi.Engine(0) as e:
+        res = check_vs_oracle(e, data, off, p["doc_ids"], p["ndocs_total"])
+        info = e.info()
+    assert info["vocab_capacity"] > int(cap)
+    assert res["nterms"] * 100 <= info["vocab_capacity"] * int(load)
