@@ -66,7 +66,7 @@ struct K1Out {
     unsigned long long* stamps;  /* diagnostic build only: K1_NSTAMP phase cycle sums, WG count,
                                     then K1_NCOUNT event counters */
 };
-#define K1_NSTAMP 12
+#define K1_NSTAMP 17
 #define K1_NCOUNT 4   /* segments, flushes, tokens taking the full probe, probe iterations */
 #define K1_STAMP_WORDS (K1_NSTAMP + 1 + K1_NCOUNT)
 

@@ -238,7 +238,8 @@ __device__ __forceinline__ uint32_t wave_agg_add_rtn(uint32_t* ctr, uint32_t idx
 }
 
 /* Emits every table entry of the group as records and clears the table. */
-__device__ void vs_flush(VsShared& S, const K1Out& o, uint32_t gd0, uint32_t ng, uint64_t cs, uint64_t ce) {
+__device__ void vs_flush(VsShared& S, const K1Out& o, uint32_t gd0, uint32_t ng, uint64_t cs, uint64_t ce,
+                         Stamps& st) {
     /* opaque copy of the thread index: keeps the per-entry indices (j * NT + tid) from being
      * hoisted out of the chunk loop and spilled — reloading them from scratch in the
      * write-out loop waited on every outstanding record store (vmcnt(0)) per iteration */
@@ -247,6 +248,7 @@ __device__ void vs_flush(VsShared& S, const K1Out& o, uint32_t gd0, uint32_t ng,
     lds_barrier();   /* every wave's walk is done (the token lists alias dcnt/doff) */
     if (tid < GCAP) S.dcnt[tid] = 0;
     lds_barrier();
+    STAMP(st, 12);
     /* pass 1: entries into registers (lane-consecutive, conflict-free), per-document counts */
     unsigned long long e[EPT];
 #pragma unroll
@@ -255,6 +257,7 @@ __device__ void vs_flush(VsShared& S, const K1Out& o, uint32_t gd0, uint32_t ng,
         if (e[j]) wave_agg_add(&S.dcnt[0], (uint32_t)(e[j] >> (CNT_BITS + SLOT_BITS)));
     }
     lds_barrier();
+    STAMP(st, 13);
     /* per-document decision, one thread per document */
     uint32_t packed = 0;
     if ((uint32_t)tid < ng) {
@@ -286,6 +289,7 @@ __device__ void vs_flush(VsShared& S, const K1Out& o, uint32_t gd0, uint32_t ng,
         S.part_base = pb;
     }
     lds_barrier();
+    STAMP(st, 14);
     const unsigned long long rb = S.rec_base, pb = S.part_base;
     const bool rec_ok = rb + nrec <= o.rec_cap, part_ok = pb + npart <= o.part_cap;
     if ((uint32_t)tid < ng && S.dstate[tid] == 2) {
@@ -307,6 +311,7 @@ __device__ void vs_flush(VsShared& S, const K1Out& o, uint32_t gd0, uint32_t ng,
         }
     }
     lds_barrier();
+    STAMP(st, 15);
     /* coalesced write-out; each thread then clears exactly the entries it read */
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
@@ -325,6 +330,7 @@ __device__ void vs_flush(VsShared& S, const K1Out& o, uint32_t gd0, uint32_t ng,
         }
         S.T[i] = 0ull;
     }
+    STAMP(st, 16);
 }
 
 }  // namespace
@@ -397,21 +403,31 @@ __global__ __launch_bounds__(NT, K1_WAVES_PER_SIMD) void k_tokcount_vs(CorpusDev
         const uint32_t hl = tbl_hash(key) & (TB - 1);
         /* first LDS probe: a CAS claim, or a plain read in overflow mode */
         const bool over = S.over != 0;
-        uint32_t claims = 0;
-        if (key != ~0ull) {
-            const unsigned long long old = over ? S.T[hl] : atomicCAS(&S.T[hl], 0ull, (key << CNT_BITS) | 1ull);
-            const unsigned long long nx = S.T[(hl + 1) & (TB - 1)];
-#if K1_ABL & 128
-            claims = old == 0ull ? 1u : 0u;
-            (void)nx;
-#else
-            claims = tbl_count(S, o, key, hl, old, nx, over, gd0_cur);
-#endif
+        const bool valid = key != ~0ull;
+        unsigned long long old = 0ull, nx = 0ull;
+        if (valid) {
+            old = over ? S.T[hl] : atomicCAS(&S.T[hl], 0ull, (key << CNT_BITS) | 1ull);
+            nx = S.T[(hl + 1) & (TB - 1)];
         }
+        /* the common outcomes (claimed, or counted at the home slot) stay branch-light;
+         * collisions and overflow mode take tbl_count, entered once per wave if any lane
+         * needs it */
+        const bool hit = valid && old != 0ull && (old >> CNT_BITS) == key;
+        const bool claimed = valid && old == 0ull && !over;
+        if (hit) atomicAdd(&S.T[hl], 1ull);
+        uint32_t claims = claimed ? 1u : 0u;
+#if !(K1_ABL & 128)
+        const bool rest = valid && !hit && !claimed;
+        if (__ballot(rest) != 0ull) {
+            if (rest) claims = tbl_count(S, o, key, hl, old, nx, over, gd0_cur);
+        }
+#else
+        (void)nx;
+#endif
         STAMP(st, 9);
         if (K1_ABL & 64) return;
         /* claims -> overflow mode: one LDS add per wave and round */
-        const uint32_t wc = wave_sum(claims);
+        const uint32_t wc = (uint32_t)__popcll(__ballot(claims != 0u));
         if (wc && lane == 0) {
             const uint32_t f = atomicAdd(&S.fill, wc);
             if (f + wc >= FILL_LIMIT) S.over = 1;
@@ -595,7 +611,7 @@ __global__ __launch_bounds__(NT, K1_WAVES_PER_SIMD) void k_tokcount_vs(CorpusDev
 #endif
             STAMP(st, 1);
             /* group end is a document boundary (or the chunk end): emit everything */
-            vs_flush(S, o, gd0, ng, cs, ce);
+            vs_flush(S, o, gd0, ng, cs, ce, st);
             STAMP(st, 2);
             if ((uint32_t)tid < ng) {
                 const uint32_t n = S.dsz[tid];

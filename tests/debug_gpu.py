@@ -59,28 +59,28 @@ def rccl1():
 def stamps():
     """K1 phase breakdown (diagnostic build): TFIDF_LIB=stamps TFIDF_STAMPS=1"""
     import ctypes as C
-    names = ["group setup", "walk tail", "flush", "docsize write", "classify", "compact",
+    names = ["group setup", "barrier wait (walk imbalance)", "flush tail", "docsize write", "classify", "compact",
              "round: keys+loads", "round: compare+miss", "round: docsize", "round: LDS count",
-             "round: claims", "step loop top"]
-    names[1] = "barrier wait (walk imbalance)"
+             "round: claims", "step loop top", "flush: sync+zero", "flush: pass 1", "flush: decide+alloc",
+             "flush: staging", "flush: write-out"]
+    NS = len(names)
     p = tfidf_configs.plan("c2", scale=float(os.environ.get("SCALE", "1.0")))
     with tfidf_abi.Engine(0) as e:
         c = e.synth_device(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"], p["ndocs_total"])
         for _ in range(2):
             e.run_corpus(c)
         info = e.info()
-        buf = (C.c_uint64 * 17)()
+        buf = (C.c_uint64 * (NS + 5))()
         L = tfidf_abi.lib()
         L.tfidf_debug_k1_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
-        n = L.tfidf_debug_k1_stamps(e.h, buf, 17)
-        # the second run accumulated counters once (stamps are reset per run)
-        print("tokens", info["ntokens"], "counted", buf[13], "vocab first-probe misses", buf[14],
-              "-", buf[15], "lane token-loop iterations", buf[16])
+        n = L.tfidf_debug_k1_stamps(e.h, buf, NS + 5)
+        print("tokens", info["ntokens"], "counted", buf[NS + 1], "vocab first-probe misses", buf[NS + 2],
+              "-", buf[NS + 3], "lane token-loop iterations", buf[NS + 4])
     print("k1 ms", info["ms_tokcount"], "flags", info["flags"], "stamps", n)
-    wgs = buf[12]
-    tot = sum(buf[:12])
-    for k in range(12):
-        print("%-18s %12.0f cyc/WG  %5.1f%%" % (names[k], buf[k] / max(wgs, 1), 100.0 * buf[k] / max(tot, 1)))
+    wgs = buf[NS]
+    tot = sum(buf[:NS])
+    for k in range(NS):
+        print("%-30s %12.0f cyc/WG  %5.1f%%" % (names[k], buf[k] / max(wgs, 1), 100.0 * buf[k] / max(tot, 1)))
     print("WGs", wgs, "total cyc/WG", tot / max(wgs, 1))
 
 
