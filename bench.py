@@ -76,6 +76,7 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--cpu-sample-docs", type=int, default=12000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-emit", action="store_true", help="skip the (untimed) output-emission measurement")
     ap.add_argument("--vocab", type=int, default=0, help="diagnostics only: override the config's vocabulary size")
     args = ap.parse_args()
 
@@ -123,6 +124,21 @@ def main():
     info = eng.info()
     C_bytes, P_pairs, T_tok = info["nbytes"], info["npairs"], info["ntokens"]
 
+    # output emission, outside the timed region and not in `value`:
+    # GPU %.16f formatting of the last step's lines, then the pinned D2H + write path
+    emit = None
+    if not args.no_emit:
+        t1 = time.perf_counter()
+        n = eng.format_bytes()
+        t_fmt = time.perf_counter() - t1
+        t2 = time.perf_counter()
+        eng.write_output("/dev/null")
+        t_wr = time.perf_counter() - t2
+        emit = {"text_bytes": int(n), "format_ms": round(t_fmt * 1e3, 3),
+                "format_GBps": round(n / t_fmt / 1e9, 2) if t_fmt > 0 else None,
+                "d2h_write_devnull_ms": round(t_wr * 1e3, 3),
+                "note": "GPU formatting (wall, incl. the size sync) and pinned D2H to /dev/null; not in value"}
+
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -168,6 +184,7 @@ def main():
                          "traffic": traffic, "alg_bytes_per_launch": int(alg_bytes),
                          "k1_avg_ms": round(k1_avg_ms, 4)},
             "cpu_baseline": None,
+            "emit": emit,
         }
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_sample_docs)

@@ -140,7 +140,24 @@ int tfidf_debug_k1_stamps(tfidf_ctx* ctx, uint64_t* out, int n);
 
 /* ---------------------------------------------------------------- emission -- */
 
-/* Writes result lines "docN@word\t%.16f\n" (TFIDF.c:245,280-281) to `path`. */
+/* GPU emission (the default output path): formats the last run's lines
+ * "docN@word\t%.16f\n" (TFIDF.c:245,281) in output order into one text in HBM.  %.16f
+ * is computed exactly (integer significand x 10^16, 128-bit, ties to even: glibc
+ * printf's result).  The corpus of the run must still be valid (long terms' bytes are
+ * read from it).  *nbytes = the text's size. */
+int tfidf_format(tfidf_ctx* ctx, uint64_t* nbytes);
+/* Copies bytes [off, off + n) of the formatted text to host memory. */
+int tfidf_copy_text(tfidf_ctx* ctx, uint64_t off, void* dst, uint64_t n);
+/* tfidf_format + D2H through two pinned buffers + fwrite to `path` (TFIDF.c:274-282);
+ * append != 0 appends (a shard after the previous ones).  TFIDF_E_OUTPUT when the file
+ * cannot be opened or written. */
+int tfidf_write_output_gpu(tfidf_ctx* ctx, const char* path, int append);
+/* The device %.16f formatter on n host doubles: out = n 32-byte slots, NUL-padded.
+ * TFIDF_E_INVAL for values outside [0, 2^63/10^16) (scores are < 23). */
+int tfidf_format_f64(tfidf_ctx* ctx, const double* vals, uint64_t n, char* out);
+
+/* Host emission from a fetched result (glibc snprintf; kept for callers that already
+ * hold a tfidf_result): writes the same lines to `path`. */
 int tfidf_write_output(const tfidf_result* r, const char* path);
 /* Prints the debug TF Job / IDF Job blocks (TFIDF.c:199-205,236-239) to stdout,
  * one block pair for this shard, pairs in output order. */

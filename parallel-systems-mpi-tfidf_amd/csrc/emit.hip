@@ -1,0 +1,240 @@
+/*
+ * emit.hip — output emission on the GPU: the reference's
+ * "docN@word\t%.16f" lines (TFIDF.c:245) in output order (TFIDF.c:273), written as one
+ * contiguous text in HBM for output.txt (TFIDF.c:274-282).
+ *
+ *   %.16f        exact binary -> decimal: q = x * 10^16 rounded half-to-even from the
+ *                double's integer significand with 128-bit arithmetic (glibc printf's
+ *                result for every finite x >= 0 below 2^63 / 10^16; scores are
+ *                tf * log(N/df) <= log(2^32) < 23)
+ *   lines        one wave per document: its lines' lengths, a wave scan for their
+ *                offsets, then each lane writes its line
+ */
+#include "kernels.h"
+#include "dev_common.h"
+
+namespace {
+
+constexpr int NT = 256;
+inline unsigned grid_for(uint64_t n, int nt = NT) { return (unsigned)((n + nt - 1) / nt); }
+int ok() { return hipGetLastError() == hipSuccess ? 0 : -1; }
+
+constexpr uint64_t P16 = 10000000000000000ull;
+
+/* q = round-half-even(x * 10^16); false when x is negative, not finite or >= 2^63/10^16 */
+__device__ __forceinline__ bool fixed16(double x, uint64_t& q) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    if (b >> 63) return false;
+    const uint32_t ex = (uint32_t)(b >> 52) & 0x7FFu;
+    uint64_t m = b & ((1ull << 52) - 1ull);
+    if (ex == 0x7FFu) return false;
+    if (ex == 0u && m == 0ull) { q = 0; return true; }
+    int e;
+    if (ex == 0u) e = -1074;
+    else { m |= 1ull << 52; e = (int)ex - 1075; }
+    /* x = m * 2^e;  x * 10^16 = m * 10^16 * 2^e with m * 10^16 < 2^107 */
+    unsigned __int128 p = (unsigned __int128)m * P16;
+    if (e >= 0) {
+        if (e > 10) return false;
+        p <<= e;
+        if ((p >> 63) != 0) return false;
+        q = (uint64_t)p;
+        return true;
+    }
+    const int s = -e;
+    if (s >= 108) { q = 0; return true; } /* p < 2^107 <= 2^(s-1): below half */
+    const unsigned __int128 hi = p >> s;
+    if ((hi >> 63) != 0) return false;
+    uint64_t r = (uint64_t)hi;
+    const unsigned __int128 one = 1;
+    const unsigned __int128 rem = p & ((one << s) - one), half = one << (s - 1);
+    if (rem > half || (rem == half && (r & 1ull))) ++r;
+    q = r;
+    return true;
+}
+
+__device__ __forceinline__ uint32_t ndig(uint64_t v) {
+    uint32_t n = 1;
+    while (v >= 10ull) { v /= 10ull; ++n; }
+    return n;
+}
+
+/* writes v's n decimal digits ending before p + n */
+__device__ __forceinline__ void put_dec(uint8_t* p, uint64_t v, uint32_t n) {
+    for (uint32_t i = n; i-- > 0;) { p[i] = (uint8_t)('0' + (uint32_t)(v % 10ull)); v /= 10ull; }
+}
+
+/* "%.16f" of a fixed16 value: integer digits, '.', 16 fraction digits */
+__device__ __forceinline__ uint32_t score_len(uint64_t q) { return ndig(q / P16) + 17u; }
+__device__ __forceinline__ void put_score(uint8_t* p, uint64_t q) {
+    const uint64_t ip = q / P16, fr = q % P16;
+    const uint32_t ni = ndig(ip);
+    put_dec(p, ip, ni);
+    p[ni] = '.';
+    put_dec(p + ni + 1, fr / 100000000ull, 8);
+    put_dec(p + ni + 9, fr % 100000000ull, 8);
+}
+
+/* per term rank: its byte length and where its bytes are (short terms: the 16-byte key,
+ * bytes up to the TAB terminator; long terms: a corpus position from the vocabulary rep) */
+__global__ void k_term_meta(const uint4* __restrict__ vkeys, const uint64_t* __restrict__ vrep,
+                            const uint32_t* __restrict__ slot_of_rank, uint32_t V, uint4* __restrict__ tkey,
+                            uint32_t* __restrict__ tlen) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= V) return;
+    const uint32_t sl = slot_of_rank[r];
+    const uint4 k = vkeys[sl];
+    if ((k.w >> 24) == 0xFFu) { /* long term: 120-bit hash key, bytes in the corpus */
+        const uint64_t rep = vrep[sl];
+        tkey[r] = make_uint4((uint32_t)rep, (uint32_t)(rep >> 32), 0u, 0xFFFFFFFFu);
+        tlen[r] = (uint32_t)(rep >> 40);
+        return;
+    }
+    const uint32_t w[4] = {k.x, k.y, k.z, k.w};
+    uint32_t n = 16;
+    for (uint32_t i = 0; i < 16; ++i)
+        if (((w[i >> 2] >> (8 * (i & 3))) & 0xFFu) == 0x09u) { n = i; break; }
+    tkey[r] = k;
+    tlen[r] = n;
+}
+
+struct EmitArgs {
+    const uint32_t* order;     /* output position -> local document */
+    const uint32_t* doc_ids;   /* local document -> global id (NULL: index + 1) */
+    const uint64_t* out_off;   /* N + 1 pair offsets per output position */
+    const uint32_t* term;      /* per pair: term rank */
+    const double* score;       /* per pair */
+    const uint4* tkey;
+    const uint32_t* tlen;
+    const uint8_t* corpus;     /* long terms' bytes */
+    uint32_t ndocs;
+    uint64_t* doc_bytes;       /* pass 1: text bytes per output position */
+    const uint64_t* doc_text;  /* pass 2: text offset per output position */
+    uint8_t* text;
+    uint32_t* status;
+};
+
+__device__ __forceinline__ uint32_t doc_id_of(const EmitArgs& a, uint32_t i) {
+    const uint32_t d = a.order[i];
+    return a.doc_ids ? a.doc_ids[d] : d + 1u;
+}
+
+/* "doc" id '@' word '\t' score '\n' */
+__device__ __forceinline__ uint32_t line_len(const EmitArgs& a, uint32_t nid, uint64_t p, uint64_t& q) {
+    if (!fixed16(a.score[p], q)) { atomicOr(a.status, ST_BOUNDS); q = 0; }
+    return 3u + nid + 1u + a.tlen[a.term[p]] + 1u + score_len(q) + 1u;
+}
+
+__global__ __launch_bounds__(NT) void k_doc_text_bytes(EmitArgs a) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t stride = gridDim.x * (NT / 64);
+    for (uint32_t i = blockIdx.x * (NT / 64) + (threadIdx.x >> 6); i < a.ndocs; i += stride) {
+        const uint64_t p0 = a.out_off[i], p1 = a.out_off[i + 1];
+        const uint32_t nid = ndig(doc_id_of(a, i));
+        uint64_t sum = 0;
+        for (uint64_t p = p0 + lane; p < p1; p += 64) {
+            uint64_t q;
+            sum += line_len(a, nid, p, q);
+        }
+        /* wave sum of 64-bit values: two 32-bit halves (a document's text < 2^32 * 64) */
+        const uint32_t lo = wave_sum((uint32_t)sum & 0xFFFFFFu), hi = wave_sum((uint32_t)(sum >> 24));
+        if (lane == 0) a.doc_bytes[i] = (uint64_t)lo + ((uint64_t)hi << 24);
+    }
+}
+
+__global__ __launch_bounds__(NT) void k_doc_text_write(EmitArgs a) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t stride = gridDim.x * (NT / 64);
+    for (uint32_t i = blockIdx.x * (NT / 64) + (threadIdx.x >> 6); i < a.ndocs; i += stride) {
+        const uint64_t p0 = a.out_off[i], p1 = a.out_off[i + 1];
+        const uint32_t id = doc_id_of(a, i), nid = ndig(id);
+        uint64_t base = a.doc_text[i];
+        for (uint64_t r0 = p0; r0 < p1; r0 += 64) {
+            const uint64_t p = r0 + lane;
+            const bool v = p < p1;
+            uint64_t q = 0;
+            uint32_t len = 0, t = 0;
+            if (v) { t = a.term[p]; len = line_len(a, nid, p, q); }
+            const uint32_t incl = wave_incl_scan(len);
+            const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            if (v) {
+                uint8_t* o = a.text + base + (incl - len);
+                o[0] = 'd'; o[1] = 'o'; o[2] = 'c';
+                put_dec(o + 3, id, nid);
+                o += 3 + nid;
+                *o++ = '@';
+                const uint32_t wl = a.tlen[t];
+                const uint4 k = a.tkey[t];
+                if (k.w == 0xFFFFFFFFu) { /* long term (a short key always holds its TAB): corpus bytes */
+                    const uint8_t* src = a.corpus + ((((uint64_t)k.y << 32) | k.x) & 0xFFFFFFFFFFull);
+                    for (uint32_t j = 0; j < wl; ++j) o[j] = src[j];
+                } else {
+                    const uint32_t w[4] = {k.x, k.y, k.z, k.w};
+                    for (uint32_t j = 0; j < wl; ++j) o[j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+                }
+                o += wl;
+                *o++ = '\t';
+                put_score(o, q);
+                o += score_len(q);
+                *o = '\n';
+            }
+            base += tot;
+        }
+    }
+}
+
+/* tests / diagnostics: "%.16f" of n values into 32-byte NUL-padded slots */
+__global__ void k_format_f64(const double* __restrict__ v, uint64_t n, uint8_t* __restrict__ out,
+                             uint32_t* __restrict__ status) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint8_t* o = out + i * 32;
+    for (int j = 0; j < 32; ++j) o[j] = 0;
+    uint64_t q;
+    if (!fixed16(v[i], q)) { atomicOr(status, ST_BOUNDS); return; }
+    put_score(o, q);
+}
+
+}  // namespace
+
+int launch_term_meta(const uint4* vkeys, const uint64_t* vrep, const uint32_t* slot_of_rank, uint32_t V,
+                     uint4* tkey, uint32_t* tlen, hipStream_t s) {
+    if (!V) return 0;
+    k_term_meta<<<grid_for(V), NT, 0, s>>>(vkeys, vrep, slot_of_rank, V, tkey, tlen);
+    return ok();
+}
+
+static unsigned emit_grid(uint32_t ndocs) {
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+    }
+    const uint32_t need = (ndocs + NT / 64 - 1) / (NT / 64);
+    const uint32_t cap = (uint32_t)ncu * 8u;
+    return need < cap ? (need ? need : 1u) : cap;
+}
+
+int launch_emit_bytes(const EmitLaunch& e, uint64_t* doc_bytes, hipStream_t s) {
+    if (!e.ndocs) return 0;
+    EmitArgs a{e.order, e.doc_ids, e.out_off, e.term, e.score, e.tkey, e.tlen, e.corpus, e.ndocs,
+               doc_bytes, nullptr, nullptr, e.status};
+    k_doc_text_bytes<<<emit_grid(e.ndocs), NT, 0, s>>>(a);
+    return ok();
+}
+
+int launch_emit_write(const EmitLaunch& e, const uint64_t* doc_text, uint8_t* text, hipStream_t s) {
+    if (!e.ndocs) return 0;
+    EmitArgs a{e.order, e.doc_ids, e.out_off, e.term, e.score, e.tkey, e.tlen, e.corpus, e.ndocs,
+               nullptr, doc_text, text, e.status};
+    k_doc_text_write<<<emit_grid(e.ndocs), NT, 0, s>>>(a);
+    return ok();
+}
+
+int launch_format_f64(const double* v, uint64_t n, uint8_t* out, uint32_t* status, hipStream_t s) {
+    if (!n) return 0;
+    k_format_f64<<<grid_for(n), NT, 0, s>>>(v, n, out, status);
+    return ok();
+}

@@ -104,6 +104,10 @@ struct tfidf_ctx {
     DevBuf dkey0, dkey1, dseq0, dseq1, npairs_ord, out_off, doc_meta;
     DevBuf out_term, out_cnt, out_score, idf_rank, large_list;
     DevBuf x_mine, x_send, x_recv, x_recv2, x_seq0, x_seq1, x_head, x_grank, x_dfv, x_cnt;
+    /* output text (emit.hip) */
+    DevBuf t_key, t_len, doc_tbytes, doc_toff, text;
+    uint64_t text_bytes = 0;
+    bool text_valid = false;
     uint32_t* sorted_dense = nullptr; /* points into seq0/seq1 */
     uint4* sorted_skey = nullptr;
     const uint32_t* order = nullptr;
@@ -219,7 +223,8 @@ void tfidf_close(tfidf_ctx* ctx) {
                       &ctx->skey1, &ctx->seq0, &ctx->seq1, &ctx->rank_of_slot, &ctx->slot_of_rank, &ctx->pkey0,
                       &ctx->pkey1, &ctx->pseq0, &ctx->pseq1, &ctx->phead, &ctx->df_local, &ctx->df_global,
                       &ctx->present, &ctx->idf_vals, &ctx->dkey0, &ctx->dkey1, &ctx->dseq0, &ctx->dseq1,
-                      &ctx->npairs_ord, &ctx->out_off, &ctx->doc_meta, &ctx->out_term, &ctx->out_cnt,
+                      &ctx->npairs_ord, &ctx->out_off, &ctx->doc_meta, &ctx->t_key, &ctx->t_len, &ctx->doc_tbytes,
+                      &ctx->doc_toff, &ctx->text, &ctx->out_term, &ctx->out_cnt,
                       &ctx->out_score, &ctx->idf_rank, &ctx->large_list, &ctx->x_mine, &ctx->x_send, &ctx->x_recv,
                       &ctx->x_recv2, &ctx->x_seq0, &ctx->x_seq1, &ctx->x_head, &ctx->x_grank, &ctx->x_dfv,
                       &ctx->x_cnt, &ctx->stamps};
@@ -640,6 +645,7 @@ extern "C" int tfidf_run(tfidf_ctx* ctx, const tfidf_corpus* in) {
     const uint64_t Nt = in->ndocs_total ? in->ndocs_total : N;
     if (Nt < N || Nt > 0xFFFFFFFFull) return TFIDF_E_INVAL;
     ctx->have_result = false;
+    ctx->text_valid = false;
     int rc = 1;
     for (int attempt = 0; attempt < 8 && rc == 1; ++attempt) {
         size_t need = ctx->arena.peak > ctx->arena_buf.cap ? ctx->arena.peak * 2 : ctx->arena_buf.cap;
@@ -874,4 +880,131 @@ extern "C" int tfidf_synth_device(tfidf_ctx* ctx, uint64_t seed, uint32_t V, uin
     out->flags = TFIDF_CORPUS_DEVICE;
     out->ndocs_total = ndocs_total ? ndocs_total : ndocs;
     return TFIDF_OK;
+}
+
+/* ------------------------------------------------------------ emission (GPU) ----
+ * the "docN@word\t%.16f\n" lines (TFIDF.c:245,281) formatted in HBM
+ * by emit.hip (exact round-half-even %.16f), then copied out / written to output.txt
+ * (TFIDF.c:274-282). */
+extern "C" int tfidf_format(tfidf_ctx* ctx, uint64_t* nbytes) {
+    if (!ctx || !nbytes) return TFIDF_E_INVAL;
+    if (!ctx->have_result) return TFIDF_E_STATE;
+    if (ctx->text_valid) { *nbytes = ctx->text_bytes; return TFIDF_OK; }
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const uint32_t N = ctx->ndocs, V = ctx->V;
+    unsigned long long* cnt = ctx->counters.as<unsigned long long>();
+    uint32_t* status = (uint32_t*)(cnt + 3);
+    HIPCHK(hipMemsetAsync(status, 0, 4, s));
+    ENSURE(ctx->t_key, (size_t)V * 16 + 16);
+    ENSURE(ctx->t_len, (size_t)V * 4 + 4);
+    ENSURE(ctx->doc_tbytes, ((size_t)N + 1) * 8);
+    ENSURE(ctx->doc_toff, ((size_t)N + 1) * 8);
+    if (launch_term_meta(ctx->vkeys.as<uint4>(), ctx->vrep.as<uint64_t>(), ctx->slot_of_rank.as<uint32_t>(), V,
+                         ctx->t_key.as<uint4>(), ctx->t_len.as<uint32_t>(), s))
+        return TFIDF_E_HIP;
+    EmitLaunch e{ctx->order, ctx->dev_ids, ctx->out_off.as<uint64_t>(), ctx->out_term.as<uint32_t>(),
+                 ctx->out_score.as<double>(), ctx->t_key.as<uint4>(), ctx->t_len.as<uint32_t>(), ctx->dev_bytes, N,
+                 status};
+    uint64_t total = 0;
+    if (N) {
+        if (launch_emit_bytes(e, ctx->doc_tbytes.as<uint64_t>(), s)) return TFIDF_E_HIP;
+        ctx->arena.used = 0;
+        if (scan_excl_u64(ctx->doc_tbytes.as<uint64_t>(), ctx->doc_toff.as<uint64_t>(), N, ctx->arena, s))
+            return TFIDF_E_HIP;
+        HIPCHK(hipMemcpyAsync(&total, ctx->doc_toff.as<uint64_t>() + N, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    ENSURE(ctx->text, total + 64);
+    if (total && launch_emit_write(e, ctx->doc_toff.as<uint64_t>(), ctx->text.as<uint8_t>(), s)) return TFIDF_E_HIP;
+    uint32_t st = 0;
+    HIPCHK(hipMemcpyAsync(&st, status, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (st & ST_BOUNDS) {
+        fprintf(stderr, "tfidf: score outside the %%.16f formatter's range\n");
+        return TFIDF_E_STATE;
+    }
+    ctx->text_bytes = total;
+    ctx->text_valid = true;
+    *nbytes = total;
+    return TFIDF_OK;
+}
+
+extern "C" int tfidf_copy_text(tfidf_ctx* ctx, uint64_t off, void* dst, uint64_t n) {
+    if (!ctx || (n && !dst)) return TFIDF_E_INVAL;
+    if (!ctx->text_valid) return TFIDF_E_STATE;
+    if (off > ctx->text_bytes || n > ctx->text_bytes - off) return TFIDF_E_INVAL;
+    if (!n) return TFIDF_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipMemcpy(dst, ctx->text.as<uint8_t>() + off, n, hipMemcpyDeviceToHost));
+    return TFIDF_OK;
+}
+
+extern "C" int tfidf_write_output_gpu(tfidf_ctx* ctx, const char* path, int append) {
+    if (!ctx || !path) return TFIDF_E_INVAL;
+    uint64_t total = 0;
+    int rc = tfidf_format(ctx, &total);
+    if (rc) return rc;
+    FILE* f = fopen(path, append ? "ab" : "wb");
+    if (!f) return TFIDF_E_OUTPUT;
+    /* two pinned staging buffers: the copy of block k+1 overlaps the write of block k */
+    const uint64_t B = 64ull << 20;
+    uint8_t* hb[2] = {nullptr, nullptr};
+    hipEvent_t ev[2];
+    bool ok = true;
+    for (int i = 0; i < 2; ++i) {
+        if (hipHostMalloc((void**)&hb[i], B, hipHostMallocDefault) != hipSuccess) ok = false;
+        if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) ok = false;
+    }
+    hipStream_t s = ctx->stream;
+    const uint8_t* src = ctx->text.as<uint8_t>();
+    uint64_t nblk = (total + B - 1) / B;
+    for (uint64_t k = 0; ok && k < nblk && k < 2; ++k) {
+        const uint64_t n = (k + 1) * B <= total ? B : total - k * B;
+        if (hipMemcpyAsync(hb[k & 1], src + k * B, n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipEventRecord(ev[k & 1], s) != hipSuccess) ok = false;
+    }
+    for (uint64_t k = 0; ok && k < nblk; ++k) {
+        const uint64_t n = (k + 1) * B <= total ? B : total - k * B;
+        if (hipEventSynchronize(ev[k & 1]) != hipSuccess) { ok = false; break; }
+        if (fwrite(hb[k & 1], 1, n, f) != n) { rc = TFIDF_E_OUTPUT; ok = false; break; }
+        const uint64_t k2 = k + 2;
+        if (k2 < nblk) {
+            const uint64_t n2 = (k2 + 1) * B <= total ? B : total - k2 * B;
+            if (hipMemcpyAsync(hb[k2 & 1], src + k2 * B, n2, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipEventRecord(ev[k2 & 1], s) != hipSuccess) ok = false;
+        }
+    }
+    (void)hipStreamSynchronize(s);
+    for (int i = 0; i < 2; ++i) {
+        if (hb[i]) (void)hipHostFree(hb[i]);
+        (void)hipEventDestroy(ev[i]);
+    }
+    if (fclose(f) != 0 && !rc) rc = TFIDF_E_OUTPUT;
+    if (!ok && !rc) rc = TFIDF_E_HIP;
+    return rc;
+}
+
+extern "C" int tfidf_format_f64(tfidf_ctx* ctx, const double* vals, uint64_t n, char* out) {
+    if (!ctx || (n && (!vals || !out))) return TFIDF_E_INVAL;
+    if (!n) return TFIDF_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    DevBuf v, o;
+    if (v.ensure(n * 8) || o.ensure(n * 32)) { v.release(); o.release(); return TFIDF_E_NOMEM; }
+    unsigned long long* cnt = ctx->counters.as<unsigned long long>();
+    uint32_t* status = (uint32_t*)(cnt + 3);
+    uint32_t st = 0;
+    int rc = TFIDF_OK;
+    if (hipMemsetAsync(status, 0, 4, s) != hipSuccess ||
+        hipMemcpyAsync(v.p, vals, n * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+        launch_format_f64(v.as<double>(), n, o.as<uint8_t>(), status, s) ||
+        hipMemcpyAsync(out, o.p, n * 32, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(&st, status, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        rc = TFIDF_E_HIP;
+    v.release();
+    o.release();
+    if (!rc && (st & ST_BOUNDS)) rc = TFIDF_E_INVAL;
+    return rc;
 }

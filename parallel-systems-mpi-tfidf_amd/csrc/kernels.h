@@ -162,4 +162,23 @@ int launch_synth_fill(const void* spec, const uint32_t* doc_ids, const uint64_t*
                       uint64_t nblocks, uint32_t ndocs, const uint64_t* blk_off, uint8_t* bytes, uint64_t* doc_off,
                       hipStream_t s);
 
+/* ---- output emission (emit.hip) ---- */
+struct EmitLaunch {
+    const uint32_t* order;
+    const uint32_t* doc_ids;
+    const uint64_t* out_off;
+    const uint32_t* term;
+    const double* score;
+    const uint4* tkey;
+    const uint32_t* tlen;
+    const uint8_t* corpus;
+    uint32_t ndocs;
+    uint32_t* status;
+};
+int launch_term_meta(const uint4* vkeys, const uint64_t* vrep, const uint32_t* slot_of_rank, uint32_t V,
+                     uint4* tkey, uint32_t* tlen, hipStream_t s);
+int launch_emit_bytes(const EmitLaunch& e, uint64_t* doc_bytes, hipStream_t s);
+int launch_emit_write(const EmitLaunch& e, const uint64_t* doc_text, uint8_t* text, hipStream_t s);
+int launch_format_f64(const double* v, uint64_t n, uint8_t* out, uint32_t* status, hipStream_t s);
+
 #endif

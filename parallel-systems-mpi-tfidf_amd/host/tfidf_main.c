@@ -52,13 +52,18 @@ int main(int argc, char** argv) {
     c.ndocs = ndocs;
     c.ndocs_total = ndocs;
     rc = tfidf_run(ctx, &c);
-    tfidf_result r;
-    if (!rc) rc = tfidf_fetch(ctx, &r);
     if (rc) { fprintf(stderr, "tfidf: %s\n", tfidf_strerror(rc)); tfidf_close(ctx); return 3; }
-    if (debug) tfidf_print_jobs(&r);
-    rc = tfidf_write_output(&r, outpath);
+    if (debug) {
+        tfidf_result r;
+        rc = tfidf_fetch(ctx, &r);
+        if (rc) { fprintf(stderr, "tfidf: %s\n", tfidf_strerror(rc)); tfidf_close(ctx); return 3; }
+        tfidf_print_jobs(&r);
+        tfidf_result_free(&r);
+    }
+    /* lines formatted on the GPU, copied out through pinned buffers (TFIDF.c:245,274-282) */
+    rc = tfidf_write_output_gpu(ctx, outpath, 0);
     if (rc == TFIDF_E_OUTPUT) printf("Error Opening File: %s\n", outpath);
-    tfidf_result_free(&r);
+    else if (rc) { fprintf(stderr, "tfidf: %s\n", tfidf_strerror(rc)); tfidf_close(ctx); return 3; }
     tfidf_close(ctx);
     tfidf_free(bytes);
     tfidf_free(doc_off);

@@ -27,6 +27,7 @@ EXPORTS = [
     "tfidf_comm_init", "tfidf_run", "tfidf_fetch", "tfidf_result_free", "tfidf_last_run_info",
     "tfidf_stage_name", "tfidf_set_timing", "tfidf_write_output", "tfidf_print_jobs",
     "tfidf_ingest_dir", "tfidf_free", "tfidf_synth_host", "tfidf_synth_device",
+    "tfidf_format", "tfidf_copy_text", "tfidf_write_output_gpu", "tfidf_format_f64",
 ]
 
 
@@ -81,6 +82,10 @@ def lib() -> C.CDLL:
         L.tfidf_comm_unique_id.argtypes = [C.c_void_p]
         L.tfidf_comm_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
         L.tfidf_write_output.argtypes = [C.POINTER(Result), C.c_char_p]
+        L.tfidf_format.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+        L.tfidf_copy_text.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64]
+        L.tfidf_write_output_gpu.argtypes = [C.c_void_p, C.c_char_p, C.c_int]
+        L.tfidf_format_f64.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
         L.tfidf_synth_host.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.c_uint32, C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p]
         L.tfidf_synth_device.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p,
@@ -179,6 +184,31 @@ class Engine:
         d = {k: getattr(r, k) for k, _ in RunInfo._fields_ if k != "ms_stage"}
         d["stages"] = {lib().tfidf_stage_name(i).decode(): r.ms_stage[i] for i in range(r.nstages)}
         return d
+
+    def format_bytes(self) -> int:
+        """Formats the last run's lines on the GPU; returns the text size."""
+        n = C.c_uint64(0)
+        _chk(lib().tfidf_format(self.h, C.byref(n)), "tfidf_format")
+        return int(n.value)
+
+    def text(self) -> bytes:
+        """output.txt bytes formatted on the GPU (tfidf_format + tfidf_copy_text)."""
+        n = C.c_uint64(0)
+        _chk(lib().tfidf_format(self.h, C.byref(n)), "tfidf_format")
+        buf = np.empty(int(n.value), dtype=np.uint8)
+        if n.value:
+            _chk(lib().tfidf_copy_text(self.h, 0, buf.ctypes.data, n.value), "tfidf_copy_text")
+        return buf.tobytes()
+
+    def write_output(self, path: str, append: bool = False):
+        _chk(lib().tfidf_write_output_gpu(self.h, path.encode(), 1 if append else 0), "tfidf_write_output_gpu")
+
+    def format_f64(self, vals) -> list:
+        """The device %.16f formatter on host doubles (tests)."""
+        v = np.ascontiguousarray(vals, dtype=np.float64)
+        out = np.zeros(v.size * 32, dtype=np.uint8)
+        _chk(lib().tfidf_format_f64(self.h, v.ctypes.data, v.size, out.ctypes.data), "tfidf_format_f64")
+        return [bytes(out[i * 32:(i + 1) * 32]).rstrip(b"\0") for i in range(v.size)]
 
     def fetch(self) -> dict:
         r = Result()

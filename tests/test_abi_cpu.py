@@ -18,7 +18,7 @@ def declared_functions():
     with open(os.path.join(REPO, "include", "tfidf.h")) as f:
         src = f.read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(tfidf_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(tfidf_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_library_exports_every_declared_symbol():

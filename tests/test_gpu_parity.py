@@ -26,6 +26,8 @@ def check_vs_oracle(engine, data, off, ids=None, n_total=0):
     ora = oracle_py.run(data, off, ids, n_total)
     assert_same_result(res, ora)
     assert res["output_txt"] == ora["output_txt"]
+    # the GPU-formatted text (emit.hip) is the same bytes
+    assert engine.text() == ora["output_txt"]
     return res
 
 
@@ -300,3 +302,48 @@ def test_vocabulary_table_growth(monkeypatch, cap, load):
         info = e.info()
     assert info["vocab_capacity"] > int(cap)
     assert res["nterms"] * 100 <= info["vocab_capacity"] * int(load)
+
+
+def _py_fixed16(vals):
+    return [b"%.16f" % v for v in vals]
+
+
+def test_gpu_format_f64_matches_printf(engine):
+    """Device %.16f against Python's (correctly rounded, ties to even = glibc printf):
+    exact ties k/2^17, powers of two, tiny and subnormal values, values just
+    around the 17th-decimal rounding boundary, and a random sweep over score ranges."""
+    rng = np.random.default_rng(11)
+    vals = [0.0, 1.0, 0.5, 22.999999999999996, 10.0, 9.999999999999998, 5e-324, 2.2250738585072014e-308,
+            1e-17, 5e-17, 4.9999999999999996e-17, 1.5e-16, 0.1, 0.2, 0.3, 1 / 3, 2 / 3]
+    vals += [k / 2 ** 17 for k in range(1, 200)]
+    vals += [k / 2 ** 20 for k in range(1, 64)]
+    vals += [2.0 ** -e for e in range(0, 80)]
+    vals += [(k + 0.5) * 1e-16 for k in range(0, 50)]
+    vals += list(rng.random(20000) * 23.0)
+    vals += list(np.exp(rng.uniform(np.log(1e-12), np.log(23.0), 20000)))
+    got = engine.format_f64(vals)
+    want = _py_fixed16(vals)
+    bad = [(v, g, w) for v, g, w in zip(vals, got, want) if g != w]
+    assert not bad, bad[:5]
+
+
+def test_gpu_output_file_matches_golden(engine, tmp_path):
+    """tfidf_write_output_gpu (pinned double-buffered D2H + fwrite) writes the golden
+    output.txt bytes; append mode concatenates."""
+    for case in golden_cases()[:3]:
+        g = load_golden(case)
+        engine.run_host(g["data"], g["off"])
+        path = str(tmp_path / (case + ".txt"))
+        engine.write_output(path)
+        assert open(path, "rb").read() == g["output"]
+        engine.write_output(path, append=True)
+        assert open(path, "rb").read() == g["output"] * 2
+
+
+def test_gpu_text_c2_slice_vs_oracle(engine):
+    """A c2 slice through the whole path: GPU text == oracle output.txt."""
+    p = tfidf_configs.plan("c2", scale=0.004)
+    data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
+    engine.run_host(data, off, p["doc_ids"], p["ndocs_total"])
+    ora = oracle_py.run(data, off, p["doc_ids"], p["ndocs_total"])
+    assert engine.text() == ora["output_txt"]
