@@ -98,7 +98,7 @@ struct tfidf_ctx {
     uint64_t part_cap = 0;
     DevBuf doc_recoff, doc_npairs, doc_size, doc_flags;
     DevBuf counters;
-    DevBuf dense, vslot, skey0, skey1, seq0, seq1, rank_of_slot, slot_of_rank;
+    DevBuf dense, vslot, skey0, skey1, seq0, seq1, rank_of_slot, slot_of_rank, rank16;
     DevBuf pkey0, pkey1, pseq0, pseq1, phead;
     DevBuf df_local, df_global, present, idf_vals;
     DevBuf dkey0, dkey1, dseq0, dseq1, npairs_ord, out_off, doc_meta;
@@ -220,7 +220,7 @@ void tfidf_close(tfidf_ctx* ctx) {
                       &ctx->chunk_start, &ctx->chunk_doc, &ctx->vkeys, &ctx->vrep, &ctx->rec_slot, &ctx->rec_cnt,
                       &ctx->part_doc, &ctx->part_slot, &ctx->part_cnt, &ctx->doc_recoff, &ctx->doc_npairs,
                       &ctx->doc_size, &ctx->doc_flags, &ctx->counters, &ctx->dense, &ctx->vslot, &ctx->skey0,
-                      &ctx->skey1, &ctx->seq0, &ctx->seq1, &ctx->rank_of_slot, &ctx->slot_of_rank, &ctx->pkey0,
+                      &ctx->skey1, &ctx->seq0, &ctx->seq1, &ctx->rank_of_slot, &ctx->slot_of_rank, &ctx->rank16, &ctx->pkey0,
                       &ctx->pkey1, &ctx->pseq0, &ctx->pseq1, &ctx->phead, &ctx->df_local, &ctx->df_global,
                       &ctx->present, &ctx->idf_vals, &ctx->dkey0, &ctx->dkey1, &ctx->dseq0, &ctx->dseq1,
                       &ctx->npairs_ord, &ctx->out_off, &ctx->doc_meta, &ctx->t_key, &ctx->t_len, &ctx->doc_tbytes,
@@ -452,8 +452,10 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     ctx->sorted_skey = cur ? ctx->skey1.as<uint4>() : ctx->skey0.as<uint4>();
     ctx->sorted_dense = cur ? ctx->seq1.as<uint32_t>() : ctx->seq0.as<uint32_t>();
     LCHK(launch_vocab_long_fixup(ctx->sorted_skey, ctx->sorted_dense, ctx->vslot.as<uint32_t>(), vd, c, V, s));
+    uint16_t* r16 = nullptr;
+    if (V <= 65536u) { ENSURE(ctx->rank16, cap * 2); r16 = ctx->rank16.as<uint16_t>(); }
     LCHK(launch_vocab_rank(ctx->sorted_dense, ctx->vslot.as<uint32_t>(), V, ctx->rank_of_slot.as<uint32_t>(),
-                           ctx->slot_of_rank.as<uint32_t>(), s));
+                           ctx->slot_of_rank.as<uint32_t>(), r16, s));
     /* ---- partial documents ---- */
     mark(ctx, S_MERGE);
     uint64_t R_total = R_main;
@@ -502,7 +504,8 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     ENSURE(ctx->df_local, (size_t)V * 4 + 4);
     ENSURE(ctx->df_global, (size_t)V * 4 + 4);
     /* also rewrites every record's slot as its term rank (K5 then needs no rank gather) */
-    LCHK(launch_df_hist(ctx->rec_slot.as<uint32_t>(), R_total, ctx->rank_of_slot.as<uint32_t>(), V, cap,
+    LCHK(launch_df_hist(ctx->rec_slot.as<uint32_t>(), R_total, ctx->rank_of_slot.as<uint32_t>(),
+                        V <= 65536u ? ctx->rank16.as<uint16_t>() : nullptr, V, cap,
                         (uint32_t*)(cnt + 3), ctx->df_local.as<uint32_t>(), ar, s));
     mark(ctx, S_EXCHANGE);
     if (ctx->comm && ctx->nranks > 1) {

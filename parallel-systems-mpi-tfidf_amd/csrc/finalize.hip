@@ -79,16 +79,18 @@ int launch_vocab_compact(const VocabDev& v, uint64_t cap, const uint32_t* dense_
 }
 
 __global__ void k_vocab_rank(const uint32_t* __restrict__ sorted_dense, const uint32_t* __restrict__ vslot, uint32_t V,
-                             uint32_t* __restrict__ rank_of_slot, uint32_t* __restrict__ slot_of_rank) {
+                             uint32_t* __restrict__ rank_of_slot, uint32_t* __restrict__ slot_of_rank,
+                             uint16_t* __restrict__ rank16) {
     uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= V) return;
     uint32_t s = vslot[sorted_dense[r]];
     rank_of_slot[s] = r;
     slot_of_rank[r] = s;
+    if (rank16) rank16[s] = (uint16_t)r;
 }
 int launch_vocab_rank(const uint32_t* sorted_dense, const uint32_t* vslot, uint32_t V, uint32_t* rank_of_slot,
-                      uint32_t* slot_of_rank, hipStream_t s) {
-    k_vocab_rank<<<grid_for(V), NT, 0, s>>>(sorted_dense, vslot, V, rank_of_slot, slot_of_rank);
+                      uint32_t* slot_of_rank, uint16_t* rank16, hipStream_t s) {
+    k_vocab_rank<<<grid_for(V), NT, 0, s>>>(sorted_dense, vslot, V, rank_of_slot, slot_of_rank, rank16);
     return ok();
 }
 
@@ -215,7 +217,8 @@ constexpr uint32_t DFH_MAXV = 65536;
 constexpr int DFH_NT = 1024;
 constexpr int DFH_B = 16;
 __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ rec_slot, uint64_t nrec,
-                                                        const uint32_t* __restrict__ rank_of_slot, uint32_t V,
+                                                        const uint32_t* __restrict__ rank_of_slot,
+                                                        const uint16_t* __restrict__ rank16, uint32_t V,
                                                         uint64_t slot_cap, uint32_t* __restrict__ status,
                                                         uint32_t* __restrict__ part /* [grid][V/2 words] */) {
     extern __shared__ __attribute__((aligned(16))) uint32_t bins[]; /* V/2 words of two u16 counters */
@@ -234,14 +237,22 @@ __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ r
 #pragma unroll
         for (int q = 0; q < DFH_B; ++q) {
             if (sl[q] != 0xFFFFFFFFu && sl[q] >= slot_cap) { atomicOr(status, ST_BOUNDS); sl[q] = 0xFFFFFFFFu; }
-            r[q] = sl[q] != 0xFFFFFFFFu ? rank_of_slot[sl[q]] : 0u;
+#if defined(DF_ABL) && (DF_ABL & 1)
+            r[q] = sl[q] != 0xFFFFFFFFu ? (sl[q] & 0x7FFFu) : 0u; /* timing only */
+#else
+            /* V <= 65536: the 2-byte map (half the footprint of the 4-byte one: more of
+             * these random gathers hit L2) */
+            r[q] = sl[q] == 0xFFFFFFFFu ? 0u : rank16 ? (uint32_t)rank16[sl[q]] : rank_of_slot[sl[q]];
+#endif
         }
 #pragma unroll
         for (int q = 0; q < DFH_B; ++q) {
             if (sl[q] == 0xFFFFFFFFu) continue;
             atomicAdd(&bins[r[q] >> 1], 1u << (16 * (r[q] & 1)));
             /* records carry term ranks from here on: K5 reads them without a gather */
+#if !(defined(DF_ABL) && (DF_ABL & 2))
             __builtin_nontemporal_store(r[q], &rec_slot[i + (uint64_t)q * DFH_NT]);
+#endif
         }
     }
     __syncthreads();
@@ -276,8 +287,8 @@ __global__ void k_df_hist_atomic(uint32_t* __restrict__ rec_slot, uint64_t nrec,
         rec_slot[i] = r;
     }
 }
-int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* rank_of_slot, uint32_t V, uint64_t slot_cap,
-                   uint32_t* status, uint32_t* df, Arena& ar, hipStream_t s) {
+int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* rank_of_slot, const uint16_t* rank16, uint32_t V,
+                   uint64_t slot_cap, uint32_t* status, uint32_t* df, Arena& ar, hipStream_t s) {
     if (V == 0) return 0;
     if (nrec == 0) return hipMemsetAsync(df, 0, (size_t)V * 4, s) == hipSuccess ? 0 : -1;
     if (V <= DFH_MAXV) {
@@ -287,7 +298,8 @@ int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* rank_of_sl
         uint32_t* part = (uint32_t*)ar.get((size_t)nparts * W * 4);
         if (!part) return -2;
         if (hipMemsetAsync(df, 0, (size_t)V * 4, s) != hipSuccess) return -1;
-        k_df_hist_lds<<<nparts, DFH_NT, (size_t)W * 4, s>>>(rec_slot, nrec, rank_of_slot, V, slot_cap, status, part);
+        k_df_hist_lds<<<nparts, DFH_NT, (size_t)W * 4, s>>>(rec_slot, nrec, rank_of_slot, rank16, V, slot_cap, status,
+                                                             part);
         k_df_colsum<<<dim3(grid_for(V), (nparts + DFC_G - 1) / DFC_G), NT, 0, s>>>(part, nparts, V, df);
         ar.release(m);
         return ok();

@@ -93,7 +93,7 @@ int launch_vocab_flags(const VocabDev& v, uint64_t cap, uint32_t* flags, hipStre
 int launch_vocab_compact(const VocabDev& v, uint64_t cap, const uint32_t* dense_of_slot, const CorpusDev& c,
                          uint32_t* vslot, uint4* sortkey, uint32_t* seq, hipStream_t s);
 int launch_vocab_rank(const uint32_t* sorted_dense, const uint32_t* vslot, uint32_t V, uint32_t* rank_of_slot,
-                      uint32_t* slot_of_rank, hipStream_t s);
+                      uint32_t* slot_of_rank, uint16_t* rank16, hipStream_t s);
 int launch_vocab_long_fixup(const uint4* sorted_keys, uint32_t* sorted_dense, const uint32_t* vslot,
                             const VocabDev& v, const CorpusDev& c, uint32_t V, hipStream_t s);
 
@@ -107,8 +107,8 @@ int launch_part_merge(const uint64_t* keys, const uint32_t* seq, const uint32_t*
                       hipStream_t s);
 
 /* DF */
-int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* rank_of_slot, uint32_t V, uint64_t slot_cap,
-                   uint32_t* status, uint32_t* df, Arena& ar, hipStream_t s);
+int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* rank_of_slot, const uint16_t* rank16, uint32_t V,
+                   uint64_t slot_cap, uint32_t* status, uint32_t* df, Arena& ar, hipStream_t s);
 int launch_df_mark(const uint32_t* df, uint32_t V, uint32_t* present, hipStream_t s);
 int launch_df_list(const uint32_t* present_scan, uint64_t nvals, uint32_t* vals, hipStream_t s);
 

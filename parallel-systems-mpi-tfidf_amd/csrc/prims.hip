@@ -286,46 +286,54 @@ __global__ __launch_bounds__(TS_NT) void k_tile_sort(const K* __restrict__ kin, 
     }
 }
 
-/* An element's rank: the searches over the other tiles advance in lockstep, TS_LB at a
- * time, so a thread has TS_LB independent loads in flight per step instead of one
- * dependent chain per tile. */
+/* An element's rank, split over blockIdx.y groups of TS_LB tiles so the grid has
+ * enough waves to hide the searches' latency: each thread advances its group's TS_LB
+ * searches in lockstep (TS_LB independent loads in flight per step) and adds the count
+ * to pos[element] (group 0 also adds the element's index in its own tile). */
 constexpr uint32_t TS_LB = 8;
 template <typename K>
-__global__ __launch_bounds__(256) void k_tile_rank(const K* __restrict__ tk, const uint32_t* __restrict__ tv,
-                                                  const uint32_t* __restrict__ ti, uint64_t n, K* __restrict__ kout,
-                                                  uint32_t* __restrict__ vout) {
+__global__ __launch_bounds__(256) void k_tile_rank(const K* __restrict__ tk, const uint32_t* __restrict__ ti,
+                                                  uint64_t n, uint32_t* __restrict__ pos) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n) return;
     const uint32_t t = (uint32_t)(g / TS_T), nt = (uint32_t)((n + TS_T - 1) / TS_T);
+    const uint32_t b0 = blockIdx.y * TS_LB;
     const K key = tk[g];
     const uint32_t idx = ti[g];
-    uint64_t pos = g - (uint64_t)t * TS_T;
-    for (uint32_t b0 = 0; b0 < nt; b0 += TS_LB) {
-        uint32_t lo[TS_LB], len[TS_LB];
+    uint32_t lo[TS_LB], len[TS_LB];
+#pragma unroll
+    for (uint32_t q = 0; q < TS_LB; ++q) {
+        const uint32_t b = b0 + q;
+        const uint64_t st = (uint64_t)b * TS_T;
+        lo[q] = 0;
+        len[q] = (b < nt && b != t) ? (uint32_t)((n - st) < TS_T ? (n - st) : TS_T) : 0u;
+    }
+    for (uint32_t it = 0; it < 12; ++it) {  /* ceil(log2(TS_T + 1)) steps */
 #pragma unroll
         for (uint32_t q = 0; q < TS_LB; ++q) {
-            const uint32_t b = b0 + q;
-            const uint64_t st = (uint64_t)b * TS_T;
-            lo[q] = 0;
-            len[q] = (b < nt && b != t) ? (uint32_t)((n - st) < TS_T ? (n - st) : TS_T) : 0u;
+            if (len[q] == 0u) continue;
+            const uint32_t half = len[q] >> 1, mid = lo[q] + half;
+            const uint64_t e = (uint64_t)(b0 + q) * TS_T + mid;
+            const K m = tk[e];
+            const bool before = key_lt(m, key) || (key_eq(m, key) && ti[e] < idx);
+            if (before) { lo[q] = mid + 1u; len[q] -= half + 1u; }
+            else len[q] = half;
         }
-        for (uint32_t it = 0; it < 12; ++it) {  /* ceil(log2(TS_T + 1)) steps */
-#pragma unroll
-            for (uint32_t q = 0; q < TS_LB; ++q) {
-                if (len[q] == 0u) continue;
-                const uint32_t half = len[q] >> 1, mid = lo[q] + half;
-                const uint64_t e = (uint64_t)(b0 + q) * TS_T + mid;
-                const K m = tk[e];
-                const bool before = key_lt(m, key) || (key_eq(m, key) && ti[e] < idx);
-                if (before) { lo[q] = mid + 1u; len[q] -= half + 1u; }
-                else len[q] = half;
-            }
-        }
-#pragma unroll
-        for (uint32_t q = 0; q < TS_LB; ++q) pos += lo[q];
     }
-    kout[pos] = key;
-    vout[pos] = tv[g];
+    uint32_t c = blockIdx.y == 0 ? (uint32_t)(g - (uint64_t)t * TS_T) : 0u;
+#pragma unroll
+    for (uint32_t q = 0; q < TS_LB; ++q) c += lo[q];
+    if (c) atomicAdd(&pos[g], c);
+}
+template <typename K>
+__global__ void k_tile_place(const K* __restrict__ tk, const uint32_t* __restrict__ tv,
+                             const uint32_t* __restrict__ pos, uint64_t n, K* __restrict__ kout,
+                             uint32_t* __restrict__ vout) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n) return;
+    const uint32_t p = pos[g];
+    kout[p] = tk[g];
+    vout[p] = tv[g];
 }
 
 template <typename K>
@@ -336,8 +344,12 @@ int tile_sort_t(const K* k0, const uint32_t* v0, K* k1, uint32_t* v1, uint64_t n
     uint32_t* tv = (uint32_t*)ar.get(n * 4);
     uint32_t* ti = (uint32_t*)ar.get(n * 4);
     if (!tk || !tv || !ti) return -2;
+    uint32_t* pos = (uint32_t*)ar.get(n * 4);
+    if (!pos) return -2;
+    if (hipMemsetAsync(pos, 0, n * 4, s) != hipSuccess) return -1;
     k_tile_sort<K><<<nt, TS_NT, 0, s>>>(k0, v0, n, tk, tv, ti);
-    k_tile_rank<K><<<(unsigned)((n + 255) / 256), 256, 0, s>>>(tk, tv, ti, n, k1, v1);
+    k_tile_rank<K><<<dim3((unsigned)((n + 255) / 256), (nt + TS_LB - 1) / TS_LB), 256, 0, s>>>(tk, ti, n, pos);
+    k_tile_place<K><<<(unsigned)((n + 255) / 256), 256, 0, s>>>(tk, tv, pos, n, k1, v1);
     ar.release(m);
     return hipGetLastError() == hipSuccess ? 1 : -1;
 }
