@@ -484,11 +484,10 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
         uint32_t* ph = ctx->phead.as<uint32_t>();
         LCHK(launch_part_heads(pk, Q, ph, s));
         LCHK(scan_excl_u32(ph, ph, Q, ar, s));
-        uint32_t U = 0;
-        HIPCHK(hipMemcpyAsync(&U, ph + Q, 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        if (R_main + U > ctx->rec_cap) {
-            uint64_t ncap = R_main + U + (R_main + U) / 8 + 4096;
+        /* U = ph[Q] merged records (<= Q) stays on the device: no host round trip; the
+         * record arrays are sized for the worst case R_main + Q */
+        if (R_main + Q > ctx->rec_cap) {
+            uint64_t ncap = R_main + Q + (R_main + Q) / 8 + 4096;
             if (ctx->rec_slot.grow_keep(ncap * 4, R_main * 4, s) || ctx->rec_cnt.grow_keep(ncap * 4, R_main * 4, s))
                 return TFIDF_E_NOMEM;
             ctx->rec_cap = ncap;
@@ -497,14 +496,15 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
                                ctx->rec_slot.as<uint32_t>(), ctx->rec_cnt.as<uint32_t>(),
                                ctx->doc_recoff.as<uint64_t>(), ctx->doc_npairs.as<uint32_t>(),
                                ctx->doc_flags.as<uint8_t>(), s));
-        R_total = R_main + U;
+        R_total = R_main + Q; /* an upper bound: the true count is R_main + ph[Q] */
     }
     /* ---- DF ---- */
     mark(ctx, S_DF);
     ENSURE(ctx->df_local, (size_t)V * 4 + 4);
     ENSURE(ctx->df_global, (size_t)V * 4 + 4);
     /* also rewrites every record's slot as its term rank (K5 then needs no rank gather) */
-    LCHK(launch_df_hist(ctx->rec_slot.as<uint32_t>(), R_total, ctx->rank_of_slot.as<uint32_t>(),
+    LCHK(launch_df_hist(ctx->rec_slot.as<uint32_t>(), R_main, Q ? ctx->phead.as<uint32_t>() + Q : nullptr, R_total,
+                        ctx->rank_of_slot.as<uint32_t>(),
                         V <= 65536u ? ctx->rank16.as<uint16_t>() : nullptr, V, cap,
                         (uint32_t*)(cnt + 3), ctx->df_local.as<uint32_t>(), ar, s));
     mark(ctx, S_EXCHANGE);
@@ -515,41 +515,42 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
         ctx->Vg = V;
         if (V) HIPCHK(hipMemcpyAsync(ctx->df_global.p, ctx->df_local.p, (size_t)V * 4, hipMemcpyDeviceToDevice, s));
     }
-    /* ---- idf LUT: log(N/df) on the host's libm for each distinct df (TFIDF.c:243) ---- */
+    /* ---- idf LUT: log(N/df) on the host's libm for each distinct df (TFIDF.c:243) ----
+     * The distinct df values are listed on the device; their count K, the first
+     * IDF_SPEC of them and the pair total P come back in ONE host round trip together
+     * with the document-order stage below. */
     mark(ctx, S_IDF);
     ENSURE(ctx->present, (Nt + 2) * 4);
     HIPCHK(hipMemsetAsync(ctx->present.p, 0, (Nt + 2) * 4, s));
     LCHK(launch_df_mark(ctx->df_global.as<uint32_t>(), V, ctx->present.as<uint32_t>(), s));
     LCHK(scan_excl_u32(ctx->present.as<uint32_t>(), ctx->present.as<uint32_t>(), Nt + 1, ar, s));
-    uint32_t K = 0;
-    HIPCHK(hipMemcpyAsync(&K, ctx->present.as<uint32_t>() + Nt + 1, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    ENSURE(ctx->idf_vals, (size_t)K * 8 + 8);
-    uint32_t* vals_dev = (uint32_t*)ar.get((size_t)K * 4 + 4);
+    uint32_t* vals_dev = (uint32_t*)ar.get((size_t)(Nt + 2) * 4);
     if (!vals_dev) return 1;
     LCHK(launch_df_list(ctx->present.as<uint32_t>(), Nt + 1, vals_dev, s));
-    std::vector<uint32_t> vals(K);
-    std::vector<double> idf(K);
-    if (K) HIPCHK(hipMemcpyAsync(vals.data(), vals_dev, (size_t)K * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    for (uint32_t k = 0; k < K; ++k) idf[k] = log(1.0 * (double)Nt / (double)vals[k]);
-    if (K) HIPCHK(hipMemcpyAsync(ctx->idf_vals.p, idf.data(), (size_t)K * 8, hipMemcpyHostToDevice, s));
-    /* ---- document order ---- */
+    constexpr uint32_t IDF_SPEC = 16384;
+    const uint32_t spec = (uint32_t)((Nt + 1) < IDF_SPEC ? (Nt + 1) : IDF_SPEC);
+    std::vector<uint32_t> vals(spec);
+    uint32_t K = 0;
+    HIPCHK(hipMemcpyAsync(&K, ctx->present.as<uint32_t>() + Nt + 1, 4, hipMemcpyDeviceToHost, s));
+    if (spec) HIPCHK(hipMemcpyAsync(vals.data(), vals_dev, (size_t)spec * 4, hipMemcpyDeviceToHost, s));
+    /* ---- document order: per-position metadata and pair offsets ---- */
     mark(ctx, S_ORDER);
+    ENSURE(ctx->npairs_ord, (size_t)N * 8 + 8);
+    ENSURE(ctx->out_off, (size_t)N * 8 + 8);
     ENSURE(ctx->dkey0, (size_t)N * 8 + 8);
     ENSURE(ctx->dkey1, (size_t)N * 8 + 8);
     ENSURE(ctx->dseq0, (size_t)N * 4 + 4);
     ENSURE(ctx->dseq1, (size_t)N * 4 + 4);
-    ENSURE(ctx->npairs_ord, (size_t)N * 8 + 8);
-    ENSURE(ctx->out_off, (size_t)N * 8 + 8);
     LCHK(launch_doc_keys(dev_ids, N, ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), s));
-    uint32_t dm = 0;
-    dm = 0x1Fu; /* base-11 keys of 10 digits are < 11^10 < 2^35: five bytes, no probe */
-    /* five known digit bytes: the radix sort beats the tile sort's 49-tile rank search here */
-    int dc = radix_sort_u64(ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), ctx->dkey1.as<uint64_t>(),
-                            ctx->dseq1.as<uint32_t>(), N, dm, ar, s);
-    LCHK(dc);
-    ctx->order = dc ? ctx->dseq1.as<uint32_t>() : ctx->dseq0.as<uint32_t>();
+    /* base-11 keys of 10 digits are < 11^10 < 2^35: five bytes, no probe.  (A side
+     * stream overlapping this sort with K1 was slower: K1's persistent grid then starts
+     * on fewer CUs.) */
+    {
+        int dc = radix_sort_u64(ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), ctx->dkey1.as<uint64_t>(),
+                                ctx->dseq1.as<uint32_t>(), N, 0x1Fu, ar, s);
+        LCHK(dc);
+        ctx->order = dc ? ctx->dseq1.as<uint32_t>() : ctx->dseq0.as<uint32_t>();
+    }
     ENSURE(ctx->doc_meta, (size_t)N * 16 + 16);
     LCHK(launch_gather_meta(ctx->order, ctx->doc_npairs.as<uint32_t>(), ctx->doc_recoff.as<uint64_t>(),
                             ctx->doc_size.as<uint32_t>(), ctx->doc_flags.as<uint8_t>(), N,
@@ -558,6 +559,14 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     uint64_t P = 0;
     HIPCHK(hipMemcpyAsync(&P, ctx->out_off.as<uint64_t>() + N, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    if (K > spec) {
+        vals.resize(K);
+        HIPCHK(hipMemcpy(vals.data() + spec, vals_dev + spec, (size_t)(K - spec) * 4, hipMemcpyDeviceToHost));
+    }
+    ENSURE(ctx->idf_vals, (size_t)K * 8 + 8);
+    std::vector<double> idf(K);
+    for (uint32_t k = 0; k < K; ++k) idf[k] = log(1.0 * (double)Nt / (double)vals[k]);
+    if (K) HIPCHK(hipMemcpyAsync(ctx->idf_vals.p, idf.data(), (size_t)K * 8, hipMemcpyHostToDevice, s));
     ctx->npairs = P;
     /* ---- score + per-document term order ---- */
     mark(ctx, S_SCORE);

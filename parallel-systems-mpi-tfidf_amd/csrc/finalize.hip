@@ -217,6 +217,7 @@ constexpr uint32_t DFH_MAXV = 65536;
 constexpr int DFH_NT = 1024;
 constexpr int DFH_B = 16;
 __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ rec_slot, uint64_t nrec,
+                                                        const uint32_t* __restrict__ nrec_extra,
                                                         const uint32_t* __restrict__ rank_of_slot,
                                                         const uint16_t* __restrict__ rank16, uint32_t V,
                                                         uint64_t slot_cap, uint32_t* __restrict__ status,
@@ -225,6 +226,7 @@ __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ r
     const uint32_t W = (V + 1) / 2;
     for (uint32_t k = threadIdx.x; k < W; k += DFH_NT) bins[k] = 0;
     __syncthreads();
+    if (nrec_extra) nrec += *nrec_extra; /* merged partial records, counted on the device */
     const uint64_t r0 = (uint64_t)blockIdx.x * DFH_RECS;
     const uint64_t r1 = r0 + DFH_RECS < nrec ? r0 + DFH_RECS : nrec;
     for (uint64_t i = r0 + threadIdx.x; i < r1; i += (uint64_t)DFH_B * DFH_NT) {
@@ -276,9 +278,10 @@ __global__ void k_df_colsum(const uint32_t* __restrict__ part, uint32_t nparts, 
     for (uint32_t q = 0; q < DFC_G; ++q) sum += (v[q] >> sh) & 0xFFFFu;
     if (sum) atomicAdd(&df[r], sum);
 }
-__global__ void k_df_hist_atomic(uint32_t* __restrict__ rec_slot, uint64_t nrec,
+__global__ void k_df_hist_atomic(uint32_t* __restrict__ rec_slot, uint64_t nrec, const uint32_t* __restrict__ nrec_extra,
                                  const uint32_t* __restrict__ rank_of_slot, uint64_t slot_cap,
                                  uint32_t* __restrict__ status, uint32_t* __restrict__ df) {
+    if (nrec_extra) nrec += *nrec_extra;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nrec; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t sl = rec_slot[i];
         if (sl >= slot_cap) { atomicOr(status, ST_BOUNDS); continue; }
@@ -287,25 +290,27 @@ __global__ void k_df_hist_atomic(uint32_t* __restrict__ rec_slot, uint64_t nrec,
         rec_slot[i] = r;
     }
 }
-int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* rank_of_slot, const uint16_t* rank16, uint32_t V,
-                   uint64_t slot_cap, uint32_t* status, uint32_t* df, Arena& ar, hipStream_t s) {
+int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra, uint64_t nrec_max,
+                   const uint32_t* rank_of_slot, const uint16_t* rank16, uint32_t V, uint64_t slot_cap,
+                   uint32_t* status, uint32_t* df, Arena& ar, hipStream_t s) {
     if (V == 0) return 0;
-    if (nrec == 0) return hipMemsetAsync(df, 0, (size_t)V * 4, s) == hipSuccess ? 0 : -1;
+    if (nrec_max < nrec) nrec_max = nrec;
+    if (nrec_max == 0) return hipMemsetAsync(df, 0, (size_t)V * 4, s) == hipSuccess ? 0 : -1;
     if (V <= DFH_MAXV) {
-        uint32_t nparts = (uint32_t)((nrec + DFH_RECS - 1) / DFH_RECS);
+        uint32_t nparts = (uint32_t)((nrec_max + DFH_RECS - 1) / DFH_RECS);
         uint32_t W = (V + 1) / 2;
         size_t m = ar.mark();
         uint32_t* part = (uint32_t*)ar.get((size_t)nparts * W * 4);
         if (!part) return -2;
         if (hipMemsetAsync(df, 0, (size_t)V * 4, s) != hipSuccess) return -1;
-        k_df_hist_lds<<<nparts, DFH_NT, (size_t)W * 4, s>>>(rec_slot, nrec, rank_of_slot, rank16, V, slot_cap, status,
+        k_df_hist_lds<<<nparts, DFH_NT, (size_t)W * 4, s>>>(rec_slot, nrec, nrec_extra, rank_of_slot, rank16, V, slot_cap, status,
                                                              part);
         k_df_colsum<<<dim3(grid_for(V), (nparts + DFC_G - 1) / DFC_G), NT, 0, s>>>(part, nparts, V, df);
         ar.release(m);
         return ok();
     }
     if (hipMemsetAsync(df, 0, (size_t)V * 4, s) != hipSuccess) return -1;
-    k_df_hist_atomic<<<2048, NT, 0, s>>>(rec_slot, nrec, rank_of_slot, slot_cap, status, df);
+    k_df_hist_atomic<<<2048, NT, 0, s>>>(rec_slot, nrec, nrec_extra, rank_of_slot, slot_cap, status, df);
     return ok();
 }
 
@@ -383,6 +388,12 @@ constexpr uint32_t K5_SMALL = 64;     /* one wave, bitonic across the lanes */
 constexpr uint32_t K5_WAVE = 1024;    /* one wave, LDS radix sort of packed (rank, index) keys */
 constexpr uint32_t K5_IDX_BITS = 11;  /* index bits of a packed key (n <= 2048) */
 constexpr int K5_BATCH = 8;           /* gathers per lane in flight together */
+#ifndef K5_EB
+#define K5_EB 4                       /* bucket path: idf gathers per lane in flight together */
+#endif
+#ifndef K5_WPS
+#define K5_WPS 4                      /* waves per SIMD the wave kernel is compiled for */
+#endif
 constexpr uint32_t K5_NB_BITS = 9;    /* bucket sort: 512 buckets by the rank's top bits */
 constexpr uint32_t K5_NB = 1u << K5_NB_BITS;
 constexpr uint32_t K5_GROUP_MAX = 48; /* larger buckets (skewed ranks): the radix path */
@@ -517,7 +528,7 @@ __device__ __forceinline__ void k5_prefetch(const K5Args& a, const uint4& m, uin
     }
 }
 
-__global__ __launch_bounds__(NT, 4) void k_score_wave(K5Args a) {
+__global__ __launch_bounds__(NT, K5_WPS) void k_score_wave(K5Args a) {
     __shared__ uint32_t kb[NT / 64][2][K5_WAVE];
     __shared__ uint32_t hist[NT / 64][K5_NB];
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -671,7 +682,7 @@ __global__ __launch_bounds__(NT, 4) void k_score_wave(K5Args a) {
             if (64u * q + lane < n) buf1[pp[q]] = pk[q];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        constexpr int EB = 4;
+        constexpr int EB = K5_EB;
         for (uint32_t j0 = 0; j0 < n; j0 += 64 * EB) {
             uint32_t key[EB], cnt[EB];
             double idf[EB];

@@ -107,8 +107,9 @@ int launch_part_merge(const uint64_t* keys, const uint32_t* seq, const uint32_t*
                       hipStream_t s);
 
 /* DF */
-int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* rank_of_slot, const uint16_t* rank16, uint32_t V,
-                   uint64_t slot_cap, uint32_t* status, uint32_t* df, Arena& ar, hipStream_t s);
+int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra, uint64_t nrec_max,
+                   const uint32_t* rank_of_slot, const uint16_t* rank16, uint32_t V, uint64_t slot_cap,
+                   uint32_t* status, uint32_t* df, Arena& ar, hipStream_t s);
 int launch_df_mark(const uint32_t* df, uint32_t V, uint32_t* present, hipStream_t s);
 int launch_df_list(const uint32_t* present_scan, uint64_t nvals, uint32_t* vals, hipStream_t s);
 
