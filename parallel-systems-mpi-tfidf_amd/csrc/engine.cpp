@@ -379,6 +379,7 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     o.doc_size = ctx->doc_size.as<uint32_t>();
     o.doc_flags = ctx->doc_flags.as<uint8_t>();
     o.ntokens = cnt + 2;
+    o.chunk_ctr = cnt + 5;
     o.status = (uint32_t*)(cnt + 3);
     o.stamps = nullptr;
     o.ablate = ctx->ablate;

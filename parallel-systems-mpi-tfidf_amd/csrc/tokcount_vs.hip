@@ -106,6 +106,7 @@ struct VsShared {
     uint32_t over;                        /* overflow mode */
     uint32_t wsum[NWAVE];
     unsigned long long rec_base, part_base;
+    uint64_t next_chunk;                  /* dynamic chunk schedule */
 };
 
 /* Streaming corpus load: clamped to the last 16-byte block holding corpus bytes, and
@@ -435,10 +436,17 @@ __global__ __launch_bounds__(NT, K1_WAVES_PER_SIMD) void k_tokcount_vs(CorpusDev
         STAMP(st, 10);
     };
 
-    for (uint64_t chunk = c0 + blockIdx.x; chunk < c1; chunk += gridDim.x) {
+    /* chunks are handed out by a global counter (chunk sizes vary up to BIG_DOC, so a
+     * static round-robin share leaves a tail of the slowest workgroups); the next index
+     * is claimed when a chunk starts, so the atomic's round trip is hidden */
+    if (tid == 0) S.next_chunk = c0 + atomicAdd(o.chunk_ctr, 1ull);
+    lds_barrier();
+    uint64_t next_claim = 0;
+    for (uint64_t chunk = uni64(S.next_chunk); chunk < c1; chunk = uni64(S.next_chunk)) {
+        if (tid == 0) next_claim = c0 + atomicAdd(o.chunk_ctr, 1ull);
         const uint64_t cs = chunk_start[chunk], ce = chunk_start[chunk + 1];
-        if (cs >= ce) continue;
         const uint32_t dfirst = chunk_doc[chunk], dlast = chunk_doc[chunk + 1];
+        if (cs < ce)
         for (uint32_t gd0 = dfirst; gd0 <= dlast; gd0 += GCAP) {
             gd0_cur = gd0;
             const uint32_t ng = (dlast + 1 - gd0) < (uint32_t)GCAP ? (dlast + 1 - gd0) : (uint32_t)GCAP;
@@ -625,6 +633,8 @@ __global__ __launch_bounds__(NT, K1_WAVES_PER_SIMD) void k_tokcount_vs(CorpusDev
             STAMP(st, 3);
             if (gd0 + GCAP < gd0) break; /* overflow guard */
         }
+        if (tid == 0) S.next_chunk = next_claim;
+        lds_barrier();
     }
     /* tokens (wave-uniform count): one atomic per wave */
     if (lane == 0 && tokens_wg) atomicAdd(o.ntokens, tokens_wg);
