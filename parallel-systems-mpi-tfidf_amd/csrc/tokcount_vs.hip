@@ -463,30 +463,29 @@ __global__ __launch_bounds__(NT, K1_WAVES_PER_SIMD) void k_tokcount_vs(CorpusDev
                 const uint64_t b0 = gs & ~(uint64_t)15;
                 const uint32_t nsteps = (uint32_t)((ge - b0 + WSTEP - 1) / WSTEP);
                 const uint64_t lane_off = 16ull * lane;
-                uint4 pf0 = make_uint4(0, 0, 0, 0), pf1 = pf0, pe0 = pf0, pe1 = pf0;
+                uint4 pf0 = make_uint4(0, 0, 0, 0), pe0 = pf0;
                 {
                     const uint64_t a0 = b0 + (uint64_t)wid * WSTEP + lane_off;
-                    const uint64_t a1 = a0 + (uint64_t)NWAVE * WSTEP;
                     pf0 = ld16c(c.bytes, last_blk, a0);
-                    pf1 = ld16c(c.bytes, last_blk, a1);
-                    if (edge_lane) { pe0 = ld16c(c.bytes, last_blk, a0 + eoff); pe1 = ld16c(c.bytes, last_blk, a1 + eoff); }
+                    if (edge_lane) pe0 = ld16c(c.bytes, last_blk, a0 + eoff);
                 }
                 uint32_t wr = 0;             /* wave-uniform: document containing the step start */
                 uint16_t* tl = S.tlist[wid];
                 for (uint32_t s = wid; s < nsteps; s += NWAVE) {
                     const uint64_t sb = b0 + (uint64_t)s * WSTEP;
                     const uint64_t gpos = sb + lane_off;
+                    /* one step of prefetch: the copy into `cur` waits for the load issued a
+                     * step ago (a second buffer's copy forced a wait for the load just
+                     * issued at every step end) */
                     const uint4 cur = pf0, edge = pe0;
-                    pf0 = pf1;
-                    pe0 = pe1;
                     {
-                        const uint64_t a2 = gpos + 2ull * NWAVE * WSTEP; /* harmless past ge */
+                        const uint64_t a1 = gpos + 1ull * NWAVE * WSTEP; /* harmless past ge */
 #if K1_ABL & 32
-                        pf1 = make_uint4(0x20616161u ^ (uint32_t)a2, 0x61612061u, 0x61206161u, 0x20616161u);
-                        pe1 = pf1;
+                        pf0 = make_uint4(0x20616161u ^ (uint32_t)a1, 0x61612061u, 0x61206161u, 0x20616161u);
+                        pe0 = pf0;
 #else
-                        pf1 = ld16c(c.bytes, last_blk, a2);
-                        if (edge_lane) pe1 = ld16c(c.bytes, last_blk, a2 + eoff);
+                        pf0 = ld16c(c.bytes, last_blk, a1);
+                        if (edge_lane) pe0 = ld16c(c.bytes, last_blk, a1 + eoff);
 #endif
                     }
                     STAMP(st, 11);
