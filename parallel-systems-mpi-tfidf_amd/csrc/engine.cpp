@@ -81,6 +81,12 @@ struct tfidf_ctx {
     hipEvent_t ev[S_NSTAGES + 1];
     Arena arena;
     DevBuf arena_buf;
+    /* side stream: the document-order sort (needs only the document ids) runs beside the
+     * vocabulary / merge / DF stages, after K1 (K1's persistent grid wants every CU) */
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_order = nullptr;
+    Arena arena2;
+    DevBuf arena2_buf;
     /* host-input staging */
     DevBuf in_bytes, in_off, in_ids;
     /* synthetic corpus */
@@ -203,6 +209,9 @@ int tfidf_open(int device, tfidf_ctx** out) {
         if (l >= 10 && l <= 90) ctx->vload_pct = l;
     }
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ctx->ev_order, hipEventDisableTiming));
     for (int i = 0; i <= S_NSTAGES; ++i) HIPCHK(hipEventCreate(&ctx->ev[i]));
     if (arena_reset(ctx, 64ull << 20) != 0) { delete ctx; return TFIDF_E_NOMEM; }
     if (ctx->counters.ensure(256) != 0) { delete ctx; return TFIDF_E_NOMEM; }
@@ -215,6 +224,10 @@ void tfidf_close(tfidf_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+    if (ctx->stream2) { (void)hipStreamSynchronize(ctx->stream2); (void)hipStreamDestroy(ctx->stream2); }
+    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    if (ctx->ev_order) (void)hipEventDestroy(ctx->ev_order);
+    ctx->arena2_buf.release();
     DevBuf* bufs[] = {&ctx->arena_buf, &ctx->in_bytes, &ctx->in_off, &ctx->in_ids, &ctx->syn_bytes, &ctx->syn_off,
                       &ctx->syn_ids, &ctx->syn_ntok, &ctx->syn_blkfirst, &ctx->syn_blkbytes, &ctx->syn_cdf,
                       &ctx->chunk_start, &ctx->chunk_doc, &ctx->vkeys, &ctx->vrep, &ctx->rec_slot, &ctx->rec_cnt,
@@ -420,6 +433,28 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     if (st & ST_REC_FULL) { ctx->rec_cap = R_main + R_main / 4 + 4096; retry = true; }
     if (st & ST_PART_FULL) { ctx->part_cap = Q + Q / 4 + 4096; retry = true; }
     if (retry) return 1;
+    /* ---- document order on the side stream (joined before the per-position metadata) ---- */
+    ENSURE(ctx->dkey0, (size_t)N * 8 + 8);
+    ENSURE(ctx->dkey1, (size_t)N * 8 + 8);
+    ENSURE(ctx->dseq0, (size_t)N * 4 + 4);
+    ENSURE(ctx->dseq1, (size_t)N * 4 + 4);
+    {
+        hipStream_t s2 = ctx->stream2;
+        const size_t need2 = (size_t)256 * 4 * ((N + 2047) / 2048 + 1) + (1u << 20);
+        if (need2 > ctx->arena2_buf.cap && ctx->arena2_buf.ensure(need2) != 0) return TFIDF_E_NOMEM;
+        ctx->arena2.base = (uint8_t*)ctx->arena2_buf.p;
+        ctx->arena2.cap = ctx->arena2_buf.cap;
+        ctx->arena2.used = 0;
+        HIPCHK(hipEventRecord(ctx->ev_fork, s));
+        HIPCHK(hipStreamWaitEvent(s2, ctx->ev_fork, 0));
+        LCHK(launch_doc_keys(dev_ids, N, ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), s2));
+        /* base-11 keys of 10 digits are < 11^10 < 2^35: five bytes, no probe */
+        int dc = radix_sort_u64(ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), ctx->dkey1.as<uint64_t>(),
+                                ctx->dseq1.as<uint32_t>(), N, 0x1Fu, ctx->arena2, s2);
+        LCHK(dc);
+        ctx->order = dc ? ctx->dseq1.as<uint32_t>() : ctx->dseq0.as<uint32_t>();
+        HIPCHK(hipEventRecord(ctx->ev_order, s2));
+    }
     /* ---- vocabulary ---- */
     const uint64_t cap = ctx->vcap;
     ENSURE(ctx->dense, (cap + 1) * 4);
@@ -538,20 +573,7 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     mark(ctx, S_ORDER);
     ENSURE(ctx->npairs_ord, (size_t)N * 8 + 8);
     ENSURE(ctx->out_off, (size_t)N * 8 + 8);
-    ENSURE(ctx->dkey0, (size_t)N * 8 + 8);
-    ENSURE(ctx->dkey1, (size_t)N * 8 + 8);
-    ENSURE(ctx->dseq0, (size_t)N * 4 + 4);
-    ENSURE(ctx->dseq1, (size_t)N * 4 + 4);
-    LCHK(launch_doc_keys(dev_ids, N, ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), s));
-    /* base-11 keys of 10 digits are < 11^10 < 2^35: five bytes, no probe.  (A side
-     * stream overlapping this sort with K1 was slower: K1's persistent grid then starts
-     * on fewer CUs.) */
-    {
-        int dc = radix_sort_u64(ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), ctx->dkey1.as<uint64_t>(),
-                                ctx->dseq1.as<uint32_t>(), N, 0x1Fu, ar, s);
-        LCHK(dc);
-        ctx->order = dc ? ctx->dseq1.as<uint32_t>() : ctx->dseq0.as<uint32_t>();
-    }
+    HIPCHK(hipStreamWaitEvent(s, ctx->ev_order, 0)); /* join the side stream's document order */
     ENSURE(ctx->doc_meta, (size_t)N * 16 + 16);
     LCHK(launch_gather_meta(ctx->order, ctx->doc_npairs.as<uint32_t>(), ctx->doc_recoff.as<uint64_t>(),
                             ctx->doc_size.as<uint32_t>(), ctx->doc_flags.as<uint8_t>(), N,
@@ -664,7 +686,7 @@ extern "C" int tfidf_run(tfidf_ctx* ctx, const tfidf_corpus* in) {
         size_t need = ctx->arena.peak > ctx->arena_buf.cap ? ctx->arena.peak * 2 : ctx->arena_buf.cap;
         if (arena_reset(ctx, need) != 0) return TFIDF_E_NOMEM;
         rc = run_once(ctx, c, dev_ids, Nt);
-        if (rc == 1) HIPCHK(hipStreamSynchronize(s));
+        if (rc == 1) { HIPCHK(hipStreamSynchronize(s)); HIPCHK(hipStreamSynchronize(ctx->stream2)); }
     }
     if (rc == 1) return TFIDF_E_CAPACITY;
     if (rc) return rc;
