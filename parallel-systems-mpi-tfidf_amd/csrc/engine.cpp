@@ -415,8 +415,16 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
         ctx->npairs = 0;
         return 0;
     }
+    /* the vocabulary's used-slot flags and count are enqueued before the host reads K1's
+     * counters: one host round trip for both */
+    const uint64_t cap = ctx->vcap;
+    ENSURE(ctx->dense, (cap + 1) * 4);
+    LCHK(launch_vocab_flags(vd, cap, ctx->dense.as<uint32_t>(), s));
+    LCHK(scan_excl_u32(ctx->dense.as<uint32_t>(), ctx->dense.as<uint32_t>(), cap, ar, s));
+    uint32_t V = 0;
     unsigned long long hc[4];
     HIPCHK(hipMemcpyAsync(hc, cnt, sizeof hc, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&V, ctx->dense.as<uint32_t>() + cap, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     const uint64_t R_main = hc[0], Q = hc[1];
     const uint32_t st = (uint32_t)hc[3];
@@ -456,13 +464,6 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
         HIPCHK(hipEventRecord(ctx->ev_order, s2));
     }
     /* ---- vocabulary ---- */
-    const uint64_t cap = ctx->vcap;
-    ENSURE(ctx->dense, (cap + 1) * 4);
-    LCHK(launch_vocab_flags(vd, cap, ctx->dense.as<uint32_t>(), s));
-    LCHK(scan_excl_u32(ctx->dense.as<uint32_t>(), ctx->dense.as<uint32_t>(), cap, ar, s));
-    uint32_t V = 0;
-    HIPCHK(hipMemcpyAsync(&V, ctx->dense.as<uint32_t>() + cap, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
     ctx->V = V;
     if ((uint64_t)V * 100 > cap * ctx->vload_pct) { ctx->vcap *= 4; return 1; } /* keep probes short */
     ENSURE(ctx->vslot, (size_t)V * 4 + 4);
