@@ -173,6 +173,26 @@ int tfidf_ingest_dir(const char* dir, uint8_t** bytes, uint64_t* nbytes,
                      uint64_t** doc_off, uint32_t* ndocs, uint32_t* bad_doc);
 void tfidf_free(void* p);
 
+/* Streaming ingest into HBM (replaces TFIDF.c:98-110,130-147): the
+ * same contract as tfidf_ingest_dir (N = entries of `dir` other than "." and "..";
+ * documents dir/doc1..docN; TFIDF_E_NOINPUT / TFIDF_E_NODOC with *bad_doc = the smallest
+ * document that cannot be read), but the files are pread() by `nthreads` host threads
+ * (0: OMP_NUM_THREADS, at most 16) into a ring of pinned 8 MiB segments whose H2D copies
+ * overlap the reads.  *out is a device corpus (TFIDF_CORPUS_DEVICE, doc ids 1..N) owned
+ * by the context, valid until the next ingest, host-corpus tfidf_run or tfidf_close.
+ * `info` (optional) receives sizes and host wall times. */
+typedef struct tfidf_ingest_info {
+    uint64_t nbytes;      /* corpus bytes */
+    uint64_t segments;    /* 8 MiB staging segments copied */
+    uint32_t ndocs;       /* N */
+    uint32_t threads;     /* reader threads used */
+    double   ms_scan;     /* directory count + open/fstat of every document */
+    double   ms_read;     /* reads + overlapped H2D, until the last copy completed */
+    double   ms_total;
+} tfidf_ingest_info;
+int tfidf_ingest_dir_device(tfidf_ctx* ctx, const char* dir, int nthreads, tfidf_corpus* out,
+                            uint32_t* bad_doc, tfidf_ingest_info* info);
+
 /* ---------------------------------------------------------------- synthetic - */
 
 /* Synthetic Zipfian corpus (generator in csrc/synth.h).  ntok[i] tokens

@@ -6,7 +6,13 @@
 #include "dev_common.h"
 #include "kernels.h"
 
-#define VOCAB_MAX_PROBE (1u << 20)
+/* A probe run this long only happens in a table close to full (expected runs are a few
+ * slots at the engine's load limits): the insert flags ST_VOCAB_FULL and the engine
+ * retries with a larger table.  Once the flag is up, every other insert stops within 64
+ * probes, so a run over a too-small table (e.g. config 4's 1e7 terms against the first
+ * 1M-slot table) ends after about one pass of tokens instead of probing the full table
+ * per token. */
+#define VOCAB_MAX_PROBE 4096u
 
 /* Lock-free find-or-insert of a 128-bit key into the global vocabulary.
  * A slot is {lo, hi}; hi is the claim word: EMPTY -> PENDING (CAS) -> key (exchange)
@@ -18,6 +24,8 @@ __device__ __forceinline__ uint32_t vocab_insert_s(uint4* __restrict__ keys, uin
                                                 uint64_t klo, uint64_t khi, uint64_t rep, uint32_t* status) {
     uint64_t h = key_hash(klo, khi) & mask;
     for (uint32_t probe = 0; probe < VOCAB_MAX_PROBE && probe <= mask; ++probe, h = (h + 1) & mask) {
+        if ((probe & 63u) == 63u && (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ST_VOCAB_FULL))
+            return INVALID_SLOT;
         unsigned long long* slot = reinterpret_cast<unsigned long long*>(&keys[h]);
         uint4 s = keys[h];
         uint64_t lo = ((uint64_t)s.y << 32) | s.x, hi = ((uint64_t)s.w << 32) | s.z;

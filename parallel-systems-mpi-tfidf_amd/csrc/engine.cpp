@@ -97,6 +97,7 @@ struct tfidf_ctx {
     /* vocabulary table: K1 is measurably faster at low load (fewer displaced keys behind
      * the two slots it loads per token): 1M slots (16 MB) to start, x4 past 12 % load */
     uint64_t vcap = 1ull << 20;
+#define VOCAB_LOW_LOAD_CAP (1ull << 24)
     uint32_t vload_pct = 12;
     DevBuf rec_slot, rec_cnt;
     uint64_t rec_cap = 0;
@@ -437,7 +438,11 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
         fprintf(stderr, "tfidf: internal bounds check tripped in K1 (status 0x%x)\n", st);
         return TFIDF_E_STATE;
     }
-    if (st & ST_VOCAB_FULL) { ctx->vcap *= 4; retry = true; }
+    if (st & ST_VOCAB_FULL) {   /* the run stopped inserting early: V unknown */
+        if (ctx->vcap >= K1_VS_MAX_CAP) return TFIDF_E_CAPACITY;
+        ctx->vcap = ctx->vcap * 8 < K1_VS_MAX_CAP ? ctx->vcap * 8 : K1_VS_MAX_CAP;
+        retry = true;
+    }
     if (st & ST_REC_FULL) { ctx->rec_cap = R_main + R_main / 4 + 4096; retry = true; }
     if (st & ST_PART_FULL) { ctx->part_cap = Q + Q / 4 + 4096; retry = true; }
     if (retry) return 1;
@@ -465,7 +470,13 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     }
     /* ---- vocabulary ---- */
     ctx->V = V;
-    if ((uint64_t)V * 100 > cap * ctx->vload_pct) { ctx->vcap *= 4; return 1; } /* keep probes short */
+    /* keep probes short: the low load pays while the table is L2/MALL-sized (<= 16M slots,
+     * 256 MB of keys); past that every probe is an HBM access anyway, so up to 45 % */
+    if ((uint64_t)V * 100 > cap * (cap < VOCAB_LOW_LOAD_CAP ? ctx->vload_pct : 45u)) {
+        while ((uint64_t)V * 100 > ctx->vcap * (ctx->vcap < VOCAB_LOW_LOAD_CAP ? ctx->vload_pct : 45u)) ctx->vcap *= 4;
+        if (ctx->vcap > K1_VS_MAX_CAP && cap < K1_VS_MAX_CAP) ctx->vcap = K1_VS_MAX_CAP;
+        if (ctx->vcap != cap) return 1;
+    }
     ENSURE(ctx->vslot, (size_t)V * 4 + 4);
     ENSURE(ctx->skey0, (size_t)V * 16 + 16);
     ENSURE(ctx->skey1, (size_t)V * 16 + 16);
@@ -862,6 +873,17 @@ extern "C" int tfidf_fetch(tfidf_ctx* ctx, tfidf_result* r) {
 }
 
 /* ----------------------------------------------------------------- synthetic -- */
+
+/* ----------------------------------------------------------------- ingest ----
+ * ingest.cpp streams input/doc1..N into the context's host-input buffers (§8f row 2). */
+int tfidf_ctx_ingest_buffers(tfidf_ctx* ctx, uint64_t nbytes, uint32_t ndocs, uint8_t** dbytes, uint64_t** doff) {
+    HIPCHK(hipSetDevice(ctx->device));
+    ENSURE(ctx->in_bytes, nbytes + 64);
+    ENSURE(ctx->in_off, ((size_t)ndocs + 1) * 8);
+    *dbytes = ctx->in_bytes.as<uint8_t>();
+    *doff = ctx->in_off.as<uint64_t>();
+    return TFIDF_OK;
+}
 
 extern "C" int tfidf_synth_device(tfidf_ctx* ctx, uint64_t seed, uint32_t V, uint32_t mode, const double* cdf,
                                   const uint32_t* doc_ids, const uint64_t* ntok, uint32_t ndocs,

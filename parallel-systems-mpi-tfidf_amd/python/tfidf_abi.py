@@ -28,6 +28,7 @@ EXPORTS = [
     "tfidf_stage_name", "tfidf_set_timing", "tfidf_write_output", "tfidf_print_jobs",
     "tfidf_ingest_dir", "tfidf_free", "tfidf_synth_host", "tfidf_synth_device",
     "tfidf_format", "tfidf_copy_text", "tfidf_write_output_gpu", "tfidf_format_f64",
+    "tfidf_ingest_dir_device",
 ]
 
 
@@ -56,6 +57,13 @@ class RunInfo(C.Structure):
         ("nterms_global", C.c_uint32), ("nchunks", C.c_uint64), ("partial_records", C.c_uint64),
         ("ndocs", C.c_uint32), ("vocab_capacity", C.c_uint32), ("ms_total", C.c_double),
         ("ms_tokcount", C.c_double), ("ms_stage", C.c_double * 16), ("nstages", C.c_uint32), ("flags", C.c_uint32),
+    ]
+
+
+class IngestInfo(C.Structure):
+    _fields_ = [
+        ("nbytes", C.c_uint64), ("segments", C.c_uint64), ("ndocs", C.c_uint32), ("threads", C.c_uint32),
+        ("ms_scan", C.c_double), ("ms_read", C.c_double), ("ms_total", C.c_double),
     ]
 
 
@@ -90,6 +98,8 @@ def lib() -> C.CDLL:
                                        C.c_uint32, C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p]
         L.tfidf_synth_device.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p,
                                          C.c_void_p, C.c_uint32, C.c_uint64, C.POINTER(Corpus)]
+        L.tfidf_ingest_dir_device.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.POINTER(Corpus),
+                                              C.POINTER(C.c_uint32), C.POINTER(IngestInfo)]
         _lib = L
     return _lib
 
@@ -177,6 +187,29 @@ class Engine:
         _chk(lib().tfidf_synth_device(self.h, seed, V, mode, _ptr(cdf), _ptr(ids), _ptr(ntok), len(ntok),
                                       ndocs_total, C.byref(c)), "tfidf_synth_device")
         return c
+
+    def ingest_dir(self, path: str, threads: int = 0):
+        """input/doc1..N streamed into HBM (tfidf_ingest_dir_device).  Returns (Corpus, info);
+        raises TfidfError (rc -6 / -7, `bad_doc` attribute set for -7) like the reference."""
+        c, bad, ii = Corpus(), C.c_uint32(0), IngestInfo()
+        rc = lib().tfidf_ingest_dir_device(self.h, path.encode(), threads, C.byref(c), C.byref(bad), C.byref(ii))
+        if rc:
+            e = TfidfError(rc, "tfidf_ingest_dir_device")
+            e.bad_doc, e.ndocs = bad.value, c.ndocs
+            raise e
+        return c, {k: getattr(ii, k) for k, _ in IngestInfo._fields_}
+
+    def corpus_bytes(self, c: Corpus) -> np.ndarray:
+        """Device corpus bytes copied back to the host (test plumbing)."""
+        out = np.empty(c.nbytes, dtype=np.uint8)
+        hip = C.CDLL("libamdhip64.so.7")
+        hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        if c.nbytes and hip.hipMemcpy(out.ctypes.data, c.bytes, c.nbytes, 2) != 0:
+            raise RuntimeError("hipMemcpy D2H failed")
+        off = np.empty(c.ndocs + 1, dtype=np.uint64)
+        if hip.hipMemcpy(off.ctypes.data, c.doc_off, off.nbytes, 2) != 0:
+            raise RuntimeError("hipMemcpy D2H failed")
+        return out, off
 
     def info(self) -> dict:
         r = RunInfo()

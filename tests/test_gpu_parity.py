@@ -182,11 +182,14 @@ def test_cli_error_contract():
         assert p.returncode == 0 and p.stdout.startswith(b"Error Opening File: input/doc1")
 
 
-def test_full_c2_properties():
-    """Config 2 at full size (1e5 docs, ~1 GB, device-generated): size-independent
-    properties — sum of counts = tokens, per-document sums = docSize, DF = pairs per term,
-    strict output order, scores recomputed (<= 1e-12 relative)."""
-    p = tfidf_configs.plan("c2")
+@pytest.mark.parametrize("cfg", ["c2", "c4", "c5"])
+def test_full_config_properties(cfg):
+    """BASELINE configs at full size, device-generated: c2 (1e5 docs, ~1 GB), c4 (V = 1e7:
+    ~1e7 distinct terms, vocabulary-table growth, radix-sorted vocabulary), c5 (four 100 MB
+    documents among 1e6 ~600 B ones).  Size-independent properties — sum of counts =
+    tokens, per-document sums = docSize, DF = pairs per term, strict output order, scores
+    recomputed (<= 1e-12 relative)."""
+    p = tfidf_configs.plan(cfg)
     with tfidf_abi.Engine(0) as e:
         c = e.synth_device(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"], p["ndocs_total"])
         e.run_corpus(c)
