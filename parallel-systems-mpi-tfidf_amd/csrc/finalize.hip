@@ -162,22 +162,37 @@ int launch_part_heads(const uint64_t* keys, uint64_t n, uint32_t* head, hipStrea
     return ok();
 }
 
+/* One merged record per (doc, rank) run of the sorted partial records.  Runs can be
+ * thousands of records long (a term of a 100 MB document appears in each of its ~6000
+ * chunks), so the counts are not summed by the run's head thread: every record adds its
+ * count after a wave-level segmented reduction (runs are contiguous, so lanes of one run
+ * are adjacent), one device atomic per run and wave into the zeroed rec_cnt. */
 __global__ void k_part_merge(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ seq,
                              const uint32_t* __restrict__ pcnt, const uint32_t* __restrict__ head_pos, uint64_t n,
                              const uint32_t* __restrict__ slot_of_rank, uint64_t rec_base,
                              uint32_t* __restrict__ rec_slot, uint32_t* __restrict__ rec_cnt,
                              uint64_t* __restrict__ doc_recoff, uint8_t* __restrict__ doc_flags) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    uint64_t k = keys[i];
-    if (i > 0 && keys[i - 1] == k) return;
-    uint32_t sum = 0;
-    for (uint64_t j = i; j < n && keys[j] == k; ++j) sum += pcnt[seq[j]];
-    uint64_t u = rec_base + head_pos[i];
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const bool val = i < n;
+    const uint64_t k = val ? keys[i] : ~0ull;
+    const uint64_t kp = (val && i > 0) ? keys[i - 1] : ~0ull;
+    const bool head = val && (i == 0 || kp != k);
+    const uint64_t u = val ? rec_base + head_pos[i] - (head ? 0u : 1u) : ~0ull;
+    uint32_t v = val ? pcnt[seq[i]] : 0u;
+    /* suffix sums within the run: after the step with offset o, v = sum over [lane, lane + 2o) of the run */
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t vo = __shfl_down(v, o);
+        const uint64_t uo = __shfl_down(u, o);
+        if (lane + o < 64 && uo == u) v += vo;
+    }
+    const uint64_t up = __shfl_up(u, 1);
+    if (val && (lane == 0 || up != u)) atomicAdd(&rec_cnt[u], v);
+    if (!head) return;
     rec_slot[u] = slot_of_rank[(uint32_t)k];
-    rec_cnt[u] = sum;
     uint32_t d = (uint32_t)(k >> 32);
-    if (i == 0 || (uint32_t)(keys[i - 1] >> 32) != d) {
+    if (i == 0 || (uint32_t)(kp >> 32) != d) {
         doc_recoff[d] = u;
         doc_flags[d] = DF_PARTIAL | DF_PRESORTED;
     }
@@ -199,6 +214,8 @@ int launch_part_merge(const uint64_t* keys, const uint32_t* seq, const uint32_t*
                       uint32_t* rec_cnt, uint64_t* doc_recoff, uint32_t* doc_npairs, uint8_t* doc_flags,
                       hipStream_t s) {
     if (!n) return 0;
+    /* merged counts accumulate atomically: zero the (at most n) merged record slots */
+    if (hipMemsetAsync(rec_cnt + rec_base, 0, n * 4, s) != hipSuccess) return -1;
     k_part_merge<<<grid_for(n), NT, 0, s>>>(keys, seq, part_cnt, head_pos, n, slot_of_rank, rec_base, rec_slot,
                                            rec_cnt, doc_recoff, doc_flags);
     k_part_npairs<<<grid_for(n), NT, 0, s>>>(keys, head_pos, n, rec_base, doc_recoff, doc_npairs);
