@@ -120,6 +120,7 @@ struct tfidf_ctx {
     const uint32_t* order = nullptr;
     /* last run */
     bool have_result = false;
+    bool have_info = false;   /* run counters/timings valid (also after an ablation run) */
     tfidf_corpus corpus{};
     const uint8_t* dev_bytes = nullptr;
     const uint32_t* dev_ids = nullptr;
@@ -692,6 +693,7 @@ extern "C" int tfidf_run(tfidf_ctx* ctx, const tfidf_corpus* in) {
     const uint64_t Nt = in->ndocs_total ? in->ndocs_total : N;
     if (Nt < N || Nt > 0xFFFFFFFFull) return TFIDF_E_INVAL;
     ctx->have_result = false;
+    ctx->have_info = false;
     ctx->text_valid = false;
     int rc = 1;
     for (int attempt = 0; attempt < 8 && rc == 1; ++attempt) {
@@ -707,7 +709,9 @@ extern "C" int tfidf_run(tfidf_ctx* ctx, const tfidf_corpus* in) {
     ctx->dev_ids = dev_ids;
     ctx->ndocs = N;
     ctx->ndocs_total = Nt;
-    ctx->have_result = true;
+    /* an ablation run (timing experiment) leaves no valid result: fetch/format refuse it */
+    ctx->have_result = ctx->ablate == 0;
+    ctx->have_info = true;
     if (ctx->timing) {
         for (int i = 0; i < S_NSTAGES; ++i) {
             float ms = 0;
@@ -731,7 +735,7 @@ extern "C" int tfidf_debug_k1_stamps(tfidf_ctx* ctx, uint64_t* out, int n) {
 
 extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info) {
     if (!ctx || !info) return TFIDF_E_INVAL;
-    if (!ctx->have_result) return TFIDF_E_STATE;
+    if (!ctx->have_info) return TFIDF_E_STATE;
     memset(info, 0, sizeof(*info));
     info->nbytes = ctx->corpus.ndocs ? 0 : 0;
     {

@@ -1,11 +1,12 @@
 #!/bin/bash
 # rocprofv3 kernel-trace summary of a short bench run (GPU box):
-#   bash scripts/kstats.sh <tag>   -> gpurun_out/ks_<tag>/..., table on stdout
+#   bash scripts/kstats.sh <tag> [bench args]   -> gpurun_out/ks_<tag>/..., table on stdout
 cd /tmp && export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-/root/repo}
 T=${1:-ks}
+shift
 timeout -s KILL 180 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/ks_$T -o ks -- \
-    python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $R/gpurun_out/ks_$T.log 2>&1 || exit 1
+    python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > $R/gpurun_out/ks_$T.log 2>&1 || exit 1
 f=$(find $R/gpurun_out/ks_$T -name "*kernel_stats.csv" | head -1)
 python3 - "$f" <<'PY'
 import csv, sys
