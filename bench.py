@@ -14,7 +14,9 @@ N x 1e5 documents (contiguous "docN" strcmp ranges; idf uses the global N).
 Rank 0 prints one JSON line.  `roofline` is priced on the dominant kernel (K1
 tokenize+count), algorithmic bytes per launch = C + 12*P, divided by K1's
 average duration measured with HIP events on the engine's stream inside the timed steps.
-`cpu_baseline` times the oracle restatement on the host cores (one thread per document
+`roofline.measured_read_peak` / `measured_copy_peak` are this device's streaming read and
+copy rates (tfidf_hbm_probe, 2 GiB, outside the timed region).
+`cpu_baseline` (N = 1 only) times the oracle restatement on the host cores (one thread per document
 shard, OMP_NUM_THREADS = 16 threads on the GPU box) on a bounded sample, with a
 single-thread leg alongside.
 """
@@ -115,6 +117,7 @@ def main():
     ap.add_argument("--cpu-sample-docs", type=int, default=48000)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: OMP_NUM_THREADS (16 on the GPU box), at most 16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-probe", action="store_true", help="skip the measured HBM read/copy peak probe")
     ap.add_argument("--no-emit", action="store_true", help="skip the (untimed) output-emission measurement")
     ap.add_argument("--vocab", type=int, default=0, help="diagnostics only: override the config's vocabulary size")
     args = ap.parse_args()
@@ -189,6 +192,9 @@ def main():
     else:
         C_all, P_all, T_all = float(C_bytes), float(P_pairs), float(T_tok)
 
+    # measured streaming peaks, outside the timed region, rank 0 only
+    probe = eng.hbm_probe(2 << 30, 10) if (rank == 0 and not args.no_probe) else None
+
     if rank == 0:
         ms_step = elapsed / args.steps * 1e3
         k1_avg_ms = float(np.mean(k1_ms))
@@ -221,11 +227,14 @@ def main():
             "roofline": {"bound": "hbm", "kernel": "k_tokcount_vs (K1)", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "alg_bytes_per_launch": int(alg_bytes),
-                         "k1_avg_ms": round(k1_avg_ms, 4)},
+                         "k1_avg_ms": round(k1_avg_ms, 4),
+                         "measured_read_peak": round(probe["read_GBps"], 1) if probe else None,
+                         "measured_copy_peak": round(probe["copy_GBps"], 1) if probe else None,
+                         "frac_of_measured_read": round(achieved / probe["read_GBps"], 4) if probe else None},
             "cpu_baseline": None,
             "emit": emit,
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
             thr = args.cpu_threads or min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count() or 1)
             line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_sample_docs, max(1, min(16, thr)))
         print(json.dumps(line), flush=True)

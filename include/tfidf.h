@@ -138,6 +138,11 @@ int tfidf_set_timing(tfidf_ctx* ctx, int enable);
  * tfidf_open.  Returns the number of values written (phases + workgroup count). */
 int tfidf_debug_k1_stamps(tfidf_ctx* ctx, uint64_t* out, int n);
 
+/* Diagnostics: measured HBM streaming peaks on this device (SURVEY §8d's "fraction of a
+ * measured copy-kernel peak"): GB/s of a read-only stream over nbytes and of an nbytes
+ * copy (2 x nbytes moved), each averaged over `iters` passes after a warm-up. */
+int tfidf_hbm_probe(tfidf_ctx* ctx, uint64_t nbytes, int iters, double* read_gbps, double* copy_gbps);
+
 /* ---------------------------------------------------------------- emission -- */
 
 /* GPU emission (the default output path): formats the last run's lines

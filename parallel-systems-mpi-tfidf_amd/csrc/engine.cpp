@@ -733,6 +733,52 @@ extern "C" int tfidf_debug_k1_stamps(tfidf_ctx* ctx, uint64_t* out, int n) {
     return m;
 }
 
+/* Measured HBM streaming peaks: `iters` timed passes of a read-only stream
+ * over nbytes and of an nbytes copy (counted as 2 x nbytes), after one warm-up pass each;
+ * the buffers are allocated for the call and released. */
+extern "C" int tfidf_hbm_probe(tfidf_ctx* ctx, uint64_t nbytes, int iters, double* read_gbps, double* copy_gbps) {
+    if (!ctx || !read_gbps || !copy_gbps || nbytes < 4096 || iters <= 0) return TFIDF_E_INVAL;
+    HIPCHK(hipSetDevice(ctx->device));
+    nbytes &= ~(uint64_t)4095;
+    hipStream_t s = ctx->stream;
+    void *a = nullptr, *b = nullptr;
+    uint32_t* sink = nullptr;
+    if (hipMalloc(&a, nbytes) != hipSuccess) return TFIDF_E_NOMEM;
+    if (hipMalloc(&b, nbytes) != hipSuccess) { (void)hipFree(a); return TFIDF_E_NOMEM; }
+    if (hipMalloc((void**)&sink, 256) != hipSuccess) { (void)hipFree(a); (void)hipFree(b); return TFIDF_E_NOMEM; }
+    int ncu = 256, dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const unsigned grid = (unsigned)(ncu > 0 ? ncu : 256) * 16u;
+    hipEvent_t e0, e1;
+    int rc = TFIDF_OK;
+    float ms_r = 0.f, ms_c = 0.f;
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) rc = TFIDF_E_HIP;
+    if (!rc && (hipMemsetAsync(a, 0, nbytes, s) != hipSuccess || hipMemsetAsync(b, 0, nbytes, s) != hipSuccess)) rc = TFIDF_E_HIP;
+    if (!rc && (launch_stream_read(a, nbytes, sink, grid, s) || launch_stream_copy(a, b, nbytes, grid, s))) rc = TFIDF_E_HIP;
+    if (!rc) {
+        bool ok = hipEventRecord(e0, s) == hipSuccess;
+        for (int i = 0; ok && i < iters; ++i) ok = launch_stream_read(a, nbytes, sink, grid, s) == 0;
+        ok = ok && hipEventRecord(e1, s) == hipSuccess && hipEventSynchronize(e1) == hipSuccess &&
+             hipEventElapsedTime(&ms_r, e0, e1) == hipSuccess;
+        ok = ok && hipEventRecord(e0, s) == hipSuccess;
+        for (int i = 0; ok && i < iters; ++i) ok = launch_stream_copy(a, b, nbytes, grid, s) == 0;
+        ok = ok && hipEventRecord(e1, s) == hipSuccess && hipEventSynchronize(e1) == hipSuccess &&
+             hipEventElapsedTime(&ms_c, e0, e1) == hipSuccess;
+        if (!ok) rc = TFIDF_E_HIP;
+    }
+    if (!rc) {
+        *read_gbps = ms_r > 0 ? (double)nbytes * iters / (ms_r * 1e-3) / 1e9 : 0.0;
+        *copy_gbps = ms_c > 0 ? 2.0 * (double)nbytes * iters / (ms_c * 1e-3) / 1e9 : 0.0;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(a);
+    (void)hipFree(b);
+    (void)hipFree(sink);
+    return rc;
+}
+
 extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info) {
     if (!ctx || !info) return TFIDF_E_INVAL;
     if (!ctx->have_info) return TFIDF_E_STATE;

@@ -49,4 +49,8 @@ int tile_sort_u128(const uint4* k0, const uint32_t* v0, uint4* k1, uint32_t* v1,
 int key_varying_bytes_u64(const uint64_t* k, uint64_t n, uint32_t* mask, Arena& ar, hipStream_t s);
 int key_varying_bytes_u128(const uint4* k, uint64_t n, uint32_t* mask, Arena& ar, hipStream_t s);
 
+/* HBM probes (diagnostics for the roofline's measured peak) */
+int launch_stream_read(const void* p, uint64_t nbytes, uint32_t* sink, unsigned grid, hipStream_t s);
+int launch_stream_copy(const void* src, void* dst, uint64_t nbytes, unsigned grid, hipStream_t s);
+
 #endif

@@ -475,3 +475,41 @@ int key_varying_bytes_u128(const uint4* k, uint64_t n, uint32_t* mask, Arena& ar
     if (n == 0) { *mask = 0; return 0; }
     return varying_common(2, k, n, mask, ar, s);
 }
+
+/* ------------------------------------------------------------ HBM probes --
+ * Measured streaming peaks for the roofline ("also report the fraction of a
+ * measured copy-kernel peak"): a read-only stream (16-byte non-temporal loads, 4 in
+ * flight per lane, XOR-folded so nothing is elided) and a copy.  Diagnostics only. */
+typedef unsigned int probe_u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_stream_read(const probe_u32x4* __restrict__ p, uint64_t n16,
+                                                     uint32_t* __restrict__ sink) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    probe_u32x4 acc = {0u, 0u, 0u, 0u};
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        const probe_u32x4 a = __builtin_nontemporal_load(p + i), b = __builtin_nontemporal_load(p + i + stride);
+        const probe_u32x4 c = __builtin_nontemporal_load(p + i + 2 * stride), d = __builtin_nontemporal_load(p + i + 3 * stride);
+        acc ^= a ^ b ^ c ^ d;
+    }
+    for (; i < n16; i += stride) acc ^= __builtin_nontemporal_load(p + i);
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9E3779B9u) sink[0] = 1u;   /* never for the probe's zero fill */
+}
+__global__ __launch_bounds__(256) void k_stream_copy(const probe_u32x4* __restrict__ src, probe_u32x4* __restrict__ dst,
+                                                     uint64_t n16) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + stride < n16; i += 2 * stride) {
+        const probe_u32x4 a = __builtin_nontemporal_load(src + i), b = __builtin_nontemporal_load(src + i + stride);
+        __builtin_nontemporal_store(a, dst + i);
+        __builtin_nontemporal_store(b, dst + i + stride);
+    }
+    for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+int launch_stream_read(const void* p, uint64_t nbytes, uint32_t* sink, unsigned grid, hipStream_t s) {
+    k_stream_read<<<grid, 256, 0, s>>>((const probe_u32x4*)p, nbytes / 16, sink);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_stream_copy(const void* src, void* dst, uint64_t nbytes, unsigned grid, hipStream_t s) {
+    k_stream_copy<<<grid, 256, 0, s>>>((const probe_u32x4*)src, (probe_u32x4*)dst, nbytes / 16);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

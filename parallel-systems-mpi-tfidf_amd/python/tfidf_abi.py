@@ -28,7 +28,7 @@ EXPORTS = [
     "tfidf_stage_name", "tfidf_set_timing", "tfidf_write_output", "tfidf_print_jobs",
     "tfidf_ingest_dir", "tfidf_free", "tfidf_synth_host", "tfidf_synth_device",
     "tfidf_format", "tfidf_copy_text", "tfidf_write_output_gpu", "tfidf_format_f64",
-    "tfidf_ingest_dir_device",
+    "tfidf_ingest_dir_device", "tfidf_hbm_probe",
 ]
 
 
@@ -100,6 +100,7 @@ def lib() -> C.CDLL:
                                          C.c_void_p, C.c_uint32, C.c_uint64, C.POINTER(Corpus)]
         L.tfidf_ingest_dir_device.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.POINTER(Corpus),
                                               C.POINTER(C.c_uint32), C.POINTER(IngestInfo)]
+        L.tfidf_hbm_probe.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
         _lib = L
     return _lib
 
@@ -198,6 +199,12 @@ class Engine:
             e.bad_doc, e.ndocs = bad.value, c.ndocs
             raise e
         return c, {k: getattr(ii, k) for k, _ in IngestInfo._fields_}
+
+    def hbm_probe(self, nbytes: int = 2 << 30, iters: int = 10) -> dict:
+        """Measured streaming read / copy GB/s of this device (tfidf_hbm_probe)."""
+        r, c = C.c_double(0), C.c_double(0)
+        _chk(lib().tfidf_hbm_probe(self.h, nbytes, iters, C.byref(r), C.byref(c)), "tfidf_hbm_probe")
+        return {"read_GBps": r.value, "copy_GBps": c.value}
 
     def corpus_bytes(self, c: Corpus) -> np.ndarray:
         """Device corpus bytes copied back to the host (test plumbing)."""
