@@ -107,6 +107,7 @@ struct tfidf_ctx {
     DevBuf counters;
     DevBuf dense, vslot, skey0, skey1, seq0, seq1, rank_of_slot, slot_of_rank, rank16;
     DevBuf pkey0, pkey1, pseq0, pseq1, phead;
+    DevBuf big_list, big_idx, dense_cnt, kcnt, tile_cnt;   /* dense merge of long documents */
     DevBuf df_local, df_global, present, idf_vals;
     DevBuf dkey0, dkey1, dseq0, dseq1, npairs_ord, out_off, doc_meta;
     DevBuf out_term, out_cnt, out_score, idf_rank, large_list;
@@ -242,7 +243,8 @@ void tfidf_close(tfidf_ctx* ctx) {
                       &ctx->doc_toff, &ctx->text, &ctx->out_term, &ctx->out_cnt,
                       &ctx->out_score, &ctx->idf_rank, &ctx->large_list, &ctx->x_mine, &ctx->x_send, &ctx->x_recv,
                       &ctx->x_recv2, &ctx->x_seq0, &ctx->x_seq1, &ctx->x_head, &ctx->x_grank, &ctx->x_dfv,
-                      &ctx->x_cnt, &ctx->stamps};
+                      &ctx->x_cnt, &ctx->stamps, &ctx->big_list, &ctx->big_idx, &ctx->dense_cnt, &ctx->kcnt,
+                      &ctx->tile_cnt};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i <= S_NSTAGES; ++i) (void)hipEventDestroy(ctx->ev[i]);
     (void)hipStreamDestroy(ctx->stream);
@@ -362,7 +364,10 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     HIPCHK(hipMemsetAsync(ctx->doc_npairs.p, 0, (size_t)N * 4 + 4, s));
     HIPCHK(hipMemsetAsync(ctx->doc_size.p, 0, (size_t)N * 4 + 4, s));
     HIPCHK(hipMemsetAsync(ctx->doc_flags.p, 0, (size_t)N + 1, s));
-    if (nchunks) LCHK(launch_plan_chunks(c, nchunks, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), s));
+    ENSURE(ctx->big_list, (size_t)BIG_LIST_CAP * 4);
+    if (nchunks)
+        LCHK(launch_plan_chunks(c, nchunks, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(),
+                                ctx->big_list.as<uint32_t>(), cnt + 6, s));
     /* K1 variant: the slot-keyed kernel (tokcount_vs.hip) needs a 16-byte aligned corpus
      * base; TFIDF_K1=general / =ws select the older kernels (cross-checks, diagnostics) */
     uint32_t not_ws_sep = 1;
@@ -424,11 +429,11 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     LCHK(launch_vocab_flags(vd, cap, ctx->dense.as<uint32_t>(), s));
     LCHK(scan_excl_u32(ctx->dense.as<uint32_t>(), ctx->dense.as<uint32_t>(), cap, ar, s));
     uint32_t V = 0;
-    unsigned long long hc[4];
+    unsigned long long hc[8];
     HIPCHK(hipMemcpyAsync(hc, cnt, sizeof hc, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(&V, ctx->dense.as<uint32_t>() + cap, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    const uint64_t R_main = hc[0], Q = hc[1];
+    const uint64_t R_main = hc[0], Q = hc[1], nbig = hc[6];
     const uint32_t st = (uint32_t)hc[3];
     ctx->ntokens = hc[2];
     ctx->nchunks = nchunks;
@@ -508,51 +513,96 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     /* ---- partial documents ---- */
     mark(ctx, S_MERGE);
     uint64_t R_total = R_main;
+    const uint32_t* merged_count = nullptr;   /* device: merged + dense records beyond R_main */
     if (Q) {
         ENSURE(ctx->pkey0, Q * 8);
         ENSURE(ctx->pkey1, Q * 8);
         ENSURE(ctx->pseq0, Q * 4);
         ENSURE(ctx->pseq1, Q * 4);
         ENSURE(ctx->phead, (Q + 1) * 4);
-        LCHK(launch_part_keys(ctx->part_doc.as<uint32_t>(), ctx->part_slot.as<uint32_t>(), ctx->rank_of_slot.as<uint32_t>(),
-                              Q, ctx->pkey0.as<uint64_t>(), ctx->pseq0.as<uint32_t>(), s));
-        uint32_t pm = 0;
-        /* key = (local doc << 32) | rank: the varying bytes follow from N and V (no probe,
-         * no host sync) */
-        {
-            const uint32_t rb = V > 1 ? 32u - (uint32_t)__builtin_clz(V - 1) : 1u;
-            const uint32_t db = N > 1 ? 32u - (uint32_t)__builtin_clz(N - 1) : 1u;
-            for (uint32_t b = 0; b < (rb + 7) / 8; ++b) pm |= 1u << b;
-            for (uint32_t b = 0; b < (db + 7) / 8; ++b) pm |= 1u << (4 + b);
-        }
-        int pc = radix_sort_u64(ctx->pkey0.as<uint64_t>(), ctx->pseq0.as<uint32_t>(), ctx->pkey1.as<uint64_t>(),
-                                ctx->pseq1.as<uint32_t>(), Q, pm, ar, s);
-        LCHK(pc);
-        uint64_t* pk = pc ? ctx->pkey1.as<uint64_t>() : ctx->pkey0.as<uint64_t>();
-        uint32_t* ps = pc ? ctx->pseq1.as<uint32_t>() : ctx->pseq0.as<uint32_t>();
-        uint32_t* ph = ctx->phead.as<uint32_t>();
-        LCHK(launch_part_heads(pk, Q, ph, s));
-        LCHK(scan_excl_u32(ph, ph, Q, ar, s));
-        /* U = ph[Q] merged records (<= Q) stays on the device: no host round trip; the
-         * record arrays are sized for the worst case R_main + Q */
+        /* merged (and dense) records land in [R_main, R_main + Q): size for the worst case */
         if (R_main + Q > ctx->rec_cap) {
             uint64_t ncap = R_main + Q + (R_main + Q) / 8 + 4096;
             if (ctx->rec_slot.grow_keep(ncap * 4, R_main * 4, s) || ctx->rec_cnt.grow_keep(ncap * 4, R_main * 4, s))
                 return TFIDF_E_NOMEM;
             ctx->rec_cap = ncap;
         }
-        LCHK(launch_part_merge(pk, ps, ctx->part_cnt.as<uint32_t>(), ph, Q, ctx->slot_of_rank.as<uint32_t>(), R_main,
-                               ctx->rec_slot.as<uint32_t>(), ctx->rec_cnt.as<uint32_t>(),
-                               ctx->doc_recoff.as<uint64_t>(), ctx->doc_npairs.as<uint32_t>(),
-                               ctx->doc_flags.as<uint8_t>(), s));
-        R_total = R_main + Q; /* an upper bound: the true count is R_main + ph[Q] */
+        /* documents longer than DENSE_DOC (listed by K0): their partial records are summed
+         * in dense per-document arrays over ranks (<= 256 MB of them) instead of sorted */
+        uint32_t nb = 0;
+        if (nbig && V) {
+            const uint64_t lim = (256ull << 20) / (4ull * V * DENSE_REP);
+            uint64_t m = nbig < (uint64_t)BIG_LIST_CAP ? nbig : (uint64_t)BIG_LIST_CAP;
+            nb = (uint32_t)(m < lim ? m : lim);
+        }
+        uint64_t Qs = Q;                                  /* records to sort */
+        const uint32_t* scnt = ctx->part_cnt.as<uint32_t>();
+        if (nb) {
+            ENSURE(ctx->big_idx, (size_t)N * 4 + 4);
+            ENSURE(ctx->dense_cnt, (size_t)nb * V * 4 * DENSE_REP);
+            ENSURE(ctx->kcnt, Q * 4);
+            uint32_t* nkeep = (uint32_t*)(cnt + 7);   /* zeroed with the run's counters */
+            HIPCHK(hipMemsetAsync(ctx->big_idx.p, 0xFF, (size_t)N * 4 + 4, s));
+            HIPCHK(hipMemsetAsync(ctx->dense_cnt.p, 0, (size_t)nb * V * 4 * DENSE_REP, s));
+            LCHK(launch_set_big_idx(ctx->big_list.as<uint32_t>(), nb, ctx->big_idx.as<uint32_t>(), s));
+            LCHK(launch_part_dense(ctx->part_doc.as<uint32_t>(), ctx->part_slot.as<uint32_t>(), ctx->part_cnt.as<uint32_t>(),
+                                   Q, ctx->big_idx.as<uint32_t>(), ctx->rank_of_slot.as<uint32_t>(), V,
+                                   ctx->dense_cnt.as<uint32_t>(), ctx->pkey0.as<uint64_t>(), ctx->pseq0.as<uint32_t>(),
+                                   ctx->kcnt.as<uint32_t>(), nkeep, s));
+            uint32_t qk = 0;   /* the sort needs its size on the host: one round trip, dense runs only */
+            HIPCHK(hipMemcpyAsync(&qk, nkeep, 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            Qs = qk;
+            scnt = ctx->kcnt.as<uint32_t>();
+        } else {
+            LCHK(launch_part_keys(ctx->part_doc.as<uint32_t>(), ctx->part_slot.as<uint32_t>(),
+                                  ctx->rank_of_slot.as<uint32_t>(), Q, ctx->pkey0.as<uint64_t>(),
+                                  ctx->pseq0.as<uint32_t>(), s));
+        }
+        uint32_t* ph = ctx->phead.as<uint32_t>();
+        if (Qs) {
+            uint32_t pm = 0;
+            /* key = (local doc << 32) | rank: the varying bytes follow from N and V (no probe,
+             * no host sync) */
+            {
+                const uint32_t rb = V > 1 ? 32u - (uint32_t)__builtin_clz(V - 1) : 1u;
+                const uint32_t db = N > 1 ? 32u - (uint32_t)__builtin_clz(N - 1) : 1u;
+                for (uint32_t b = 0; b < (rb + 7) / 8; ++b) pm |= 1u << b;
+                for (uint32_t b = 0; b < (db + 7) / 8; ++b) pm |= 1u << (4 + b);
+            }
+            int pc = radix_sort_u64(ctx->pkey0.as<uint64_t>(), ctx->pseq0.as<uint32_t>(), ctx->pkey1.as<uint64_t>(),
+                                    ctx->pseq1.as<uint32_t>(), Qs, pm, ar, s);
+            LCHK(pc);
+            uint64_t* pk = pc ? ctx->pkey1.as<uint64_t>() : ctx->pkey0.as<uint64_t>();
+            uint32_t* ps = pc ? ctx->pseq1.as<uint32_t>() : ctx->pseq0.as<uint32_t>();
+            LCHK(launch_part_heads(pk, Qs, ph, s));
+            LCHK(scan_excl_u32(ph, ph, Qs, ar, s));
+            /* U = ph[Qs] merged records (<= Qs) stays on the device: no host round trip */
+            LCHK(launch_part_merge(pk, ps, scnt, ph, Qs, ctx->slot_of_rank.as<uint32_t>(), R_main,
+                                   ctx->rec_slot.as<uint32_t>(), ctx->rec_cnt.as<uint32_t>(),
+                                   ctx->doc_recoff.as<uint64_t>(), ctx->doc_npairs.as<uint32_t>(),
+                                   ctx->doc_flags.as<uint8_t>(), s));
+        } else {
+            HIPCHK(hipMemsetAsync(ph, 0, 4, s));
+        }
+        if (nb) {
+            const uint64_t nt = ((uint64_t)V + 1023) / 1024;
+            ENSURE(ctx->tile_cnt, (nt * nb + 1) * 4);
+            LCHK(launch_dense_emit(ctx->dense_cnt.as<uint32_t>(), nb, V, ctx->big_list.as<uint32_t>(),
+                                   ctx->slot_of_rank.as<uint32_t>(), R_main, ph + Qs, ctx->tile_cnt.as<uint32_t>(),
+                                   ctx->rec_slot.as<uint32_t>(), ctx->rec_cnt.as<uint32_t>(),
+                                   ctx->doc_recoff.as<uint64_t>(), ctx->doc_npairs.as<uint32_t>(),
+                                   ctx->doc_flags.as<uint8_t>(), ar, s));
+        }
+        merged_count = ph + Qs;
+        R_total = R_main + Q; /* an upper bound: the true count is R_main + *merged_count */
     }
     /* ---- DF ---- */
     mark(ctx, S_DF);
     ENSURE(ctx->df_local, (size_t)V * 4 + 4);
     ENSURE(ctx->df_global, (size_t)V * 4 + 4);
     /* also rewrites every record's slot as its term rank (K5 then needs no rank gather) */
-    LCHK(launch_df_hist(ctx->rec_slot.as<uint32_t>(), R_main, Q ? ctx->phead.as<uint32_t>() + Q : nullptr, R_total,
+    LCHK(launch_df_hist(ctx->rec_slot.as<uint32_t>(), R_main, merged_count, R_total,
                         ctx->rank_of_slot.as<uint32_t>(),
                         V <= 65536u ? ctx->rank16.as<uint16_t>() : nullptr, V, cap,
                         (uint32_t*)(cnt + 3), ctx->df_local.as<uint32_t>(), ar, s));

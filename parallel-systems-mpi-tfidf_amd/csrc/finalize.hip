@@ -222,6 +222,133 @@ int launch_part_merge(const uint64_t* keys, const uint32_t* seq, const uint32_t*
     return ok();
 }
 
+/* ------------------------------------------------ dense merge (long documents) --
+ * A document of many chunks (longer than DENSE_DOC, listed by K0) leaves one partial
+ * record per (chunk, term): c5's four 100 MB documents give 23 M of them.  Instead of
+ * radix-sorting those, they are summed into a dense per-document count array over term
+ * ranks (u32[nb][V], L2/MALL-resident at V = 5e4), and only the other partial records
+ * are sorted and merged; the dense arrays are then emitted in rank order — the same
+ * presorted runs the merge writes. */
+__global__ void k_set_big_idx(const uint32_t* __restrict__ big_list, uint32_t nb, uint32_t* __restrict__ big_idx) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < nb) big_idx[big_list[b]] = b;
+}
+int launch_set_big_idx(const uint32_t* big_list, uint32_t nb, uint32_t* big_idx, hipStream_t s) {
+    if (!nb) return 0;
+    k_set_big_idx<<<grid_for(nb), NT, 0, s>>>(big_list, nb, big_idx);
+    return ok();
+}
+
+/* Records of listed documents are added into their dense array; the others are written
+ * straight out as sort keys (order is irrelevant: they are sorted next), positions by a
+ * wave-aggregated atomic on *nkeep. */
+__global__ void k_part_dense(const uint32_t* __restrict__ pdoc, const uint32_t* __restrict__ pslot,
+                             const uint32_t* __restrict__ pcnt, uint64_t q, const uint32_t* __restrict__ big_idx,
+                             const uint32_t* __restrict__ rank_of_slot, uint32_t V, uint32_t* __restrict__ dense,
+                             uint64_t* __restrict__ keys, uint32_t* __restrict__ seq, uint32_t* __restrict__ cnt_out,
+                             uint32_t* __restrict__ nkeep) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool val = i < q;
+    const uint32_t d = val ? pdoc[i] : 0u;
+    const uint32_t b = val ? big_idx[d] : 0u;
+    const uint32_t r = val ? rank_of_slot[pslot[i]] : 0u;
+    const uint32_t c = val ? pcnt[i] : 0u;
+    const bool kept = val && b == 0xFFFFFFFFu;
+    /* DENSE_REP copies per document, picked by workgroup: a hot term's adds (one per chunk
+     * of the document, ~6000) spread over the copies instead of queueing on one address */
+    if (val && !kept && r < V) atomicAdd(&dense[((uint64_t)b * DENSE_REP + (blockIdx.x & (DENSE_REP - 1))) * V + r], c);
+    const uint64_t km = __ballot(kept);
+    if (!km) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t leader = (uint32_t)__builtin_ctzll(km);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(nkeep, (uint32_t)__popcll(km));
+    base = (uint32_t)__shfl(base, (int)leader);
+    if (kept) {
+        const uint32_t p = base + (uint32_t)__popcll(km & ((1ull << lane) - 1ull));
+        keys[p] = ((uint64_t)d << 32) | r;
+        seq[p] = p;
+        cnt_out[p] = c;
+    }
+}
+int launch_part_dense(const uint32_t* part_doc, const uint32_t* part_slot, const uint32_t* part_cnt, uint64_t q,
+                      const uint32_t* big_idx, const uint32_t* rank_of_slot, uint32_t V, uint32_t* dense,
+                      uint64_t* keys, uint32_t* seq, uint32_t* cnt_out, uint32_t* nkeep, hipStream_t s) {
+    if (!q) return 0;
+    k_part_dense<<<grid_for(q), NT, 0, s>>>(part_doc, part_slot, part_cnt, q, big_idx, rank_of_slot, V, dense, keys,
+                                           seq, cnt_out, nkeep);
+    return ok();
+}
+
+constexpr uint32_t DENSE_TILE = 4 * NT;   /* ranks per emission tile: 4 per thread */
+__device__ __forceinline__ uint32_t dense_sum(const uint32_t* __restrict__ dense, uint32_t b, uint32_t V, uint32_t r) {
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < DENSE_REP; ++k) v += dense[((uint64_t)b * DENSE_REP + k) * V + r];
+    return v;
+}
+__global__ void k_dense_count(const uint32_t* __restrict__ dense, uint32_t V, uint32_t nt,
+                              uint32_t* __restrict__ tile_cnt) {
+    __shared__ uint32_t wsum[NT / 64];
+    const uint32_t t = blockIdx.x, b = blockIdx.y;
+    const uint32_t r0 = t * DENSE_TILE + threadIdx.x * 4;
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c += (r0 + k < V && dense_sum(dense, b, V, r0 + k) != 0u) ? 1u : 0u;
+    uint32_t tot;
+    (void)block_excl_scan<NT, false>(c, wsum, &tot);
+    if (threadIdx.x == 0) tile_cnt[(uint64_t)b * nt + t] = tot;
+}
+__global__ void k_dense_write(const uint32_t* __restrict__ dense, uint32_t V, uint32_t nt,
+                              const uint32_t* __restrict__ big_list, const uint32_t* __restrict__ slot_of_rank,
+                              uint64_t rec_base, const uint32_t* __restrict__ merged_count,
+                              const uint32_t* __restrict__ tile_off, uint32_t* __restrict__ rec_slot,
+                              uint32_t* __restrict__ rec_cnt, uint64_t* __restrict__ doc_recoff,
+                              uint32_t* __restrict__ doc_npairs, uint8_t* __restrict__ doc_flags) {
+    __shared__ uint32_t wsum[NT / 64];
+    const uint32_t t = blockIdx.x, b = blockIdx.y;
+    const uint32_t r0 = t * DENSE_TILE + threadIdx.x * 4;
+    uint32_t v[4], c = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        v[k] = r0 + k < V ? dense_sum(dense, b, V, r0 + k) : 0u;
+        c += v[k] ? 1u : 0u;
+    }
+    uint32_t tot;
+    uint32_t o = block_excl_scan<NT, false>(c, wsum, &tot);
+    const uint64_t base = rec_base + *merged_count + tile_off[(uint64_t)b * nt + t];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (v[k]) { rec_slot[base + o] = slot_of_rank[r0 + k]; rec_cnt[base + o] = v[k]; ++o; }
+    if (t == 0 && threadIdx.x == 0) {
+        const uint32_t d = big_list[b];
+        const uint64_t first = tile_off[(uint64_t)b * nt], last = tile_off[(uint64_t)(b + 1) * nt];
+        doc_recoff[d] = rec_base + *merged_count + first;
+        doc_npairs[d] = (uint32_t)(last - first);
+        doc_flags[d] = DF_PARTIAL | DF_PRESORTED;
+    }
+}
+__global__ void k_add_count(uint32_t* __restrict__ merged_count, const uint32_t* __restrict__ add) {
+    merged_count[0] += add[0];
+}
+int launch_dense_emit(const uint32_t* dense, uint32_t nb, uint32_t V, const uint32_t* big_list,
+                      const uint32_t* slot_of_rank, uint64_t rec_base, uint32_t* merged_count, uint32_t* tile_cnt,
+                      uint32_t* rec_slot, uint32_t* rec_cnt, uint64_t* doc_recoff, uint32_t* doc_npairs,
+                      uint8_t* doc_flags, Arena& ar, hipStream_t s) {
+    if (!nb || !V) return 0;
+    const uint32_t nt = (V + DENSE_TILE - 1) / DENSE_TILE;
+    const dim3 grid(nt, nb);
+    k_dense_count<<<grid, NT, 0, s>>>(dense, V, nt, tile_cnt);
+    if (ok()) return -1;
+    if (scan_excl_u32(tile_cnt, tile_cnt, (uint64_t)nt * nb, ar, s)) return -1;
+    k_dense_write<<<grid, NT, 0, s>>>(dense, V, nt, big_list, slot_of_rank, rec_base, merged_count, tile_cnt, rec_slot,
+                                      rec_cnt, doc_recoff, doc_npairs, doc_flags);
+    if (ok()) return -1;
+    /* the DF pass and K5 size the merged region from merged_count: add the dense records */
+    k_add_count<<<1, 1, 0, s>>>(merged_count, tile_cnt + (uint64_t)nt * nb);
+    return ok();
+}
+
 /* -------------------------------------------------------------------- DF -- */
 
 constexpr uint32_t DFH_RECS = 65535;      /* records per workgroup: u16 bins cannot overflow */

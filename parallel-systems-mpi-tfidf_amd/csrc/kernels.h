@@ -13,6 +13,11 @@
 #ifndef CHUNK_BYTES
 #define CHUNK_BYTES  16384u              /* nominal chunk (work unit) size */
 #endif
+#ifndef DENSE_DOC
+#define DENSE_DOC    (4ull << 20)        /* documents longer than this: dense merge of their partial records */
+#endif
+#define BIG_LIST_CAP 4096u               /* dense-merge candidates K0 lists */
+#define DENSE_REP    16u                 /* copies of each dense per-document array (spreads hot-term atomics) */
 #ifndef BIG_DOC
 #define BIG_DOC      49152u              /* documents longer than this are split across chunks */
 #endif
@@ -73,7 +78,7 @@ struct K1Out {
 
 /* K0: chunk boundaries; chunk_start has nchunks+1 entries, chunk_doc nchunks */
 int launch_plan_chunks(const CorpusDev& c, uint64_t nchunks, uint64_t* chunk_start, uint32_t* chunk_doc,
-                       hipStream_t s);
+                       uint32_t* big_list, unsigned long long* big_ctr, hipStream_t s);
 /* K1: tokenize + per-document term counts for chunks [c0, c1) */
 int launch_tokcount(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc,
                     uint64_t c0, uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s);
@@ -106,6 +111,15 @@ int launch_part_merge(const uint64_t* keys, const uint32_t* seq, const uint32_t*
                       uint64_t n, const uint32_t* slot_of_rank, uint64_t rec_base, uint32_t* rec_slot,
                       uint32_t* rec_cnt, uint64_t* doc_recoff, uint32_t* doc_npairs, uint8_t* doc_flags,
                       hipStream_t s);
+/* dense merge of the partial records of long documents (finalize.hip) */
+int launch_part_dense(const uint32_t* part_doc, const uint32_t* part_slot, const uint32_t* part_cnt, uint64_t q,
+                      const uint32_t* big_idx, const uint32_t* rank_of_slot, uint32_t V, uint32_t* dense,
+                      uint64_t* keys, uint32_t* seq, uint32_t* cnt_out, uint32_t* nkeep, hipStream_t s);
+int launch_set_big_idx(const uint32_t* big_list, uint32_t nb, uint32_t* big_idx, hipStream_t s);
+int launch_dense_emit(const uint32_t* dense, uint32_t nb, uint32_t V, const uint32_t* big_list,
+                      const uint32_t* slot_of_rank, uint64_t rec_base, uint32_t* merged_count, uint32_t* tile_cnt,
+                      uint32_t* rec_slot, uint32_t* rec_cnt, uint64_t* doc_recoff, uint32_t* doc_npairs,
+                      uint8_t* doc_flags, Arena& ar, hipStream_t s);
 
 /* DF */
 int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra, uint64_t nrec_max,

@@ -350,3 +350,18 @@ def test_gpu_text_c2_slice_vs_oracle(engine):
     engine.run_host(data, off, p["doc_ids"], p["ndocs_total"])
     ora = oracle_py.run(data, off, p["doc_ids"], p["ndocs_total"])
     assert engine.text() == ora["output_txt"]
+
+
+def test_dense_merge_long_documents(engine):
+    """Documents longer than DENSE_DOC (4 MiB) take the dense merge (partial records summed
+    per document over term ranks, emitted in rank order); a 180 KB document (split across
+    chunks, below DENSE_DOC) still takes the sorted merge in the same run.  Against the
+    oracle, bit-exact."""
+    p = tfidf_configs.plan("c5", scale=0.05)        # four ~5 MB documents among 50k small ones
+    data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
+    sizes = np.diff(off.astype(np.int64))
+    assert (sizes > (4 << 20)).sum() >= 2
+    mid = bytes(data[int(off[0]):int(off[300])])      # ~180 KB: split, but sorted-merged
+    docs = [bytes(data[int(off[i]):int(off[i + 1])]) for i in range(len(off) - 1)] + [mid]
+    d2, o2 = docs_to_arrays(docs)
+    check_vs_oracle(engine, d2, o2)
