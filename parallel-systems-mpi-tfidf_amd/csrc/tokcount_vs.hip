@@ -46,7 +46,10 @@
 
 namespace {
 
-constexpr int NT = 256;
+#ifndef K1_NT
+#define K1_NT 256
+#endif
+constexpr int NT = K1_NT;               /* threads per workgroup (timing experiments override) */
 constexpr int NWAVE = NT / 64;
 constexpr int WSTEP = 1024;               /* bytes per wave step: one 16-byte group per lane */
 #ifndef K1_TB
@@ -660,7 +663,11 @@ int launch_tokcount_vs(const CorpusDev& c, const uint64_t* chunk_start, const ui
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
             ncu = 256;
     }
-    const uint64_t grid = (c1 - c0) < (uint64_t)ncu * 4 ? (c1 - c0) : (uint64_t)ncu * 4;
+#ifndef K1_WGS_PER_CU
+#define K1_WGS_PER_CU 4
+#endif
+    const uint64_t wgs = (uint64_t)ncu * K1_WGS_PER_CU;
+    const uint64_t grid = (c1 - c0) < wgs ? (c1 - c0) : wgs;
     k_tokcount_vs<<<(unsigned)grid, NT, 0, s>>>(c, chunk_start, chunk_doc, c0, c1, v, o);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
