@@ -422,16 +422,32 @@ __global__ void k_df_colsum(const uint32_t* __restrict__ part, uint32_t nparts, 
     for (uint32_t q = 0; q < DFC_G; ++q) sum += (v[q] >> sh) & 0xFFFFu;
     if (sum) atomicAdd(&df[r], sum);
 }
+/* V > 65536 (no LDS histogram): global atomics; DFA_B records per thread per pass so that
+ * DFA_B rank gathers (random over the slot table: 256 MB at c4) are in flight together
+ * instead of one dependent gather per iteration */
+constexpr int DFA_B = 8;
 __global__ void k_df_hist_atomic(uint32_t* __restrict__ rec_slot, uint64_t nrec, const uint32_t* __restrict__ nrec_extra,
                                  const uint32_t* __restrict__ rank_of_slot, uint64_t slot_cap,
                                  uint32_t* __restrict__ status, uint32_t* __restrict__ df) {
     if (nrec_extra) nrec += *nrec_extra;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nrec; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t sl = rec_slot[i];
-        if (sl >= slot_cap) { atomicOr(status, ST_BOUNDS); continue; }
-        const uint32_t r = rank_of_slot[sl];
-        atomicAdd(&df[r], 1u);
-        rec_slot[i] = r;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < nrec; i0 += stride * DFA_B) {
+        uint32_t sl[DFA_B], r[DFA_B];
+#pragma unroll
+        for (int k = 0; k < DFA_B; ++k) {
+            const uint64_t i = i0 + (uint64_t)k * stride;
+            sl[k] = i < nrec ? rec_slot[i] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int k = 0; k < DFA_B; ++k) r[k] = sl[k] < slot_cap ? rank_of_slot[sl[k]] : 0u;
+#pragma unroll
+        for (int k = 0; k < DFA_B; ++k) {
+            const uint64_t i = i0 + (uint64_t)k * stride;
+            if (i >= nrec) continue;
+            if (sl[k] >= slot_cap) { atomicOr(status, ST_BOUNDS); continue; }
+            atomicAdd(&df[r[k]], 1u);
+            rec_slot[i] = r[k];
+        }
     }
 }
 int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra, uint64_t nrec_max,
@@ -454,7 +470,7 @@ int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra
         return ok();
     }
     if (hipMemsetAsync(df, 0, (size_t)V * 4, s) != hipSuccess) return -1;
-    k_df_hist_atomic<<<2048, NT, 0, s>>>(rec_slot, nrec, nrec_extra, rank_of_slot, slot_cap, status, df);
+    k_df_hist_atomic<<<4096, NT, 0, s>>>(rec_slot, nrec, nrec_extra, rank_of_slot, slot_cap, status, df);
     return ok();
 }
 
