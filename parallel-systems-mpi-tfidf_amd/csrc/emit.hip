@@ -8,7 +8,8 @@
  *                result for every finite x >= 0 below 2^63 / 10^16; scores are
  *                tf * log(N/df) <= log(2^32) < 23)
  *   lines        one wave per document: its lines' lengths, a wave scan for their
- *                offsets, then each lane writes its line
+ *                offsets, then each lane writes its line into the wave's LDS stage and
+ *                the wave copies the round out with 16-byte stores
  */
 #include "kernels.h"
 #include "dev_common.h"
@@ -142,8 +143,31 @@ __global__ __launch_bounds__(NT) void k_doc_text_bytes(EmitArgs a) {
     }
 }
 
+/* writes one line ("doc" id '@' word '\t' score '\n') of a short term at o */
+__device__ __forceinline__ void put_line(uint8_t* o, uint32_t id, uint32_t nid, const uint4& k, uint32_t wl,
+                                         uint64_t q) {
+    o[0] = 'd'; o[1] = 'o'; o[2] = 'c';
+    put_dec(o + 3, id, nid);
+    o += 3 + nid;
+    *o++ = '@';
+    const uint32_t w[4] = {k.x, k.y, k.z, k.w};
+    for (uint32_t j = 0; j < wl; ++j) o[j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+    o += wl;
+    *o++ = '\t';
+    put_score(o, q);
+    o += score_len(q);
+    *o = '\n';
+}
+
+/* One wave per document.  A round of 64 lines is assembled in the wave's LDS stage at
+ * the text's 16-byte phase, then copied out with 16-byte stores (whole chunks) and byte
+ * stores (the round's first and last partial chunk); rounds holding a long term (bytes in
+ * the corpus, up to any length) or more than STG bytes write their lines directly. */
+constexpr uint32_t STG = 4096;
 __global__ __launch_bounds__(NT) void k_doc_text_write(EmitArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[NT / 64][STG + 16];
     const uint32_t lane = threadIdx.x & 63;
+    uint8_t* sg = stage[threadIdx.x >> 6];
     const uint32_t stride = gridDim.x * (NT / 64);
     for (uint32_t i = blockIdx.x * (NT / 64) + (threadIdx.x >> 6); i < a.ndocs; i += stride) {
         const uint64_t p0 = a.out_off[i], p1 = a.out_off[i + 1];
@@ -154,29 +178,49 @@ __global__ __launch_bounds__(NT) void k_doc_text_write(EmitArgs a) {
             const bool v = p < p1;
             uint64_t q = 0;
             uint32_t len = 0, t = 0;
-            if (v) { t = a.term[p]; len = line_len(a, nid, p, q); }
+            uint4 k = make_uint4(0u, 0u, 0u, 0u);
+            if (v) { t = a.term[p]; len = line_len(a, nid, p, q); k = a.tkey[t]; }
+            const uint32_t wl = v ? a.tlen[t] : 0u;
             const uint32_t incl = wave_incl_scan(len);
             const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-            if (v) {
+            const bool has_long = __ballot(v && k.w == 0xFFFFFFFFu) != 0ull;
+            if (!has_long && tot <= STG) {
+                const uint32_t ph = (uint32_t)(base & 15u);          /* global 16-byte phase */
+                if (v) put_line(sg + ph + (incl - len), id, nid, k, wl, q);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                /* stage[c*16 .. c*16+16) <-> text[base - ph + c*16 ..) */
+                uint8_t* gb = a.text + (base - ph);
+                const uint32_t end = ph + tot, nch = (end + 15u) >> 4;
+                for (uint32_t c = lane; c < nch; c += 64) {
+                    const uint32_t lo = c * 16u, hi = lo + 16u;
+                    if (lo >= ph && hi <= end) {
+                        *reinterpret_cast<uint4*>(gb + lo) = *reinterpret_cast<const uint4*>(sg + lo);
+                    } else {
+                        for (uint32_t b = lo > ph ? lo : ph; b < (hi < end ? hi : end); ++b) gb[b] = sg[b];
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            } else if (v) {
                 uint8_t* o = a.text + base + (incl - len);
-                o[0] = 'd'; o[1] = 'o'; o[2] = 'c';
-                put_dec(o + 3, id, nid);
-                o += 3 + nid;
-                *o++ = '@';
-                const uint32_t wl = a.tlen[t];
-                const uint4 k = a.tkey[t];
                 if (k.w == 0xFFFFFFFFu) { /* long term (a short key always holds its TAB): corpus bytes */
+                    o[0] = 'd'; o[1] = 'o'; o[2] = 'c';
+                    put_dec(o + 3, id, nid);
+                    o += 3 + nid;
+                    *o++ = '@';
                     const uint8_t* src = a.corpus + ((((uint64_t)k.y << 32) | k.x) & 0xFFFFFFFFFFull);
                     for (uint32_t j = 0; j < wl; ++j) o[j] = src[j];
+                    o += wl;
+                    *o++ = '\t';
+                    put_score(o, q);
+                    o += score_len(q);
+                    *o = '\n';
                 } else {
-                    const uint32_t w[4] = {k.x, k.y, k.z, k.w};
-                    for (uint32_t j = 0; j < wl; ++j) o[j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+                    put_line(o, id, nid, k, wl, q);
                 }
-                o += wl;
-                *o++ = '\t';
-                put_score(o, q);
-                o += score_len(q);
-                *o = '\n';
             }
             base += tot;
         }
