@@ -76,12 +76,12 @@ def _rank_main(rank, world, port, cfg, scale, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("cfg,scale", [("c2", 0.0008), ("c5", 0.0002)])
-def test_two_rank_shards_concatenate_to_single_rank_output(tmp_path, cfg, scale):
+@pytest.mark.parametrize("cfg,scale,world", [("c2", 0.0008, 2), ("c5", 0.0002, 2), ("c2", 0.0008, 3), ("c2", 0.0008, 4)])
+def test_two_rank_shards_concatenate_to_single_rank_output(tmp_path, cfg, scale, world):
+    """Output invariant in the number of shards K (as the reference's is in -np)."""
     import oracle_py
     import tfidf_abi
     import tfidf_configs
-    world = 2
     mp.spawn(_rank_main, args=(world, _free_port(), cfg, scale, str(tmp_path)), nprocs=world, join=True)
     with open(tmp_path / "multirank.txt", "rb") as f:
         got = f.read()
