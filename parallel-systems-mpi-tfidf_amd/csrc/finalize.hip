@@ -689,7 +689,7 @@ __device__ __forceinline__ void k5_prefetch(const K5Args& a, const uint4& m, uin
 }
 
 __global__ __launch_bounds__(NT, K5_WPS) void k_score_wave(K5Args a) {
-    __shared__ uint32_t kb[NT / 64][2][K5_WAVE];
+    __shared__ __attribute__((aligned(16))) uint32_t kb[NT / 64][2][K5_WAVE];
     __shared__ uint32_t hist[NT / 64][K5_NB];
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t stride = gridDim.x * (NT / 64);
@@ -757,6 +757,53 @@ __global__ __launch_bounds__(NT, K5_WPS) void k_score_wave(K5Args a) {
                 const uint32_t j = 64u * q + lane;
                 if (j < n) k5_emit(a, ob + j, ds, r[q], buf0[j]);
             }
+            continue;
+        }
+#ifndef K5_CNT
+#define K5_CNT 128
+#endif
+        if (n <= (uint32_t)K5_CNT) {
+            /* rank by counting: ranks are distinct within a document, so an element's
+             * output position is the number of smaller ranks in the document; every lane
+             * scans the document's ranks with broadcast 16-byte LDS reads (no atomics, one
+             * fence), then gathers its idf values together and stores */
+            constexpr int QC = K5_CNT / 64;
+#pragma unroll
+            for (int q = 0; q < QC; ++q) {
+                const uint32_t j = 64u * q + lane;
+                if (j < n) buf1[j] = r[q];
+            }
+            const uint32_t n4 = (n + 3u) & ~3u;
+            if (lane < 4u && n + lane < n4) buf1[n + lane] = 0xFFFFFFFFu;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint32_t pos[QC];
+#pragma unroll
+            for (int q = 0; q < QC; ++q) pos[q] = 0u;
+            const uint4* k4p = reinterpret_cast<const uint4*>(buf1);
+            for (uint32_t i4 = 0; i4 < n4 / 4u; ++i4) {
+                const uint4 k4 = k4p[i4];
+#pragma unroll
+                for (int q = 0; q < QC; ++q)
+                    pos[q] += (k4.x < r[q] ? 1u : 0u) + (k4.y < r[q] ? 1u : 0u) + (k4.z < r[q] ? 1u : 0u) +
+                              (k4.w < r[q] ? 1u : 0u);
+            }
+            double idf[QC];
+#pragma unroll
+            for (int q = 0; q < QC; ++q) idf[q] = (64u * q + lane < n) ? a.idf_rank[r[q]] : 0.0;
+#pragma unroll
+            for (int q = 0; q < QC; ++q) {
+                const uint32_t j = 64u * q + lane;
+                if (j < n) {
+                    const uint64_t o = ob + pos[q];
+                    const uint32_t cnt = buf0[j];
+                    a.out_term[o] = r[q];
+                    a.out_cnt[o] = cnt;
+                    a.out_score[o] = ((double)cnt / ds) * idf[q];   /* TFIDF.c:202,243-244 */
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             continue;
         }
         if (n <= K5_SMALL) {
