@@ -271,10 +271,99 @@ __global__ void k_part_dense(const uint32_t* __restrict__ pdoc, const uint32_t* 
         cnt_out[p] = c;
     }
 }
+/* The same split with the listed documents' adds aggregated in LDS first (V <= 65536).
+ * Partial records arrive in K1's flush order, so a long run of them belongs to one long
+ * document (its chunks are in flight together): a workgroup takes PDL_RECS consecutive
+ * records and one slice of PDL_SLICE ranks (blockIdx.y), sums the records of its range's
+ * first document ("home") into u32 LDS bins of that slice, and adds only the non-zero
+ * bins to the dense array at the end — one device atomic per (range, term) instead of
+ * one per record.  Records of other listed documents take the global atomic as before;
+ * kept records are written by slice 0 only. */
+constexpr uint32_t PDL_NT = 1024;
+constexpr uint32_t PDL_SLICE = 32768;      /* u32 bins: 128 KB of LDS */
+constexpr uint32_t PDL_RECS = 131072;      /* records per workgroup */
+constexpr int PDL_B = 4;                   /* records per thread in flight together */
+__global__ __launch_bounds__(PDL_NT) void k_part_dense_lds(const uint32_t* __restrict__ pdoc,
+                                                           const uint32_t* __restrict__ pslot,
+                                                           const uint32_t* __restrict__ pcnt, uint64_t q,
+                                                           const uint32_t* __restrict__ big_idx,
+                                                           const uint32_t* __restrict__ rank_of_slot, uint32_t V,
+                                                           uint32_t* __restrict__ dense, uint64_t* __restrict__ keys,
+                                                           uint32_t* __restrict__ seq, uint32_t* __restrict__ cnt_out,
+                                                           uint32_t* __restrict__ nkeep) {
+    extern __shared__ uint32_t pbins[];
+    __shared__ uint32_t home;
+    const uint32_t s0 = blockIdx.y * PDL_SLICE;
+    const uint32_t sw = V - s0 < PDL_SLICE ? V - s0 : PDL_SLICE;
+    const uint64_t r0 = (uint64_t)blockIdx.x * PDL_RECS;
+    const uint64_t r1 = r0 + PDL_RECS < q ? r0 + PDL_RECS : q;
+    const uint32_t rep = blockIdx.x & (DENSE_REP - 1);
+    for (uint32_t k = threadIdx.x; k < sw; k += PDL_NT) pbins[k] = 0;
+    if (threadIdx.x == 0) home = big_idx[pdoc[r0]];
+    __syncthreads();
+    const uint32_t hb = home;
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint64_t i0 = r0 + threadIdx.x; i0 < r1; i0 += (uint64_t)PDL_B * PDL_NT) {
+        uint32_t d[PDL_B], b[PDL_B], r[PDL_B], c[PDL_B];
+#pragma unroll
+        for (int e = 0; e < PDL_B; ++e) {
+            const uint64_t i = i0 + (uint64_t)e * PDL_NT;
+            const bool val = i < r1;
+            d[e] = val ? pdoc[i] : 0u;
+            r[e] = val ? pslot[i] : 0u;
+            c[e] = val ? pcnt[i] : 0u;
+        }
+#pragma unroll
+        for (int e = 0; e < PDL_B; ++e) {
+            const bool val = i0 + (uint64_t)e * PDL_NT < r1;
+            b[e] = val ? big_idx[d[e]] : 0u;
+            r[e] = val ? rank_of_slot[r[e]] : 0u;
+        }
+#pragma unroll
+        for (int e = 0; e < PDL_B; ++e) {
+            const uint64_t i = i0 + (uint64_t)e * PDL_NT;
+            const bool val = i < r1;
+            const bool kept = val && b[e] == 0xFFFFFFFFu;
+            if (val && !kept && r[e] < V && r[e] - s0 < sw) {
+                if (b[e] == hb) atomicAdd(&pbins[r[e] - s0], c[e]);
+                else atomicAdd(&dense[((uint64_t)b[e] * DENSE_REP + rep) * V + r[e]], c[e]);
+            }
+            if (blockIdx.y != 0) continue;
+            const uint64_t km = __ballot(kept);
+            if (!km) continue;
+            const uint32_t leader = (uint32_t)__builtin_ctzll(km);
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(nkeep, (uint32_t)__popcll(km));
+            base = (uint32_t)__shfl(base, (int)leader);
+            if (kept) {
+                const uint32_t p = base + (uint32_t)__popcll(km & ((1ull << lane) - 1ull));
+                keys[p] = ((uint64_t)d[e] << 32) | r[e];
+                seq[p] = p;
+                cnt_out[p] = c[e];
+            }
+        }
+    }
+    __syncthreads();
+    if (hb == 0xFFFFFFFFu) return;
+    uint32_t* dst = dense + ((uint64_t)hb * DENSE_REP + rep) * V + s0;
+    for (uint32_t k = threadIdx.x; k < sw; k += PDL_NT) {
+        const uint32_t v = pbins[k];
+        if (v) atomicAdd(&dst[k], v);
+    }
+}
 int launch_part_dense(const uint32_t* part_doc, const uint32_t* part_slot, const uint32_t* part_cnt, uint64_t q,
                       const uint32_t* big_idx, const uint32_t* rank_of_slot, uint32_t V, uint32_t* dense,
                       uint64_t* keys, uint32_t* seq, uint32_t* cnt_out, uint32_t* nkeep, hipStream_t s) {
     if (!q) return 0;
+#ifndef PDL_OFF
+    if (V <= 2u * PDL_SLICE) {
+        const dim3 grid((uint32_t)((q + PDL_RECS - 1) / PDL_RECS), (V + PDL_SLICE - 1) / PDL_SLICE);
+        const uint32_t lds = (V < PDL_SLICE ? V : PDL_SLICE) * 4u;
+        k_part_dense_lds<<<grid, PDL_NT, lds, s>>>(part_doc, part_slot, part_cnt, q, big_idx, rank_of_slot, V, dense,
+                                                   keys, seq, cnt_out, nkeep);
+        return ok();
+    }
+#endif
     k_part_dense<<<grid_for(q), NT, 0, s>>>(part_doc, part_slot, part_cnt, q, big_idx, rank_of_slot, V, dense, keys,
                                            seq, cnt_out, nkeep);
     return ok();
