@@ -546,6 +546,96 @@ __global__ void k_df_hist_atomic(uint32_t* __restrict__ rec_slot, uint64_t nrec,
         }
     }
 }
+/* V > 65536, partitioned: the 113 M random device atomics of k_df_hist_atomic (c4) miss
+ * L2 (df is 40 MB), so instead the records' ranks are partitioned into slices of
+ * DFS_SLICE ranks and each slice is counted by one workgroup in LDS.
+ *   count    tile t of DFS_TILE records: rank gather, rank written in place (K5 reads
+ *            ranks), LDS histogram of slices -> cnt[slice * ntiles + t]
+ *   scan     exclusive scan of cnt (slice-major): each (slice, tile) gets its segment
+ *   scatter  the same tiles again: LDS positions within the tile's segments, ranks out
+ *   count    one workgroup per slice: u32 LDS bins over its ranks, df stored directly */
+constexpr uint32_t DFS_NT = 1024;
+constexpr uint32_t DFS_PER = 16;
+constexpr uint64_t DFS_TILE = (uint64_t)DFS_NT * DFS_PER;
+constexpr uint32_t DFS_SLICE = 32768;      /* u32 bins: 128 KB of LDS */
+constexpr uint32_t DFS_MAXSL = 4096;       /* slice histogram: 16 KB of LDS (V <= 134 M) */
+__global__ __launch_bounds__(DFS_NT) void k_dfs_count(uint32_t* __restrict__ rec_slot, uint64_t nrec,
+                                                      const uint32_t* __restrict__ nrec_extra,
+                                                      const uint32_t* __restrict__ rank_of_slot, uint64_t slot_cap,
+                                                      uint32_t V, uint32_t nsl, uint32_t* __restrict__ status,
+                                                      uint32_t* __restrict__ cnt) {
+    __shared__ uint32_t h[DFS_MAXSL];
+    if (nrec_extra) nrec += *nrec_extra;
+    for (uint32_t k = threadIdx.x; k < nsl; k += DFS_NT) h[k] = 0;
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)blockIdx.x * DFS_TILE + threadIdx.x;
+    uint32_t sl[DFS_PER];
+#pragma unroll
+    for (uint32_t e = 0; e < DFS_PER; ++e) {
+        const uint64_t i = t0 + (uint64_t)e * DFS_NT;
+        sl[e] = i < nrec ? rec_slot[i] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (uint32_t e = 0; e < DFS_PER; ++e) {
+        const uint64_t i = t0 + (uint64_t)e * DFS_NT;
+        if (i >= nrec) continue;
+        sl[e] = sl[e] < slot_cap ? rank_of_slot[sl[e]] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (uint32_t e = 0; e < DFS_PER; ++e) {
+        const uint64_t i = t0 + (uint64_t)e * DFS_NT;
+        if (i >= nrec) continue;
+        if (sl[e] >= V) { atomicOr(status, ST_BOUNDS); continue; }   /* never expected */
+        rec_slot[i] = sl[e];   /* records carry term ranks from here on */
+        atomicAdd(&h[sl[e] / DFS_SLICE], 1u);
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < nsl; k += DFS_NT) cnt[(uint64_t)k * gridDim.x + blockIdx.x] = h[k];
+}
+__global__ __launch_bounds__(DFS_NT) void k_dfs_scatter(const uint32_t* __restrict__ rec_rank, uint64_t nrec,
+                                                        const uint32_t* __restrict__ nrec_extra, uint32_t V,
+                                                        uint32_t nsl, const uint32_t* __restrict__ off,
+                                                        uint32_t* __restrict__ out) {
+    __shared__ uint32_t h[DFS_MAXSL];
+    if (nrec_extra) nrec += *nrec_extra;
+    for (uint32_t k = threadIdx.x; k < nsl; k += DFS_NT) h[k] = 0;
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)blockIdx.x * DFS_TILE + threadIdx.x;
+    uint32_t r[DFS_PER];
+#pragma unroll
+    for (uint32_t e = 0; e < DFS_PER; ++e) {
+        const uint64_t i = t0 + (uint64_t)e * DFS_NT;
+        r[e] = i < nrec ? rec_rank[i] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (uint32_t e = 0; e < DFS_PER; ++e) {
+        if (r[e] >= V) continue;   /* past the records, or a bad slot (flagged above) */
+        const uint32_t k = r[e] / DFS_SLICE;
+        const uint32_t p = atomicAdd(&h[k], 1u);
+        out[off[(uint64_t)k * gridDim.x + blockIdx.x] + p] = r[e];
+    }
+}
+__global__ __launch_bounds__(DFS_NT) void k_dfs_slice(const uint32_t* __restrict__ part, const uint32_t* __restrict__ off,
+                                                      uint32_t ntiles, uint32_t V, uint32_t* __restrict__ df) {
+    extern __shared__ uint32_t sbins[];
+    const uint32_t k = blockIdx.x, s0 = k * DFS_SLICE;
+    const uint32_t sw = V - s0 < DFS_SLICE ? V - s0 : DFS_SLICE;
+    for (uint32_t j = threadIdx.x; j < sw; j += DFS_NT) sbins[j] = 0;
+    __syncthreads();
+    const uint32_t b = off[(uint64_t)k * ntiles], e = off[(uint64_t)(k + 1) * ntiles];
+    constexpr int B = 8;
+    for (uint32_t i0 = b + threadIdx.x; i0 < e; i0 += B * DFS_NT) {
+        uint32_t r[B];
+#pragma unroll
+        for (int q = 0; q < B; ++q) r[q] = i0 + q * DFS_NT < e ? part[i0 + q * DFS_NT] : 0xFFFFFFFFu;
+#pragma unroll
+        for (int q = 0; q < B; ++q)
+            if (r[q] != 0xFFFFFFFFu) atomicAdd(&sbins[r[q] - s0], 1u);
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < sw; j += DFS_NT) df[s0 + j] = sbins[j];
+}
+
 int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra, uint64_t nrec_max,
                    const uint32_t* rank_of_slot, const uint16_t* rank16, uint32_t V, uint64_t slot_cap,
                    uint32_t* status, uint32_t* df, Arena& ar, hipStream_t s) {
@@ -565,6 +655,30 @@ int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra
         ar.release(m);
         return ok();
     }
+#ifndef DFS_OFF
+    {
+        const uint32_t nsl = (uint32_t)(((uint64_t)V + DFS_SLICE - 1) / DFS_SLICE);
+        const uint64_t ntiles = (nrec_max + DFS_TILE - 1) / DFS_TILE;
+        if (nsl <= DFS_MAXSL && nrec_max < (1ull << 32) && ntiles * nsl < (1ull << 31)) {
+            size_t m = ar.mark();
+            uint32_t* cnt = (uint32_t*)ar.get((size_t)(ntiles * nsl + 1) * 4);
+            uint32_t* part = (uint32_t*)ar.get((size_t)nrec_max * 4);
+            if (!cnt || !part) return -2;   /* arena too small: the run is retried with a larger one */
+            {
+                k_dfs_count<<<(uint32_t)ntiles, DFS_NT, 0, s>>>(rec_slot, nrec, nrec_extra, rank_of_slot, slot_cap, V,
+                                                               nsl, status, cnt);
+                if (ok()) return -1;
+                if (scan_excl_u32(cnt, cnt, ntiles * nsl, ar, s)) return -1;
+                k_dfs_scatter<<<(uint32_t)ntiles, DFS_NT, 0, s>>>(rec_slot, nrec, nrec_extra, V, nsl, cnt, part);
+                if (ok()) return -1;
+                k_dfs_slice<<<nsl, DFS_NT, (size_t)(V < DFS_SLICE ? V : DFS_SLICE) * 4, s>>>(part, cnt, (uint32_t)ntiles,
+                                                                                           V, df);
+                ar.release(m);
+                return ok();
+            }
+        }
+    }
+#endif
     if (hipMemsetAsync(df, 0, (size_t)V * 4, s) != hipSuccess) return -1;
     k_df_hist_atomic<<<4096, NT, 0, s>>>(rec_slot, nrec, nrec_extra, rank_of_slot, slot_cap, status, df);
     return ok();
