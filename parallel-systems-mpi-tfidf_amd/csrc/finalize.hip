@@ -597,8 +597,12 @@ __global__ __launch_bounds__(DFS_NT) void k_dfs_scatter(const uint32_t* __restri
                                                         uint32_t nsl, const uint32_t* __restrict__ off,
                                                         uint32_t* __restrict__ out) {
     __shared__ uint32_t h[DFS_MAXSL];
+    __shared__ uint32_t base[DFS_MAXSL];   /* the tile's segment starts, one gather each */
     if (nrec_extra) nrec += *nrec_extra;
-    for (uint32_t k = threadIdx.x; k < nsl; k += DFS_NT) h[k] = 0;
+    for (uint32_t k = threadIdx.x; k < nsl; k += DFS_NT) {
+        h[k] = 0;
+        base[k] = off[(uint64_t)k * gridDim.x + blockIdx.x];
+    }
     __syncthreads();
     const uint64_t t0 = (uint64_t)blockIdx.x * DFS_TILE + threadIdx.x;
     uint32_t r[DFS_PER];
@@ -612,7 +616,7 @@ __global__ __launch_bounds__(DFS_NT) void k_dfs_scatter(const uint32_t* __restri
         if (r[e] >= V) continue;   /* past the records, or a bad slot (flagged above) */
         const uint32_t k = r[e] / DFS_SLICE;
         const uint32_t p = atomicAdd(&h[k], 1u);
-        out[off[(uint64_t)k * gridDim.x + blockIdx.x] + p] = r[e];
+        out[base[k] + p] = r[e];
     }
 }
 __global__ __launch_bounds__(DFS_NT) void k_dfs_slice(const uint32_t* __restrict__ part, const uint32_t* __restrict__ off,
@@ -790,10 +794,17 @@ __device__ __forceinline__ uint32_t k5_rank(const K5Args& a, uint32_t r) {
     return r;
 }
 
+/* ranks up to 32 - K5_IDX_BITS bits pack (rank, index) keys; up to K5_WIDE_BITS the wave
+ * kernel's bucket sort packs only the rank bits below the bucket (wide mode) */
+#ifndef K5_NO_WIDE
+constexpr uint32_t K5_WIDE_BITS = 32 - K5_IDX_BITS + K5_NB_BITS;
+#else
+constexpr uint32_t K5_WIDE_BITS = 32 - K5_IDX_BITS;
+#endif
 /* which kernel sorts a document of n pairs */
 __device__ __forceinline__ bool k5_by_wave(const K5Args& a, uint32_t n, bool presorted) {
     if (presorted) return n <= K5_WAVE;
-    return n <= K5_SMALL || (n <= K5_WAVE && a.rank_bits + K5_IDX_BITS <= 32);
+    return n <= K5_SMALL || (n <= K5_WAVE && a.rank_bits <= K5_WIDE_BITS);
 }
 
 /* Skewed documents (a bucket of the bucket sort above K5_GROUP_MAX keys): LSD radix sort
@@ -898,6 +909,9 @@ __device__ __forceinline__ void k5_prefetch(const K5Args& a, const uint4& m, uin
     }
 }
 
+/* WIDE: the instance launched when ranks exceed 32 - K5_IDX_BITS bits (its extra path
+ * costs registers the common instance must not pay: c2 score 0.88 -> 1.16 ms with it) */
+template <bool WIDE>
 __global__ __launch_bounds__(NT, K5_WPS) void k_score_wave(K5Args a) {
     __shared__ __attribute__((aligned(16))) uint32_t kb[NT / 64][2][K5_WAVE];
     __shared__ uint32_t hist[NT / 64][K5_NB];
@@ -1056,6 +1070,61 @@ __global__ __launch_bounds__(NT, K5_WPS) void k_score_wave(K5Args a) {
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const bool wide = WIDE && a.rank_bits + K5_IDX_BITS > 32;
+        if (gmax > K5_GROUP_MAX && wide) { /* skewed and too wide for packed keys: k_score_large */
+            if (lane == 0) a.large_list[atomicAdd(a.large_count, 1u)] = i;
+            continue;
+        }
+#ifndef K5_NO_WIDE
+        if constexpr (WIDE) if (wide) {
+            /* wide ranks (V > 2^21): keys hold the rank bits below the bucket and the index;
+             * each lane counts its own elements' smaller bucket mates and stores its pairs
+             * at their output positions directly (as the counting path does) */
+            const uint32_t lm = (1u << hsh) - 1u;
+#pragma unroll
+            for (int q = 0; q < K5_RQ; ++q) {
+                const uint32_t j = 64u * q + lane;
+                if (j < n) buf1[atomicAdd(&h[r[q] >> hsh], 1u)] = ((r[q] & lm) << K5_IDX_BITS) | j;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            constexpr int EB = K5_EB;
+#pragma unroll
+            for (int q0 = 0; q0 < K5_RQ; q0 += EB) {
+                if (64u * q0 >= n) break;
+                uint32_t pos[EB], cnt[EB];
+                double idf[EB];
+#pragma unroll
+                for (int e = 0; e < EB; ++e) {
+                    const uint32_t j = 64u * (q0 + e) + lane;
+                    const uint32_t rk = r[q0 + e];
+                    pos[e] = 0u;
+                    cnt[e] = 0u;
+                    if (j < n) {
+                        const uint32_t d = rk >> hsh, k = ((rk & lm) << K5_IDX_BITS) | j;
+                        const uint32_t gs = d ? h[d - 1] : 0u, ge = h[d];
+                        uint32_t less = 0;
+                        for (uint32_t f = gs; f < ge; ++f) less += buf1[f] < k ? 1u : 0u;
+                        pos[e] = gs + less;
+                        cnt[e] = buf0[j];
+                    }
+                    idf[e] = j < n ? a.idf_rank[rk] : 0.0;
+                }
+#pragma unroll
+                for (int e = 0; e < EB; ++e) {
+                    if (64u * (q0 + e) + lane < n) {
+                        const uint64_t o = ob + pos[e];
+                        a.out_term[o] = r[q0 + e];
+                        a.out_cnt[o] = cnt[e];
+                        a.out_score[o] = ((double)cnt[e] / ds) * idf[e];   /* TFIDF.c:202,243-244 */
+                    }
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            continue;
+        }
+#endif
         if (gmax > K5_GROUP_MAX) { /* skewed ranks: stable radix passes over buf0 */
 #pragma unroll
             for (int q = 0; q < K5_RQ; ++q) {
@@ -1219,7 +1288,8 @@ int launch_score_order(const K5Args& a, hipStream_t s) {
     }
     const uint32_t wg_need = (a.ndocs + NT / 64 - 1) / (NT / 64);
     const uint32_t wg = wg_need < (uint32_t)ncu * 4u ? wg_need : (uint32_t)ncu * 4u; /* 36 KB LDS: 4 per CU */
-    k_score_wave<<<wg, NT, 0, s>>>(a);
+    if (a.rank_bits + K5_IDX_BITS > 32) k_score_wave<true><<<wg, NT, 0, s>>>(a);
+    else k_score_wave<false><<<wg, NT, 0, s>>>(a);
     const uint32_t grid = a.ndocs < 2048u ? a.ndocs : 2048u; /* persistent over the handed-off list */
     k_score_large<<<grid, NT, 0, s>>>(a);
     return ok();
