@@ -748,6 +748,10 @@ extern "C" int tfidf_run(tfidf_ctx* ctx, const tfidf_corpus* in) {
     int rc = 1;
     for (int attempt = 0; attempt < 8 && rc == 1; ++attempt) {
         size_t need = ctx->arena.peak > ctx->arena_buf.cap ? ctx->arena.peak * 2 : ctx->arena_buf.cap;
+        /* N > 1: a retry decided by one rank after the DF exchange would re-enter the
+         * collectives alone; start with an arena the exchange and later stages cannot
+         * exhaust at the BASELINE sizes, so retries only happen before it (in step) */
+        if (ctx->nranks > 1 && need < (2ull << 30)) need = 2ull << 30;
         if (arena_reset(ctx, need) != 0) return TFIDF_E_NOMEM;
         rc = run_once(ctx, c, dev_ids, Nt);
         if (rc == 1) { HIPCHK(hipStreamSynchronize(s)); HIPCHK(hipStreamSynchronize(ctx->stream2)); }
