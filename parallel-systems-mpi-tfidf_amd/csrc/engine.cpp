@@ -687,7 +687,7 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     a.out_term = ctx->out_term.as<uint32_t>();
     a.out_cnt = ctx->out_cnt.as<uint32_t>();
     a.out_score = ctx->out_score.as<double>();
-    LCHK(launch_score_order(a, s));
+    LCHK(launch_score_order(a, s, ctx->stream2, ctx->ev_fork, ctx->ev_order));
     mark(ctx, S_NSTAGES);
     uint32_t st_end = 0;
     HIPCHK(hipMemcpyAsync(&st_end, cnt + 3, 4, hipMemcpyDeviceToHost, s));

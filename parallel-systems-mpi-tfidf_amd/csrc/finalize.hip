@@ -970,8 +970,8 @@ __global__ __launch_bounds__(NT, K5_WPS) void k_score_wave(K5Args a) {
             k5_prefetch(a, m_cur, lane, s_cur, c_cur);
         }
         if (n == 0) continue;
-        if (!k5_by_wave(a, n, presorted)) { /* hand the document to k_score_large's list */
-            if (lane == 0) a.large_list[atomicAdd(a.large_count, 1u)] = i;
+        if (!k5_by_wave(a, n, presorted)) { /* k_score_large's document */
+            if (WIDE && lane == 0) a.large_list[atomicAdd(a.large_count, 1u)] = i; /* else listed up front */
             continue;
         }
         if (rb + n > a.rec_total) { if (lane == 0) atomicOr(a.status, ST_BOUNDS); continue; }
@@ -1274,7 +1274,25 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
     __syncthreads(); /* the next document reuses the LDS buffers */
     }
 }
-int launch_score_order(const K5Args& a, hipStream_t s) {
+/* documents (output positions) the wave kernel leaves to k_score_large, listed before
+ * either runs so that k_score_large can start beside the wave kernel */
+__global__ void k_large_list(K5Args a) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool big = false;
+    if (i < a.ndocs) {
+        const uint4 m = a.meta[i];
+        const uint32_t n = m.z & 0x3FFFFFFFu;
+        big = n != 0u && !k5_by_wave(a, n, ((m.z >> 30) & DF_PRESORTED) != 0);
+    }
+    const uint64_t bm = __ballot(big);
+    if (!bm) return;
+    const uint32_t lane = threadIdx.x & 63, leader = (uint32_t)__builtin_ctzll(bm);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(a.large_count, (uint32_t)__popcll(bm));
+    base = (uint32_t)__shfl(base, (int)leader);
+    if (big) a.large_list[base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull))] = i;
+}
+int launch_score_order(const K5Args& a, hipStream_t s, hipStream_t s2, hipEvent_t ev_fork, hipEvent_t ev_join) {
     if (!a.ndocs) return 0;
     if (hipMemsetAsync(a.large_count, 0, 4, s) != hipSuccess) return -1;
     k_idf_of_rank<<<grid_for(a.nterms ? a.nterms : 1), NT, 0, s>>>(a.df_of_rank, a.idf_idx, a.idf, a.nterms,
@@ -1288,9 +1306,27 @@ int launch_score_order(const K5Args& a, hipStream_t s) {
     }
     const uint32_t wg_need = (a.ndocs + NT / 64 - 1) / (NT / 64);
     const uint32_t wg = wg_need < (uint32_t)ncu * 4u ? wg_need : (uint32_t)ncu * 4u; /* 36 KB LDS: 4 per CU */
-    if (a.rank_bits + K5_IDX_BITS > 32) k_score_wave<true><<<wg, NT, 0, s>>>(a);
-    else k_score_wave<false><<<wg, NT, 0, s>>>(a);
     const uint32_t grid = a.ndocs < 2048u ? a.ndocs : 2048u; /* persistent over the handed-off list */
+    if (a.rank_bits + K5_IDX_BITS > 32) {   /* skewed wide documents are handed off during the run */
+        k_score_wave<true><<<wg, NT, 0, s>>>(a);
+        k_score_large<<<grid, NT, 0, s>>>(a);
+        return ok();
+    }
+    k_large_list<<<grid_for(a.ndocs), NT, 0, s>>>(a);
+#ifndef K5_SERIAL_LARGE
+    if (s2 && ev_fork && ev_join) {
+        /* the wave kernel first (its persistent grid takes the CUs), k_score_large on the
+         * side stream fills them as the wave kernel's workgroups retire */
+        if (hipEventRecord(ev_fork, s) != hipSuccess) return -1;
+        k_score_wave<false><<<wg, NT, 0, s>>>(a);
+        if (hipStreamWaitEvent(s2, ev_fork, 0) != hipSuccess) return -1;
+        k_score_large<<<grid, NT, 0, s2>>>(a);
+        if (hipEventRecord(ev_join, s2) != hipSuccess) return -1;
+        if (hipStreamWaitEvent(s, ev_join, 0) != hipSuccess) return -1;
+        return ok();
+    }
+#endif
+    k_score_wave<false><<<wg, NT, 0, s>>>(a);
     k_score_large<<<grid, NT, 0, s>>>(a);
     return ok();
 }

@@ -160,7 +160,7 @@ struct K5Args {
     uint32_t* out_cnt;           /*               wordCount */
     double* out_score;           /*               tf * idf */
 };
-int launch_score_order(const K5Args& a, hipStream_t s);
+int launch_score_order(const K5Args& a, hipStream_t s, hipStream_t s2, hipEvent_t ev_fork, hipEvent_t ev_join);
 
 /* multi-GPU vocabulary agreement */
 int launch_keys_by_rank(const uint4* vkeys, const uint32_t* slot_of_rank, uint32_t V, uint4* out, hipStream_t s);
