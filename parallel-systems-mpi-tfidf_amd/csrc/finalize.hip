@@ -455,7 +455,10 @@ constexpr uint32_t DFH_MAXV = 65536;
  * DFH_B of them in flight at once (slot loads, then rank gathers, then LDS adds): the
  * loop is latency-bound, so the number of dependent round trips is what matters. */
 constexpr int DFH_NT = 1024;
-constexpr int DFH_B = 16;
+#ifndef DFH_B_N
+#define DFH_B_N 16
+#endif
+constexpr int DFH_B = DFH_B_N;
 __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ rec_slot, uint64_t nrec,
                                                         const uint32_t* __restrict__ nrec_extra,
                                                         const uint32_t* __restrict__ rank_of_slot,
