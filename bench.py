@@ -46,65 +46,93 @@ def hip_device_sync():
         raise RuntimeError("hipDeviceSynchronize failed")
 
 
-def load_traffic():
-    """HBM bytes per K1 launch from the committed rocprofv3 PMC summary (or None)."""
+def k1_source_sha() -> str:
+    """Digest of the K1 source: a committed PMC figure is valid only for the kernel it was
+    measured on."""
+    import hashlib
+    with open(os.path.join(REPO, "parallel-systems-mpi-tfidf_amd", "csrc", "tokcount_vs.hip"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def load_traffic(cfg: str, strong: bool, ngpu: int):
+    """HBM bytes per K1 launch from the committed rocprofv3 PMC passes of THIS config and
+    THIS K1 source (profiles/k1_pmc_traffic.json, written by scripts/traffic_k1.py), or
+    None: never another config's figure."""
     p = os.path.join(REPO, "profiles", "k1_pmc_traffic.json")
-    if os.path.exists(p):
-        with open(p) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
-    return None
+    if not os.path.exists(p):
+        return None, None
+    with open(p) as f:
+        tab = json.load(f)
+    key = f"{cfg}{'_strong' if strong else ''}_g{ngpu}" if ngpu > 1 else cfg
+    e = tab.get(key) if isinstance(tab, dict) else None
+    if not isinstance(e, dict) or e.get("k1_source_sha") != k1_source_sha():
+        return None, None
+    return e.get("hbm_bytes_per_launch"), e.get("source")
 
 
-def cpu_baseline(cfg: str, ndocs_sample: int, threads: int):
+def host_cpu_info() -> dict:
+    """What the CPU baseline ran on: the CPU model, nproc, this process's affinity and the
+    cgroup CPU quota (the box's share of a larger machine)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    aff = len(os.sched_getaffinity(0))
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity": aff, "cgroup_cpus": quota}
+
+
+def cpu_baseline(cfg: str, ndocs_sample: int, threads: int, info: dict):
     """The oracle restatement (C, oracle/tfidf_oracle.c) timed on the host cores.
 
-    Multi-core leg (the reported value): `threads` host threads, each runs
-    the whole restated path (tokenize -> TF -> DF -> idf -> sorted lines) over its own
-    contiguous shard of `ndocs_sample` documents (ctypes releases the GIL); the cross-shard
-    DF combine and the final concatenation are not included, so the figure slightly
-    favours the CPU.  Single-thread leg: the first ndocs_sample / threads documents."""
-    import threading
+    Multi-core leg (the reported value): the reference's worker structure
+    on `threads` host threads — the sample's documents in "docN@" order cut into one
+    byte-balanced shard per thread; each thread tokenizes and counts its shard, the DF
+    tables are combined (CustomReduce + Bcast), each thread scores, formats and sorts its
+    lines, and the texts are concatenated in shard order (the gather).  All of it is in
+    the timed region (oracle_run_sharded).  Single-thread leg: oracle_run over a sixteenth
+    of the sample."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle_py  # oracle: CPU baseline only (never the measured GPU path)
     p = tfidf_configs.plan(cfg)
     n = min(ndocs_sample, len(p["doc_ids"]))
     ids, ntok = p["doc_ids"][:n], p["ntok"][:n]
     data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], ids, ntok)
-    cuts = [(n * k) // threads for k in range(threads + 1)]
-    shards = []
-    for k in range(threads):
-        a, b = cuts[k], cuts[k + 1]
-        o = off[a:b + 1]
-        shards.append((data[int(o[0]):int(o[-1])], o - o[0], ids[a:b]))
-    out = [None] * threads
-
-    def work(k):
-        d, o, i = shards[k]
-        out[k] = oracle_py.run(d, o, i, p["ndocs_total"], arrays=False)["npairs"]
-
+    order = np.argsort(tfidf_configs.doc_name_key(ids), kind="stable").astype(np.uint32)
+    first = tfidf_configs.shard_cuts(np.diff(off.astype(np.int64))[order], threads)
     oracle_py.lib()
     t0 = time.perf_counter()
-    th = [threading.Thread(target=work, args=(k,)) for k in range(threads)]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
+    _, pairs = oracle_py.run_sharded(data, off, ids, p["ndocs_total"], order, first)
     dt = time.perf_counter() - t0
-    pairs = sum(out)
-    # single thread, one shard's worth of documents
-    d1, o1, i1 = shards[0]
+    n1 = max(1, n // 16)
+    o1 = off[: n1 + 1]
+    d1 = data[: int(o1[-1])]
     t1 = time.perf_counter()
-    p1 = oracle_py.run(d1, o1, i1, p["ndocs_total"], arrays=False)["npairs"]
+    p1 = oracle_py.run(d1, o1, ids[:n1], p["ndocs_total"], arrays=False)["npairs"]
     dt1 = time.perf_counter() - t1
-    return {"value": round(len(data) / dt / 1e9, 6), "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/tfidf_oracle.c (C restatement of TFIDF.c) on the first {n} documents of {cfg} "
-                      f"({len(data) / 1e6:.1f} MB, {pairs} pairs) split into {threads} contiguous shards, one host "
-                      f"thread each, tokenize through sorted output lines (cross-shard DF combine not timed); "
-                      f"{dt:.2f} s wall",
-            "pairs_per_s": round(pairs / dt, 1),
-            "single_thread": {"value": round(len(d1) / dt1 / 1e9, 6), "unit": "GB/s", "cores": 1,
-                              "sample": f"first {len(o1) - 1} documents ({len(d1) / 1e6:.1f} MB, {p1} pairs); "
-                                        f"{dt1:.2f} s", "pairs_per_s": round(p1 / dt1, 1)}}
+    out = {"value": round(len(data) / dt / 1e9, 6), "unit": "GB/s", "cores": threads, "kind": "port",
+           "sample": f"oracle/tfidf_oracle.c (C restatement of TFIDF.c) on the first {n} documents of {cfg} "
+                     f"({len(data) / 1e6:.1f} MB, {pairs} pairs): {threads} host threads, one byte-balanced "
+                     f"docN@-ordered shard each; tokenize+count, DF combine, score+format+sort, shard-order "
+                     f"concatenation all timed; {dt:.2f} s wall",
+           "pairs_per_s": round(pairs / dt, 1),
+           "single_thread": {"value": round(len(d1) / dt1 / 1e9, 6), "unit": "GB/s", "cores": 1,
+                             "sample": f"first {n1} documents ({len(d1) / 1e6:.1f} MB, {p1} pairs); {dt1:.2f} s",
+                             "pairs_per_s": round(p1 / dt1, 1)}}
+    out.update(info)
+    return out
 
 
 def main():
@@ -115,7 +143,11 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--cpu-sample-docs", type=int, default=48000)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0: OMP_NUM_THREADS (16 on the GPU box), at most 16")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0: the CPUs this process may use (affinity, capped by the cgroup quota)")
+    ap.add_argument("--strong", action="store_true",
+                    help="split the config's corpus over the GPUs (c3 at --gpus 8: BASELINE's 10M docs / 40 GB "
+                         "over 8 MI355X) instead of one config-sized shard per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the measured HBM read/copy peak probe")
     ap.add_argument("--no-emit", action="store_true", help="skip the (untimed) output-emission measurement")
@@ -140,7 +172,8 @@ def main():
         dist.broadcast(uid, 0)
         eng.comm_init(bytes(uid.numpy().tobytes()), rank, world)
 
-    p = tfidf_configs.plan(args.config, scale=args.scale, rank=rank, nranks=world, weak=True, vocab=args.vocab)
+    p = tfidf_configs.plan(args.config, scale=args.scale, rank=rank, nranks=world, weak=not args.strong,
+                           vocab=args.vocab)
     corpus = eng.synth_device(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"], p["ndocs_total"])
     eng.set_timing(True)
 
@@ -200,7 +233,7 @@ def main():
         k1_avg_ms = float(np.mean(k1_ms))
         alg_bytes = C_bytes + 12.0 * P_pairs  # per K1 launch on this rank
         achieved = alg_bytes / (k1_avg_ms * 1e-3) / 1e9
-        traffic = load_traffic()
+        traffic, traffic_src = load_traffic(args.config, args.strong, ngpu)
         line = {
             "metric": "corpus GB/s (TF-IDF hot path: tokenize->TF->DF->tf*idf->ordered output)",
             "value": round(C_all * args.steps / elapsed / 1e9, 4),
@@ -210,7 +243,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "u8/u32 (f64 score)",
             "data": "synthetic (device-generated Zipfian corpus, csrc/synth.h), resident in HBM",
@@ -226,7 +259,8 @@ def main():
                         "vocab_capacity": int(info["vocab_capacity"]), "terms": int(info["nterms"])},
             "roofline": {"bound": "hbm", "kernel": "k_tokcount_vs (K1)", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "alg_bytes_per_launch": int(alg_bytes),
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "alg_bytes_per_launch": int(alg_bytes),
                          "k1_avg_ms": round(k1_avg_ms, 4),
                          "measured_read_peak": round(probe["read_GBps"], 1) if probe else None,
                          "measured_copy_peak": round(probe["copy_GBps"], 1) if probe else None,
@@ -235,8 +269,11 @@ def main():
             "emit": emit,
         }
         if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
-            thr = args.cpu_threads or min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count() or 1)
-            line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_sample_docs, max(1, min(16, thr)))
+            hi = host_cpu_info()
+            thr = args.cpu_threads or hi["affinity"]
+            if hi["cgroup_cpus"]:
+                thr = min(thr, max(1, int(hi["cgroup_cpus"])))
+            line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_sample_docs, max(1, thr), hi)
         print(json.dumps(line), flush=True)
     eng.close()
     if dist is not None:

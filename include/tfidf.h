@@ -35,7 +35,8 @@ enum tfidf_status {
     TFIDF_E_NODOC = -7,     /* input/docN cannot be opened     (TFIDF.c:134-138) */
     TFIDF_E_OUTPUT = -8,    /* output.txt cannot be written    (TFIDF.c:274-278) */
     TFIDF_E_CAPACITY = -9,  /* an internal table could not be grown */
-    TFIDF_E_STATE = -10     /* call out of order (e.g. fetch before run) */
+    TFIDF_E_STATE = -10,    /* call out of order (e.g. fetch before run) */
+    TFIDF_E_PEER = -11      /* another rank of the DF exchange failed (this rank did not) */
 };
 
 /* ---------------------------------------------------------------- corpus ---- */
@@ -89,6 +90,8 @@ typedef struct tfidf_ctx tfidf_ctx;
 
 /* Opens device `device` (HIP ordinal).  Fails with TFIDF_E_NODEV unless it is gfx950. */
 int tfidf_open(int device, tfidf_ctx** out);
+/* Number of visible HIP devices (0 when there is none). */
+int tfidf_device_count(void);
 void tfidf_close(tfidf_ctx* ctx);
 const char* tfidf_strerror(int status);
 int tfidf_abi_version(void);
@@ -98,7 +101,30 @@ int tfidf_abi_version(void);
  *      (TFIDF.c:209-222,291-326) with RCCL collectives over xGMI. */
 #define TFIDF_UNIQUE_ID_BYTES 128
 int tfidf_comm_unique_id(uint8_t id[TFIDF_UNIQUE_ID_BYTES]);
+/* Attaches an RCCL communicator rank (ncclCommInitRank).  From then on every tfidf_run
+ * of this context is collective: all ranks call it, each on its own shard (contiguous
+ * ranges of the "docN@" order, ndocs_total = N of the whole corpus).  Capacity retries
+ * are agreed between the ranks (all repeat or none does); a rank whose run fails makes
+ * the others return TFIDF_E_PEER instead of waiting. */
 int tfidf_comm_init(tfidf_ctx* ctx, const uint8_t id[TFIDF_UNIQUE_ID_BYTES], int rank, int nranks);
+
+/* ---- one process, several shards: the drop-in for `mpirun -np P ./TFIDF`
+ *      (TFIDF.c:82-92 process group, :125-130 document -> rank assignment, :253-273
+ *      gather + sort).  Rank r runs on devices[r] (NULL: device r).  When every rank has
+ *      its own GPU the ranks are one RCCL clique (ncclCommInitAll); when a device is
+ *      listed more than once (or TFIDF_GROUP_LOCAL is set) they exchange through device
+ *      copies in this process — same engine code, same results. */
+#define TFIDF_GROUP_LOCAL 1u
+typedef struct tfidf_group tfidf_group;
+int tfidf_group_open(int nranks, const int* devices, uint32_t flags, tfidf_group** out);
+int tfidf_group_size(const tfidf_group* g);
+tfidf_ctx* tfidf_group_ctx(tfidf_group* g, int rank);
+/* tfidf_run on every rank at once (one host thread per rank); shards[nranks].  Returns
+ * the lowest rank's own error, else TFIDF_E_PEER, else 0. */
+int tfidf_group_run(tfidf_group* g, const tfidf_corpus* shards);
+/* every rank formats its lines on its GPU, then output.txt = the texts in rank order */
+int tfidf_group_write_output(tfidf_group* g, const char* path);
+void tfidf_group_close(tfidf_group* g);
 
 /* Runs the whole hot path on this shard: tokenize -> per-document TF counts ->
  * vocabulary -> DF (all-reduced across ranks when a communicator is attached) ->
@@ -127,8 +153,8 @@ typedef struct tfidf_run_info {
     uint32_t nstages;
     uint32_t flags;           /* TFIDF_RUN_* */
 } tfidf_run_info;
-#define TFIDF_RUN_K1_FAST 1u  /* whitespace-separated kernel (diagnostic, TFIDF_K1=ws) */
-#define TFIDF_RUN_K1_VS   2u  /* slot-keyed tokenize+count kernel (the default path) */
+#define TFIDF_RUN_K1_VS   2u  /* slot-keyed tokenize+count kernel (the default path; the general
+                                 kernel of TFIDF_K1=general or an unaligned corpus leaves it clear) */
 int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info);
 const char* tfidf_stage_name(int stage);
 /* Enables per-stage HIP event timing (adds a few event records per run). */
@@ -197,6 +223,33 @@ typedef struct tfidf_ingest_info {
 } tfidf_ingest_info;
 int tfidf_ingest_dir_device(tfidf_ctx* ctx, const char* dir, int nthreads, tfidf_corpus* out,
                             uint32_t* bad_doc, tfidf_ingest_info* info);
+
+/* Byte-balanced shard plan of an input directory (replaces the round-robin
+ * document -> rank deal of TFIDF.c:125-130).  One scan gives N (every entry but "." and
+ * "..", TFIDF.c:98-110) and the sizes of doc1..docN (TFIDF.c:130-138 error contract:
+ * TFIDF_E_NOINPUT, TFIDF_E_NODOC with *bad_doc = the smallest missing id).  Documents are
+ * ordered by "docN@" (the output's strcmp order, TFIDF.c:49,273) and cut into nshards
+ * contiguous ranges at the cuts nearest to r * total / nshards, so every shard holds at
+ * most total / nshards + the largest document and the shards' outputs concatenate in
+ * shard order.  Release with tfidf_plan_free. */
+typedef struct tfidf_dir_plan {
+    uint32_t  ndocs;         /* N */
+    uint32_t  nshards;
+    uint32_t* doc_ids;       /* N document ids in "docN@" order */
+    uint64_t* doc_bytes;     /* their sizes */
+    uint32_t* shard_first;   /* nshards + 1: shard r = doc_ids[shard_first[r] .. shard_first[r + 1]) */
+    uint64_t* shard_bytes;   /* nshards */
+} tfidf_dir_plan;
+int tfidf_plan_dir(const char* dir, uint32_t nshards, int nthreads, tfidf_dir_plan* plan, uint32_t* bad_doc);
+void tfidf_plan_free(tfidf_dir_plan* plan);
+/* Streams shard `shard` of the plan into the context's HBM like tfidf_ingest_dir_device;
+ * the corpus carries the documents' global ids (device) and ndocs_total = N. */
+int tfidf_ingest_shard_device(tfidf_ctx* ctx, const char* dir, const tfidf_dir_plan* plan, uint32_t shard,
+                              int nthreads, tfidf_corpus* out, uint32_t* bad_doc, tfidf_ingest_info* info);
+/* The plan's pieces on their own (host only): ids 1..n in "docN@" order, and the
+ * byte-balanced cut of a sequence of sizes (first[nshards + 1]). */
+int tfidf_doc_name_order(uint32_t n, uint32_t* ids);
+int tfidf_shard_split(const uint64_t* bytes, uint32_t n, uint32_t nshards, uint32_t* first);
 
 /* ---------------------------------------------------------------- synthetic - */
 

@@ -44,6 +44,11 @@ def lib():
         L.oracle_run.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, C.POINTER(OracleOut)]
         L.oracle_free.argtypes = [C.POINTER(OracleOut)]
         L.oracle_free.restype = None
+        L.oracle_run_sharded.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                         C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64),
+                                         C.POINTER(C.c_uint64)]
+        L.oracle_free_text.argtypes = [C.c_void_p]
+        L.oracle_free_text.restype = None
         _lib = L
     return _lib
 
@@ -71,3 +76,23 @@ def run(data: np.ndarray, doc_off: np.ndarray, doc_ids=None, n_total: int = 0, a
         return res
     finally:
         lib().oracle_free(C.byref(o))
+
+
+def run_sharded(data: np.ndarray, doc_off: np.ndarray, doc_ids, n_total: int, order: np.ndarray,
+                first: np.ndarray) -> tuple:
+    """The CPU baseline of the multi-worker path (oracle_run_sharded): one host thread per
+    shard (documents order[first[s]:first[s+1]]), DF combine, per-shard sort, shard-order
+    concatenation.  Returns (output.txt bytes, pairs)."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    doc_off = np.ascontiguousarray(doc_off, dtype=np.uint64)
+    ids = None if doc_ids is None else np.ascontiguousarray(doc_ids, dtype=np.uint32)
+    order = np.ascontiguousarray(order, dtype=np.uint32)
+    first = np.ascontiguousarray(first, dtype=np.uint32)
+    txt, n, npairs = C.c_void_p(), C.c_uint64(), C.c_uint64()
+    lib().oracle_run_sharded(data.ctypes.data if len(data) else None, doc_off.ctypes.data,
+                             None if ids is None else ids.ctypes.data, n_total, order.ctypes.data,
+                             first.ctypes.data, len(first) - 1, C.byref(txt), C.byref(n), C.byref(npairs))
+    try:
+        return C.string_at(txt, n.value), int(npairs.value)
+    finally:
+        lib().oracle_free_text(txt)

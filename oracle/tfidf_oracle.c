@@ -299,6 +299,176 @@ void oracle_free(oracle_out* o) {
     memset(o, 0, sizeof(*o));
 }
 
+/* ------------------------------------------------------------------------------
+ * CPU baseline of the whole multi-worker path (bench.py cpu_baseline only): the
+ * reference's rank structure on host threads.  Shard s = documents order[first[s] ..
+ * first[s+1]) (contiguous "docN@" ranges, so shard outputs concatenate in order):
+ *   1. every thread tokenizes and counts its shard (TFIDF.c:130-196, as oracle_run);
+ *   2. the DF combine: shard vocabularies merged, df summed (CustomReduce + Bcast,
+ *      TFIDF.c:209-222,291-326);
+ *   3. every thread scores and formats its lines with the global df and sorts them
+ *      (TFIDF.c:202,243-245,273);
+ *   4. the shard texts are concatenated in shard order (the gather, TFIDF.c:253-270).
+ * All four phases are inside the caller's timed region. */
+#include <pthread.h>
+
+typedef struct {
+    const uint8_t* bytes;
+    const uint64_t* doc_off;
+    const uint32_t* doc_ids;
+    const uint32_t* order;
+    uint32_t a, b;            /* order[a .. b) */
+    uint64_t n_total;
+    o_vocab v;
+    o_pair* pairs;
+    uint64_t np;
+    uint32_t* docsize;        /* by position in [a, b) */
+    uint32_t* gdf;            /* global df of each shard term (phase 2) */
+    o_buf text;
+} o_shard;
+
+static void* o_shard_count(void* arg) {
+    o_shard* s = (o_shard*)arg;
+    o_vocab* v = &s->v;
+    ov_init(v);
+    const uint32_t nd = s->b - s->a;
+    s->docsize = (uint32_t*)calloc(nd ? nd : 1, sizeof(uint32_t));
+    uint64_t np_cap = 0, dcap = 256;
+    uint32_t* dmap = (uint32_t*)malloc(dcap * 2 * sizeof(uint32_t));
+    for (uint32_t j = 0; j < nd; ++j) {
+        const uint32_t d = s->order[s->a + j];
+        const uint8_t* p = s->bytes + s->doc_off[d];
+        const uint8_t* e = s->bytes + s->doc_off[d + 1];
+        const uint64_t first = s->np;
+        uint32_t ds = 0;
+        for (const uint8_t* q = p; q < e;) {
+            while (q < e && o_ws(*q)) ++q;
+            if (q >= e) break;
+            ++ds;
+            while (q < e && !o_ws(*q)) ++q;
+        }
+        s->docsize[j] = ds;
+        uint64_t need = 16;
+        while (need < (uint64_t)ds * 2) need *= 2;
+        if (need > dcap) { dcap = need; dmap = (uint32_t*)realloc(dmap, dcap * 2 * sizeof(uint32_t)); }
+        memset(dmap, 0, need * 2 * sizeof(uint32_t));
+        for (const uint8_t* q = p; q < e;) {
+            while (q < e && o_ws(*q)) ++q;
+            if (q >= e) break;
+            const uint8_t* w = q;
+            while (q < e && !o_ws(*q)) ++q;
+            uint64_t n = (uint64_t)(q - w);
+            const uint8_t* z = (const uint8_t*)memchr(w, 0, n);
+            if (z) n = (uint64_t)(z - w);
+            const uint32_t t = ov_intern(v, w, n);
+            uint64_t h = ((uint64_t)t * 0x9E3779B97F4A7C15ull >> 17) & (need - 1);
+            for (;;) {
+                if (dmap[2 * h] == 0) {
+                    if (s->np == np_cap) {
+                        np_cap = np_cap ? np_cap * 2 : 4096;
+                        s->pairs = (o_pair*)realloc(s->pairs, np_cap * sizeof(o_pair));
+                    }
+                    s->pairs[s->np].doc_idx = j; s->pairs[s->np].term = t; s->pairs[s->np].count = 1;
+                    dmap[2 * h] = t + 1; dmap[2 * h + 1] = (uint32_t)(s->np - first);
+                    ++s->np;
+                    break;
+                }
+                if (dmap[2 * h] == t + 1) { s->pairs[first + dmap[2 * h + 1]].count++; break; }
+                h = (h + 1) & (need - 1);
+            }
+            if (v->last_doc[t] != j) { v->df[t]++; v->last_doc[t] = j; }
+        }
+    }
+    free(dmap);
+    return NULL;
+}
+
+static void* o_shard_emit(void* arg) {
+    o_shard* s = (o_shard*)arg;
+    o_buf lines = {0};
+    uint64_t* line_off = (uint64_t*)malloc((s->np + 1) * sizeof(uint64_t));
+    char num[64];
+    for (uint64_t i = 0; i < s->np; ++i) {
+        const o_pair* pr = &s->pairs[i];
+        const uint32_t d = s->order[s->a + pr->doc_idx];
+        const uint32_t id = s->doc_ids ? s->doc_ids[d] : d + 1;
+        const char* w = s->v.pool.p + s->v.off[pr->term];
+        const int wl = (int)(s->v.off[pr->term + 1] - s->v.off[pr->term]);
+        const double sc = (1.0 * pr->count / s->docsize[pr->doc_idx]) * log(1.0 * (double)s->n_total / s->gdf[pr->term]);
+        line_off[i] = lines.n;
+        const int nn = snprintf(num, sizeof num, "doc%u@", id);
+        ob_need(&lines, (uint64_t)nn + (uint64_t)wl + 64);
+        memcpy(lines.p + lines.n, num, (size_t)nn); lines.n += (uint64_t)nn;
+        memcpy(lines.p + lines.n, w, (size_t)wl); lines.n += (uint64_t)wl;
+        lines.n += (uint64_t)snprintf(lines.p + lines.n, 64, "\t%.16f", sc);
+        lines.p[lines.n++] = 0;
+    }
+    o_line* ord = (o_line*)malloc((s->np ? s->np : 1) * sizeof(o_line));
+    for (uint64_t i = 0; i < s->np; ++i) { ord[i].s = lines.p + line_off[i]; ord[i].i = i; }
+    qsort(ord, s->np, sizeof(o_line), o_line_cmp);
+    ob_need(&s->text, lines.n + 1);
+    for (uint64_t r = 0; r < s->np; ++r) {
+        const uint64_t l = strlen(ord[r].s);
+        memcpy(s->text.p + s->text.n, ord[r].s, l);
+        s->text.n += l;
+        s->text.p[s->text.n++] = '\n';
+    }
+    free(ord); free(line_off); free(lines.p);
+    return NULL;
+}
+
+int oracle_run_sharded(const uint8_t* bytes, const uint64_t* doc_off, const uint32_t* doc_ids, uint64_t n_total,
+                       const uint32_t* order, const uint32_t* first, uint32_t nshards, char** text, uint64_t* len,
+                       uint64_t* npairs) {
+    o_shard* sh = (o_shard*)calloc(nshards, sizeof(o_shard));
+    pthread_t* th = (pthread_t*)malloc(nshards * sizeof(pthread_t));
+    for (uint32_t k = 0; k < nshards; ++k) {
+        sh[k].bytes = bytes; sh[k].doc_off = doc_off; sh[k].doc_ids = doc_ids; sh[k].order = order;
+        sh[k].a = first[k]; sh[k].b = first[k + 1]; sh[k].n_total = n_total;
+    }
+    for (uint32_t k = 0; k < nshards; ++k) pthread_create(&th[k], NULL, o_shard_count, &sh[k]);
+    for (uint32_t k = 0; k < nshards; ++k) pthread_join(th[k], NULL);
+    /* DF combine: one global term table, df summed over the shards */
+    o_vocab g;
+    ov_init(&g);
+    uint32_t** map = (uint32_t**)malloc(nshards * sizeof(uint32_t*));
+    for (uint32_t k = 0; k < nshards; ++k) {
+        map[k] = (uint32_t*)malloc((sh[k].v.n + 1) * sizeof(uint32_t));
+        for (uint32_t t = 0; t < sh[k].v.n; ++t) {
+            const uint32_t gt = ov_intern(&g, (const uint8_t*)sh[k].v.pool.p + sh[k].v.off[t], sh[k].v.off[t + 1] - sh[k].v.off[t]);
+            g.df[gt] += sh[k].v.df[t];
+            map[k][t] = gt;
+        }
+    }
+    for (uint32_t k = 0; k < nshards; ++k) {   /* the broadcast: each shard's terms get the global df */
+        sh[k].gdf = (uint32_t*)malloc((sh[k].v.n + 1) * sizeof(uint32_t));
+        for (uint32_t t = 0; t < sh[k].v.n; ++t) sh[k].gdf[t] = g.df[map[k][t]];
+    }
+    for (uint32_t k = 0; k < nshards; ++k) pthread_create(&th[k], NULL, o_shard_emit, &sh[k]);
+    for (uint32_t k = 0; k < nshards; ++k) pthread_join(th[k], NULL);
+    /* gather in shard order */
+    uint64_t total = 0, np = 0;
+    for (uint32_t k = 0; k < nshards; ++k) { total += sh[k].text.n; np += sh[k].np; }
+    char* out = (char*)malloc(total + 1);
+    uint64_t at = 0;
+    for (uint32_t k = 0; k < nshards; ++k) {
+        if (sh[k].text.n) memcpy(out + at, sh[k].text.p, sh[k].text.n);
+        at += sh[k].text.n;
+    }
+    *text = out;
+    *len = total;
+    *npairs = np;
+    for (uint32_t k = 0; k < nshards; ++k) {
+        free(sh[k].pairs); free(sh[k].docsize); free(sh[k].gdf); free(sh[k].text.p); free(map[k]);
+        free(sh[k].v.slot); free(sh[k].v.off); free(sh[k].v.df); free(sh[k].v.last_doc); free(sh[k].v.pool.p);
+    }
+    free(g.slot); free(g.off); free(g.df); free(g.last_doc); free(g.pool.p);
+    free(map); free(sh); free(th);
+    return 0;
+}
+
+void oracle_free_text(char* p) { free(p); }
+
 /* N semantics (TFIDF.c:98-110): every entry except "." and ".." */
 int oracle_count_entries(const char* dir) {
     DIR* d = opendir(dir);

@@ -27,6 +27,7 @@
 #include "../../include/tfidf.h"
 #include "kernels.h"
 #include "synth.h"
+#include "xport.h"
 
 extern "C" void tfidf_synth_spec(syn_spec* s, uint64_t seed, uint32_t V, uint32_t mode, const double* cdf);
 
@@ -69,14 +70,13 @@ const char* kStageNames[S_NSTAGES] = {"prep", "tokcount", "vocab", "merge", "df"
 struct tfidf_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    ncclComm_t comm = nullptr;
+    Xport* xp = nullptr;    /* peers of the DF exchange (RCCL or in-process); owned */
     int rank = 0, nranks = 1;
     bool timing = true;
-    int k1_mode = 0;        /* 0 auto, 2 general K1 (env TFIDF_K1=general), 3 ws K1 (TFIDF_K1=ws) */
+    int k1_mode = 0;        /* 0 auto, 2 general K1 (env TFIDF_K1=general: cross-checks) */
     bool stamps_on = false; /* env TFIDF_STAMPS=1 with the diagnostic library build */
     uint32_t ablate = 0;    /* env TFIDF_K1_ABLATE: K1 timing experiments, pipeline stops after K1 */
     DevBuf stamps;
-    bool k1_fast = false;   /* last run used the whitespace-separated kernel (TFIDF_K1=ws) */
     bool k1_vs = false;     /* last run used the slot-keyed kernel (default) */
     hipEvent_t ev[S_NSTAGES + 1];
     Arena arena;
@@ -111,7 +111,12 @@ struct tfidf_ctx {
     DevBuf df_local, df_global, present, idf_vals;
     DevBuf dkey0, dkey1, dseq0, dseq1, npairs_ord, out_off, doc_meta;
     DevBuf out_term, out_cnt, out_score, idf_rank, large_list;
-    DevBuf x_mine, x_send, x_recv, x_recv2, x_seq0, x_seq1, x_head, x_grank, x_dfv, x_cnt;
+    DevBuf x_mine, x_send, x_recv, x_recv2, x_seq0, x_seq1, x_head, x_grank, x_dfv, x_arena_buf;
+    Arena x_arena;          /* scratch of the exchange's sort/scan, sized before the exchange */
+    /* sizes the local part of a run hands to the exchange and the stages after it */
+    uint32_t run_N = 0, run_V = 0;
+    uint64_t run_cap = 0, run_R_total = 0;
+    const uint32_t* run_merged = nullptr;
     /* output text (emit.hip) */
     DevBuf t_key, t_len, doc_tbytes, doc_toff, text;
     uint64_t text_bytes = 0;
@@ -178,6 +183,11 @@ static void mark(tfidf_ctx* ctx, int stage) {
 
 extern "C" {
 
+int tfidf_device_count(void) {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess && n > 0 ? n : 0;
+}
+
 int tfidf_open(int device, tfidf_ctx** out) {
     if (!out) return TFIDF_E_INVAL;
     *out = nullptr;
@@ -194,7 +204,6 @@ int tfidf_open(int device, tfidf_ctx** out) {
     ctx->device = device;
     const char* km = getenv("TFIDF_K1");
     if (km && !strcmp(km, "general")) ctx->k1_mode = 2;
-    if (km && !strcmp(km, "ws")) ctx->k1_mode = 3;
     const char* ks = getenv("TFIDF_STAMPS");
     ctx->stamps_on = ks && ks[0] == '1';
     const char* ka = getenv("TFIDF_K1_ABLATE");
@@ -226,7 +235,7 @@ void tfidf_close(tfidf_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+    delete ctx->xp;
     if (ctx->stream2) { (void)hipStreamSynchronize(ctx->stream2); (void)hipStreamDestroy(ctx->stream2); }
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_order) (void)hipEventDestroy(ctx->ev_order);
@@ -243,7 +252,7 @@ void tfidf_close(tfidf_ctx* ctx) {
                       &ctx->doc_toff, &ctx->text, &ctx->out_term, &ctx->out_cnt,
                       &ctx->out_score, &ctx->idf_rank, &ctx->large_list, &ctx->x_mine, &ctx->x_send, &ctx->x_recv,
                       &ctx->x_recv2, &ctx->x_seq0, &ctx->x_seq1, &ctx->x_head, &ctx->x_grank, &ctx->x_dfv,
-                      &ctx->x_cnt, &ctx->stamps, &ctx->big_list, &ctx->big_idx, &ctx->dense_cnt, &ctx->kcnt,
+                      &ctx->x_arena_buf, &ctx->stamps, &ctx->big_list, &ctx->big_idx, &ctx->dense_cnt, &ctx->kcnt,
                       &ctx->tile_cnt};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i <= S_NSTAGES; ++i) (void)hipEventDestroy(ctx->ev[i]);
@@ -269,76 +278,145 @@ int tfidf_comm_unique_id(uint8_t id[TFIDF_UNIQUE_ID_BYTES]) {
 int tfidf_comm_init(tfidf_ctx* ctx, const uint8_t id[TFIDF_UNIQUE_ID_BYTES], int rank, int nranks) {
     if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return TFIDF_E_INVAL;
     HIPCHK(hipSetDevice(ctx->device));
-    if (ctx->comm) { (void)ncclCommDestroy(ctx->comm); ctx->comm = nullptr; }
+    tfidf_ctx_attach_xport(ctx, nullptr);
     ncclUniqueId u;
     memcpy(&u, id, TFIDF_UNIQUE_ID_BYTES);
-    NCCLCHK(ncclCommInitRank(&ctx->comm, nranks, u, rank));
-    ctx->rank = rank;
-    ctx->nranks = nranks;
-    return TFIDF_OK;
+    ncclComm_t comm = nullptr;
+    NCCLCHK(ncclCommInitRank(&comm, nranks, u, rank));
+    return tfidf_ctx_attach_xport(ctx, make_rccl_xport(comm, rank, nranks, ctx->device));
 }
 
 }  // extern "C"
 
+int tfidf_ctx_attach_xport(tfidf_ctx* ctx, Xport* xp) {
+    if (!ctx) { delete xp; return TFIDF_E_INVAL; }
+    delete ctx->xp;
+    ctx->xp = xp;
+    ctx->rank = xp ? xp->rank : 0;
+    ctx->nranks = xp ? xp->nranks : 1;
+    return TFIDF_OK;
+}
+int tfidf_ctx_device(const tfidf_ctx* ctx) { return ctx->device; }
+hipStream_t tfidf_ctx_stream(const tfidf_ctx* ctx) { return ctx->stream; }
+
 /* ------------------------------------------------------------------------------ */
 
-/* RCCL vocabulary agreement + DF all-reduce.  Returns df_global (by local rank). */
-static int exchange_df(tfidf_ctx* ctx, uint32_t V) {
+/* ---- the DF exchange (replaces MPI_Reduce(CustomReduce) + MPI_Bcast, TFIDF.c:209-222,
+ * 291-326).  Every rank enters it once per attempt, also when its local stages failed or
+ * asked for a retry, so the ranks always agree:
+ *   1. words(status, V): any error -> every rank returns an error (its own, or
+ *      TFIDF_E_PEER); any retry -> every rank returns 1 and repeats the run in step.
+ *   2. every buffer of the exchange is sized from max V (known to all after step 1);
+ *      words(allocation status) -> all fail together or none does.
+ *   3. the vocabulary union and the DF all-reduce.  From here on no stage of the run
+ *      returns "retry": the exchange has its own scratch arena (sized in 2) and the
+ *      stages after it were checked against the main arena before step 1 (run_local).
+ *      An error inside 3 aborts the transport, releasing the peers. */
+static uint64_t status_word(int rc) { return rc < 0 ? 0x100ull | (uint64_t)(-rc) : (uint64_t)rc; }
+
+static size_t scan_scratch(uint64_t n) { return (size_t)(n / 16) + 8192; }
+
+static int exchange_agree(tfidf_ctx* ctx, int local_rc, uint64_t v, uint64_t* maxv) {
+    Xport* xp = ctx->xp;
+    std::vector<uint64_t> all(2 * (size_t)xp->nranks);
+    const uint64_t mine[2] = {status_word(local_rc), v};
+    const int rc = xp->words(mine, all.data(), ctx->stream);
+    if (rc) return rc;
+    uint64_t worst = 0, mv = 1;
+    for (int r = 0; r < xp->nranks; ++r) {
+        worst = all[2 * r] > worst ? all[2 * r] : worst;
+        mv = all[2 * r + 1] > mv ? all[2 * r + 1] : mv;
+    }
+    if (maxv) *maxv = mv;
+    if (worst >= 0x100) return local_rc < 0 ? local_rc : TFIDF_E_PEER;
+    return worst ? 1 : 0;
+}
+
+/* errors inside the collective sequence: no retry is possible any more */
+#define XCHK(x)                                                             \
+    do {                                                                    \
+        int l_ = (x);                                                       \
+        if (l_ == -2) return TFIDF_E_CAPACITY;                              \
+        if (l_ < 0) { HIPCHK(hipGetLastError()); return TFIDF_E_HIP; }      \
+    } while (0)
+
+static int exchange_collective(tfidf_ctx* ctx, uint32_t V, uint64_t maxv) {
     hipStream_t s = ctx->stream;
-    Arena& ar = ctx->arena;
-    ENSURE(ctx->x_cnt, 8 * (size_t)ctx->nranks + 8);
-    ENSURE(ctx->x_mine, (size_t)V * 16 + 16);
-    LCHK(launch_keys_by_rank(ctx->vkeys.as<uint4>(), ctx->slot_of_rank.as<uint32_t>(), V, ctx->x_mine.as<uint4>(), s));
-    uint64_t* cnts = ctx->x_cnt.as<uint64_t>();
-    uint64_t myv = V;
-    HIPCHK(hipMemcpyAsync(cnts + ctx->nranks, &myv, 8, hipMemcpyHostToDevice, s));
-    NCCLCHK(ncclAllGather(cnts + ctx->nranks, cnts, 1, ncclUint64, ctx->comm, s));
-    std::vector<uint64_t> hc(ctx->nranks);
-    HIPCHK(hipMemcpyAsync(hc.data(), cnts, 8 * ctx->nranks, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    uint64_t maxv = 1;
-    for (uint64_t c : hc) maxv = c > maxv ? c : maxv;
-    uint64_t ntot = maxv * ctx->nranks;
-    ENSURE(ctx->x_send, maxv * 16);
-    ENSURE(ctx->x_recv, ntot * 16);
-    ENSURE(ctx->x_recv2, ntot * 16);
-    ENSURE(ctx->x_seq0, ntot * 4);
-    ENSURE(ctx->x_seq1, ntot * 4);
-    ENSURE(ctx->x_head, (ntot + 1) * 4);
-    HIPCHK(hipMemsetAsync(ctx->x_send.p, 0xEE, maxv * 16, s)); /* padding = empty-slot sentinel key */
+    Xport* xp = ctx->xp;
+    Arena& ar = ctx->x_arena;
+    ar.used = 0;
+    const uint64_t ntot = maxv * (uint64_t)xp->nranks;
+    XCHK(launch_keys_by_rank(ctx->vkeys.as<uint4>(), ctx->slot_of_rank.as<uint32_t>(), V, ctx->x_mine.as<uint4>(), s));
+    HIPCHK(hipMemsetAsync(ctx->x_send.p, 0xEE, maxv * 16, s)); /* padding = the empty-slot key (no id) */
     if (V) HIPCHK(hipMemcpyAsync(ctx->x_send.p, ctx->x_mine.p, (size_t)V * 16, hipMemcpyDeviceToDevice, s));
-    NCCLCHK(ncclAllGather(ctx->x_send.p, ctx->x_recv.p, maxv * 16, ncclUint8, ctx->comm, s));
+    int rc = xp->allgather(ctx->x_send.p, ctx->x_recv.p, maxv * 16, s);
+    if (rc) return rc;
     HIPCHK(hipMemsetAsync(ctx->x_seq0.p, 0, ntot * 4, s));
     uint32_t vm = 0;
-    LCHK(key_varying_bytes_u128(ctx->x_recv.as<uint4>(), ntot, &vm, ar, s));
+    XCHK(key_varying_bytes_u128(ctx->x_recv.as<uint4>(), ntot, &vm, ar, s));
     int cur = radix_sort_u128(ctx->x_recv.as<uint4>(), ctx->x_seq0.as<uint32_t>(), ctx->x_recv2.as<uint4>(),
                               ctx->x_seq1.as<uint32_t>(), ntot, vm, ar, s);
-    LCHK(cur);
+    XCHK(cur);
     uint4* u = cur ? ctx->x_recv2.as<uint4>() : ctx->x_recv.as<uint4>();
     uint32_t* head = ctx->x_head.as<uint32_t>();
-    LCHK(launch_union_heads(u, ntot, head, s));
-    LCHK(scan_excl_u32(head, head, ntot, ar, s));
+    XCHK(launch_union_heads(u, ntot, head, s));
+    XCHK(scan_excl_u32(head, head, ntot, ar, s));
     uint32_t Vg = 0;
     HIPCHK(hipMemcpyAsync(&Vg, head + ntot, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    ctx->Vg = Vg;
-    ENSURE(ctx->x_grank, (size_t)V * 4 + 4);
-    ENSURE(ctx->x_dfv, (size_t)Vg * 4 + 4);
-    LCHK(launch_union_lookup(ctx->x_mine.as<uint4>(), V, u, head, ntot, nullptr, ctx->x_grank.as<uint32_t>(), s));
-    HIPCHK(hipMemsetAsync(ctx->x_dfv.p, 0, (size_t)Vg * 4, s));
-    LCHK(launch_scatter_df(ctx->df_local.as<uint32_t>(), ctx->x_grank.as<uint32_t>(), V, ctx->x_dfv.as<uint32_t>(), s));
-    NCCLCHK(ncclAllReduce(ctx->x_dfv.p, ctx->x_dfv.p, Vg, ncclUint32, ncclSum, ctx->comm, s));
-    LCHK(launch_gather_df(ctx->x_dfv.as<uint32_t>(), ctx->x_grank.as<uint32_t>(), V, ctx->df_global.as<uint32_t>(), s));
+    ctx->Vg = Vg;   /* identical on every rank: the same sorted union */
+    XCHK(launch_union_lookup(ctx->x_mine.as<uint4>(), V, u, head, ntot, nullptr, ctx->x_grank.as<uint32_t>(), s));
+    HIPCHK(hipMemsetAsync(ctx->x_dfv.p, 0, (size_t)Vg * 4 + 4, s));
+    XCHK(launch_scatter_df(ctx->df_local.as<uint32_t>(), ctx->x_grank.as<uint32_t>(), V, ctx->x_dfv.as<uint32_t>(), s));
+    rc = xp->allreduce_sum_u32(ctx->x_dfv.as<uint32_t>(), Vg, s);
+    if (rc) return rc;
+    XCHK(launch_gather_df(ctx->x_dfv.as<uint32_t>(), ctx->x_grank.as<uint32_t>(), V, ctx->df_global.as<uint32_t>(), s));
     return 0;
 }
 
-/* One attempt of the pipeline.  Returns 0 on success, 1 to retry with grown
- * capacities, <0 on error. */
-static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids, uint64_t Nt) {
+static int exchange_df(tfidf_ctx* ctx, int local_rc, uint32_t V) {
+    uint64_t maxv = 1;
+    int rc = exchange_agree(ctx, local_rc, V, &maxv);   /* step 1 */
+    if (rc) return rc;
+    /* step 2: everything the exchange touches, sized from max V */
+    const uint64_t ntot = maxv * (uint64_t)ctx->xp->nranks;
+    int arc = 0;
+    auto ens = [&](DevBuf& b, size_t bytes) { if (!arc && b.ensure(bytes) != 0) arc = TFIDF_E_NOMEM; };
+    ens(ctx->x_mine, maxv * 16 + 16);
+    ens(ctx->x_send, maxv * 16 + 16);
+    ens(ctx->x_recv, ntot * 16 + 16);
+    ens(ctx->x_recv2, ntot * 16 + 16);
+    ens(ctx->x_seq0, ntot * 4 + 4);
+    ens(ctx->x_seq1, ntot * 4 + 4);
+    ens(ctx->x_head, (ntot + 1) * 4);
+    ens(ctx->x_grank, maxv * 4 + 4);
+    ens(ctx->x_dfv, ntot * 4 + 4);   /* the union has at most ntot terms */
+    /* radix histograms (256 words per 2048 keys) + the head scan + the varying-byte probe */
+    ens(ctx->x_arena_buf, (size_t)(ntot / 2) + scan_scratch(ntot) + (64u << 10));
+    if (!arc) {
+        ctx->x_arena.base = (uint8_t*)ctx->x_arena_buf.p;
+        ctx->x_arena.cap = ctx->x_arena_buf.cap;
+        ctx->x_arena.used = 0;
+    }
+    rc = exchange_agree(ctx, arc, 0, nullptr);   /* all allocated, or all fail */
+    if (rc == 1) rc = TFIDF_E_STATE;               /* no retry is ever requested here */
+    if (rc) return rc;
+    rc = exchange_collective(ctx, V, maxv);        /* step 3 */
+    if (rc && rc != TFIDF_E_PEER) ctx->xp->abort();
+    return rc;
+}
+
+/* The local stages of one attempt (this shard only, no collective): K0, K1, vocabulary,
+ * merge, local DF.  Returns 0, 1 to retry with grown capacities, 2 for a timing ablation
+ * run (nothing after K1 is valid), <0 on error.  Also checks that the main arena holds
+ * what the stages after the exchange need, so that they never ask for a retry. */
+static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids, uint64_t Nt) {
     hipStream_t s = ctx->stream;
     Arena& ar = ctx->arena;
     const uint32_t N = c.ndocs;
     ar.used = 0;
+    ctx->run_N = N;
+    ctx->run_V = 0;
     mark(ctx, S_PREP);
     /* ---- buffers ---- */
     const uint64_t span = c.hi - c.lo;
@@ -369,17 +447,9 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
         LCHK(launch_plan_chunks(c, nchunks, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(),
                                 ctx->big_list.as<uint32_t>(), cnt + 6, s));
     /* K1 variant: the slot-keyed kernel (tokcount_vs.hip) needs a 16-byte aligned corpus
-     * base; TFIDF_K1=general / =ws select the older kernels (cross-checks, diagnostics) */
-    uint32_t not_ws_sep = 1;
-    if (nchunks && ctx->k1_mode == 3) {
-        LCHK(launch_docs_ws_sep(c, (uint32_t*)(cnt + 4), s));
-        HIPCHK(hipMemcpyAsync(&not_ws_sep, cnt + 4, 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-    }
+     * base; TFIDF_K1=general selects the general kernel (cross-checks) */
     const bool aligned = (((uintptr_t)c.bytes & 15u) == 0);
-    ctx->k1_fast = false;
     ctx->k1_vs = aligned && ctx->k1_mode == 0;
-    if (ctx->k1_mode == 3) ctx->k1_fast = (not_ws_sep == 0) && aligned;
     if (ctx->k1_vs && ctx->vcap > K1_VS_MAX_CAP) return TFIDF_E_CAPACITY;
     /* ---- K1 ---- */
     mark(ctx, S_TOKCOUNT);
@@ -410,8 +480,6 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     }
     if (nchunks && ctx->k1_vs)
         LCHK(launch_tokcount_vs(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
-    else if (nchunks && ctx->k1_fast)
-        LCHK(launch_tokcount_ws(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
     else if (nchunks)
         LCHK(launch_tokcount(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
     mark(ctx, S_VOCAB);
@@ -420,7 +488,7 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
         HIPCHK(hipStreamSynchronize(s));
         ctx->V = 0;
         ctx->npairs = 0;
-        return 0;
+        return 2;
     }
     /* the vocabulary's used-slot flags and count are enqueued before the host reads K1's
      * counters: one host round trip for both */
@@ -606,14 +674,28 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
                         ctx->rank_of_slot.as<uint32_t>(),
                         V <= 65536u ? ctx->rank16.as<uint16_t>() : nullptr, V, cap,
                         (uint32_t*)(cnt + 3), ctx->df_local.as<uint32_t>(), ar, s));
-    mark(ctx, S_EXCHANGE);
-    if (ctx->comm && ctx->nranks > 1) {
-        int rc = exchange_df(ctx, V);
-        if (rc) return rc;
-    } else {
-        ctx->Vg = V;
-        if (V) HIPCHK(hipMemcpyAsync(ctx->df_global.p, ctx->df_local.p, (size_t)V * 4, hipMemcpyDeviceToDevice, s));
+    ctx->run_V = V;
+    ctx->run_cap = cap;
+    ctx->run_R_total = R_total;
+    ctx->run_merged = merged_count;
+    /* the stages after the exchange take their scratch from what is left of the arena */
+    const size_t post_need = scan_scratch(Nt + 1) + (size_t)(Nt + 2) * 4 + 512 + scan_scratch(N);
+    if (ar.cap - ar.used < post_need) {
+        ar.peak = ar.used + post_need > ar.peak ? ar.used + post_need : ar.peak;
+        return 1;
     }
+    return 0;
+}
+
+/* The stages after the DF exchange: idf LUT, document order, score.  They never return 1
+ * (run_local checked their scratch before the exchange), so no rank can ever enter the
+ * collectives of a repeated attempt alone: every `return` below is an error or success. */
+static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
+    hipStream_t s = ctx->stream;
+    Arena& ar = ctx->arena;
+    const uint32_t N = ctx->run_N, V = ctx->run_V;
+    const uint64_t cap = ctx->run_cap, R_total = ctx->run_R_total;
+    unsigned long long* cnt = ctx->counters.as<unsigned long long>();
     /* ---- idf LUT: log(N/df) on the host's libm for each distinct df (TFIDF.c:243) ----
      * The distinct df values are listed on the device; their count K, the first
      * IDF_SPEC of them and the pair total P come back in ONE host round trip together
@@ -621,11 +703,11 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     mark(ctx, S_IDF);
     ENSURE(ctx->present, (Nt + 2) * 4);
     HIPCHK(hipMemsetAsync(ctx->present.p, 0, (Nt + 2) * 4, s));
-    LCHK(launch_df_mark(ctx->df_global.as<uint32_t>(), V, ctx->present.as<uint32_t>(), s));
-    LCHK(scan_excl_u32(ctx->present.as<uint32_t>(), ctx->present.as<uint32_t>(), Nt + 1, ar, s));
+    XCHK(launch_df_mark(ctx->df_global.as<uint32_t>(), V, ctx->present.as<uint32_t>(), s));
+    XCHK(scan_excl_u32(ctx->present.as<uint32_t>(), ctx->present.as<uint32_t>(), Nt + 1, ar, s));
     uint32_t* vals_dev = (uint32_t*)ar.get((size_t)(Nt + 2) * 4);
-    if (!vals_dev) return 1;
-    LCHK(launch_df_list(ctx->present.as<uint32_t>(), Nt + 1, vals_dev, s));
+    if (!vals_dev) return TFIDF_E_CAPACITY;   /* checked by run_local: not reachable */
+    XCHK(launch_df_list(ctx->present.as<uint32_t>(), Nt + 1, vals_dev, s));
     constexpr uint32_t IDF_SPEC = 16384;
     const uint32_t spec = (uint32_t)((Nt + 1) < IDF_SPEC ? (Nt + 1) : IDF_SPEC);
     std::vector<uint32_t> vals(spec);
@@ -638,10 +720,10 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     ENSURE(ctx->out_off, (size_t)N * 8 + 8);
     HIPCHK(hipStreamWaitEvent(s, ctx->ev_order, 0)); /* join the side stream's document order */
     ENSURE(ctx->doc_meta, (size_t)N * 16 + 16);
-    LCHK(launch_gather_meta(ctx->order, ctx->doc_npairs.as<uint32_t>(), ctx->doc_recoff.as<uint64_t>(),
+    XCHK(launch_gather_meta(ctx->order, ctx->doc_npairs.as<uint32_t>(), ctx->doc_recoff.as<uint64_t>(),
                             ctx->doc_size.as<uint32_t>(), ctx->doc_flags.as<uint8_t>(), N,
                             ctx->npairs_ord.as<uint64_t>(), ctx->doc_meta.as<uint4>(), s));
-    LCHK(scan_excl_u64(ctx->npairs_ord.as<uint64_t>(), ctx->out_off.as<uint64_t>(), N, ar, s));
+    XCHK(scan_excl_u64(ctx->npairs_ord.as<uint64_t>(), ctx->out_off.as<uint64_t>(), N, ar, s));
     uint64_t P = 0;
     HIPCHK(hipMemcpyAsync(&P, ctx->out_off.as<uint64_t>() + N, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -687,7 +769,7 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     a.out_term = ctx->out_term.as<uint32_t>();
     a.out_cnt = ctx->out_cnt.as<uint32_t>();
     a.out_score = ctx->out_score.as<double>();
-    LCHK(launch_score_order(a, s, ctx->stream2, ctx->ev_fork, ctx->ev_order));
+    XCHK(launch_score_order(a, s, ctx->stream2, ctx->ev_fork, ctx->ev_order));
     mark(ctx, S_NSTAGES);
     uint32_t st_end = 0;
     HIPCHK(hipMemcpyAsync(&st_end, cnt + 3, 4, hipMemcpyDeviceToHost, s));
@@ -699,16 +781,36 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     return 0;
 }
 
-extern "C" int tfidf_run(tfidf_ctx* ctx, const tfidf_corpus* in) {
-    if (!ctx || !in) return TFIDF_E_INVAL;
+/* One attempt of the pipeline: local stages, the DF exchange (with an attached
+ * transport every rank enters it, whatever its local status, see exchange_df), the
+ * stages after it.  Returns 0 on success, 1 to retry with grown capacities (with a
+ * transport: decided by all ranks together), <0 on error. */
+static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids, uint64_t Nt) {
+    int rc = run_local(ctx, c, dev_ids, Nt);
+    if (rc == 2) return 0;   /* timing ablation (single rank): stop after K1 */
+    mark(ctx, S_EXCHANGE);
+    if (ctx->xp) {
+        rc = exchange_df(ctx, rc, ctx->run_V);
+        if (rc) return rc;
+    } else {
+        if (rc) return rc;
+        ctx->Vg = ctx->run_V;
+        if (ctx->run_V)
+            HIPCHK(hipMemcpyAsync(ctx->df_global.p, ctx->df_local.p, (size_t)ctx->run_V * 4, hipMemcpyDeviceToDevice,
+                                  ctx->stream));
+    }
+    return run_post(ctx, Nt);
+}
+
+/* Host-side preparation of a run: argument checks, the host corpus copied to HBM. */
+static int run_prepare(tfidf_ctx* ctx, const tfidf_corpus* in, CorpusDev& c, const uint32_t*& dev_ids, uint64_t& Nt) {
     if (in->ndocs && !in->doc_off) return TFIDF_E_INVAL;
     if (in->nbytes && !in->bytes) return TFIDF_E_INVAL;
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     const uint32_t N = in->ndocs;
     const bool dev = (in->flags & TFIDF_CORPUS_DEVICE) != 0;
-    CorpusDev c{};
-    const uint32_t* dev_ids = nullptr;
+    dev_ids = nullptr;
     uint64_t lo = 0, hi = 0;
     if (dev) {
         c.bytes = in->bytes;
@@ -740,20 +842,35 @@ extern "C" int tfidf_run(tfidf_ctx* ctx, const tfidf_corpus* in) {
     c.ndocs = N;
     c.lo = lo;
     c.hi = hi;
-    const uint64_t Nt = in->ndocs_total ? in->ndocs_total : N;
+    Nt = in->ndocs_total ? in->ndocs_total : N;
     if (Nt < N || Nt > 0xFFFFFFFFull) return TFIDF_E_INVAL;
+    return TFIDF_OK;
+}
+
+extern "C" int tfidf_run(tfidf_ctx* ctx, const tfidf_corpus* in) {
+    if (!ctx) return TFIDF_E_INVAL;
     ctx->have_result = false;
     ctx->have_info = false;
     ctx->text_valid = false;
-    int rc = 1;
+    CorpusDev c{};
+    const uint32_t* dev_ids = nullptr;
+    uint64_t Nt = 0;
+    int rc = in ? run_prepare(ctx, in, c, dev_ids, Nt) : TFIDF_E_INVAL;
+    if (rc) {
+        /* a rank that fails before its first stage still takes part in the agreement, so
+         * its peers return TFIDF_E_PEER instead of waiting for it */
+        if (ctx->xp) (void)exchange_agree(ctx, rc, 0, nullptr);
+        return rc;
+    }
+    hipStream_t s = ctx->stream;
+    const uint32_t N = in->ndocs;
+    rc = 1;
     for (int attempt = 0; attempt < 8 && rc == 1; ++attempt) {
-        size_t need = ctx->arena.peak > ctx->arena_buf.cap ? ctx->arena.peak * 2 : ctx->arena_buf.cap;
-        /* N > 1: a retry decided by one rank after the DF exchange would re-enter the
-         * collectives alone; start with an arena the exchange and later stages cannot
-         * exhaust at the BASELINE sizes, so retries only happen before it (in step) */
-        if (ctx->nranks > 1 && need < (2ull << 30)) need = 2ull << 30;
-        if (arena_reset(ctx, need) != 0) return TFIDF_E_NOMEM;
-        rc = run_once(ctx, c, dev_ids, Nt);
+        const size_t need = ctx->arena.peak > ctx->arena_buf.cap ? ctx->arena.peak * 2 : ctx->arena_buf.cap;
+        const int arc = arena_reset(ctx, need);
+        /* with peers, an allocation failure is reported through the agreement as well */
+        rc = arc ? arc : run_once(ctx, c, dev_ids, Nt);
+        if (arc && ctx->xp) (void)exchange_agree(ctx, arc, 0, nullptr);
         if (rc == 1) { HIPCHK(hipStreamSynchronize(s)); HIPCHK(hipStreamSynchronize(ctx->stream2)); }
     }
     if (rc == 1) return TFIDF_E_CAPACITY;
@@ -863,7 +980,7 @@ extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info) {
     info->ms_tokcount = ctx->ms_stage[S_TOKCOUNT];
     for (int i = 0; i < S_NSTAGES; ++i) info->ms_stage[i] = ctx->ms_stage[i];
     info->nstages = S_NSTAGES;
-    info->flags = (ctx->k1_fast ? TFIDF_RUN_K1_FAST : 0u) | (ctx->k1_vs ? TFIDF_RUN_K1_VS : 0u);
+    info->flags = ctx->k1_vs ? TFIDF_RUN_K1_VS : 0u;
     return TFIDF_OK;
 }
 
@@ -980,12 +1097,17 @@ extern "C" int tfidf_fetch(tfidf_ctx* ctx, tfidf_result* r) {
 
 /* ----------------------------------------------------------------- ingest ----
  * ingest.cpp streams input/doc1..N into the context's host-input buffers (§8f row 2). */
-int tfidf_ctx_ingest_buffers(tfidf_ctx* ctx, uint64_t nbytes, uint32_t ndocs, uint8_t** dbytes, uint64_t** doff) {
+int tfidf_ctx_ingest_buffers(tfidf_ctx* ctx, uint64_t nbytes, uint32_t ndocs, uint8_t** dbytes, uint64_t** doff,
+                             uint32_t** dids) {
     HIPCHK(hipSetDevice(ctx->device));
     ENSURE(ctx->in_bytes, nbytes + 64);
     ENSURE(ctx->in_off, ((size_t)ndocs + 1) * 8);
     *dbytes = ctx->in_bytes.as<uint8_t>();
     *doff = ctx->in_off.as<uint64_t>();
+    if (dids) {
+        ENSURE(ctx->in_ids, (size_t)ndocs * 4 + 4);
+        *dids = ctx->in_ids.as<uint32_t>();
+    }
     return TFIDF_OK;
 }
 

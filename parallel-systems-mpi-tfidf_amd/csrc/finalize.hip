@@ -1346,9 +1346,15 @@ int launch_keys_by_rank(const uint4* vkeys, const uint32_t* slot_of_rank, uint32
     k_keys_by_rank<<<grid_for(V), NT, 0, s>>>(vkeys, slot_of_rank, V, out);
     return ok();
 }
+/* a run head of the sorted all-gathered keys starts a union id; the padding key of ranks
+ * with fewer terms than the largest (all bytes 0xEE: byte 15 of a real key is 0x00, 0x09
+ * or 0xFF) is not a term and gets no id */
 __global__ void k_union_heads(const uint4* __restrict__ k, uint64_t n, uint32_t* __restrict__ head) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) head[i] = (i == 0 || !u128_eq(k[i], k[i - 1])) ? 1u : 0u;
+    if (i >= n) return;
+    const uint4 x = k[i];
+    const bool pad = x.x == 0xEEEEEEEEu && x.y == 0xEEEEEEEEu && x.z == 0xEEEEEEEEu && x.w == 0xEEEEEEEEu;
+    head[i] = (!pad && (i == 0 || !u128_eq(x, k[i - 1]))) ? 1u : 0u;
 }
 int launch_union_heads(const uint4* sorted, uint64_t n, uint32_t* head, hipStream_t s) {
     if (!n) return 0;
@@ -1394,6 +1400,19 @@ int launch_scatter_df(const uint32_t* df_local, const uint32_t* grank, uint32_t 
 int launch_gather_df(const uint32_t* dfv, const uint32_t* grank, uint32_t V, uint32_t* df_out, hipStream_t s) {
     if (!V) return 0;
     k_gather_df<<<grid_for(V), NT, 0, s>>>(dfv, grank, V, df_out);
+    return ok();
+}
+/* in-process transport's all-reduce: out[i] = sum of rows[r * n + i] over r */
+__global__ void k_sum_rows_u32(const uint32_t* __restrict__ rows, uint32_t nrows, uint64_t n, uint32_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t s = 0;
+    for (uint32_t r = 0; r < nrows; ++r) s += rows[(uint64_t)r * n + i];
+    out[i] = s;
+}
+int launch_sum_rows_u32(const uint32_t* rows, uint32_t nrows, uint64_t n, uint32_t* out, hipStream_t s) {
+    if (!n) return 0;
+    k_sum_rows_u32<<<grid_for(n), NT, 0, s>>>(rows, nrows, n, out);
     return ok();
 }
 

@@ -1,0 +1,280 @@
+/*
+ * group.cpp — several GPU shards driven by one process (the drop-in for
+ * `mpirun -np P ./TFIDF`, TFIDF.c:82-92,125-130), and the two rank transports of
+ * xport.h.
+ *
+ *   tfidf_group_open   opens one context per rank (rank r on devices[r]) and connects
+ *                      them: ncclCommInitAll when every rank has its own GPU (RCCL over
+ *                      xGMI), the in-process LocalXport when a device carries several
+ *                      ranks (or TFIDF_GROUP_LOCAL is asked for).
+ *   tfidf_group_run    one host thread per rank, each runs tfidf_run on its shard; the
+ *                      ranks meet only inside the DF exchange (engine.cpp).
+ *   tfidf_group_write_output
+ *                      every rank formats its lines on its GPU (in parallel), then the
+ *                      texts are written in rank order — shards are contiguous ranges of
+ *                      the "docN@" order, so this is the reference's gather + qsort
+ *                      (TFIDF.c:253-273) without either.
+ */
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <condition_variable>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/tfidf.h"
+#include "kernels.h"
+#include "xport.h"
+
+namespace {
+
+/* ------------------------------------------------------------------ RCCL -- */
+
+struct RcclXport final : Xport {
+    ncclComm_t comm = nullptr;
+    int device = 0;
+    uint64_t* dwords = nullptr;   /* 2 (send) + 2 * nranks (recv) */
+    ~RcclXport() override {
+        if (comm) (void)ncclCommDestroy(comm);
+        if (dwords) (void)hipFree(dwords);
+    }
+    int words(const uint64_t mine[2], uint64_t* all, hipStream_t s) override {
+        if (!comm) return TFIDF_E_STATE;
+        if (!dwords && hipMalloc((void**)&dwords, 16 * (size_t)(nranks + 1)) != hipSuccess) return TFIDF_E_NOMEM;
+        if (hipMemcpyAsync(dwords, mine, 16, hipMemcpyHostToDevice, s) != hipSuccess) return TFIDF_E_HIP;
+        if (ncclAllGather(dwords, dwords + 2, 2, ncclUint64, comm, s) != ncclSuccess) return TFIDF_E_RCCL;
+        if (hipMemcpyAsync(all, dwords + 2, 16 * (size_t)nranks, hipMemcpyDeviceToHost, s) != hipSuccess)
+            return TFIDF_E_HIP;
+        return hipStreamSynchronize(s) == hipSuccess ? TFIDF_OK : TFIDF_E_HIP;
+    }
+    int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+        if (!comm) return TFIDF_E_STATE;
+        return ncclAllGather(send, recv, bytes, ncclUint8, comm, s) == ncclSuccess ? TFIDF_OK : TFIDF_E_RCCL;
+    }
+    int allreduce_sum_u32(uint32_t* buf, size_t n, hipStream_t s) override {
+        if (!comm) return TFIDF_E_STATE;
+        return ncclAllReduce(buf, buf, n, ncclUint32, ncclSum, comm, s) == ncclSuccess ? TFIDF_OK : TFIDF_E_RCCL;
+    }
+    void abort() override {
+        if (comm) { (void)ncclCommAbort(comm); comm = nullptr; }
+    }
+    const char* name() const override { return "rccl"; }
+};
+
+/* -------------------------------------------------------------- in-process -- */
+
+struct Hub {
+    int n = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    bool poisoned = false;
+    std::vector<const void*> ptr;
+    std::vector<int> dev;
+    std::vector<uint64_t> w;
+    /* returns false when a rank aborted */
+    bool barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        if (poisoned) return false;
+        const uint64_t g = gen;
+        if (++arrived == n) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+            return true;
+        }
+        cv.wait(lk, [&] { return gen != g || poisoned; });
+        return gen != g;   /* completed, or released by a poisoning rank */
+    }
+    void poison() {
+        std::lock_guard<std::mutex> lk(mu);
+        poisoned = true;
+        cv.notify_all();
+    }
+};
+
+struct LocalXport final : Xport {
+    Hub* hub = nullptr;
+    int device = 0;
+    uint32_t* tmp = nullptr;
+    size_t tmp_cap = 0;
+    ~LocalXport() override {
+        if (tmp) (void)hipFree(tmp);
+    }
+    int words(const uint64_t mine[2], uint64_t* all, hipStream_t s) override {
+        (void)s;
+        hub->w[2 * rank] = mine[0];
+        hub->w[2 * rank + 1] = mine[1];
+        if (!hub->barrier()) return TFIDF_E_PEER;
+        memcpy(all, hub->w.data(), 16 * (size_t)nranks);
+        if (!hub->barrier()) return TFIDF_E_PEER;   /* nobody rewrites w before all have read */
+        return TFIDF_OK;
+    }
+    int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+        /* the send buffer is complete on this stream; peers copy from it after the barrier */
+        if (hipStreamSynchronize(s) != hipSuccess) { abort(); return TFIDF_E_HIP; }
+        hub->ptr[rank] = send;
+        if (!hub->barrier()) return TFIDF_E_PEER;
+        int rc = TFIDF_OK;
+        for (int r = 0; r < nranks && !rc && bytes; ++r) {
+            uint8_t* dst = (uint8_t*)recv + (size_t)r * bytes;
+            const hipError_t e = hub->dev[r] == device
+                ? hipMemcpyAsync(dst, hub->ptr[r], bytes, hipMemcpyDeviceToDevice, s)
+                : hipMemcpyPeerAsync(dst, device, hub->ptr[r], hub->dev[r], bytes, s);
+            if (e != hipSuccess) rc = TFIDF_E_HIP;
+        }
+        if (hipStreamSynchronize(s) != hipSuccess) rc = TFIDF_E_HIP;
+        if (rc) { abort(); return rc; }
+        /* every rank has copied every send buffer before any of them is reused */
+        if (!hub->barrier()) return TFIDF_E_PEER;
+        return TFIDF_OK;
+    }
+    int allreduce_sum_u32(uint32_t* buf, size_t n, hipStream_t s) override {
+        if (!n) return hub->barrier() ? TFIDF_OK : TFIDF_E_PEER;
+        const size_t need = n * (size_t)nranks * 4;
+        if (need > tmp_cap) {
+            if (tmp) (void)hipFree(tmp);
+            tmp = nullptr;
+            tmp_cap = 0;
+            if (hipMalloc((void**)&tmp, need) != hipSuccess) { abort(); return TFIDF_E_NOMEM; }
+            tmp_cap = need;
+        }
+        int rc = allgather(buf, tmp, n * 4, s);
+        if (rc) return rc;
+        if (launch_sum_rows_u32(tmp, (uint32_t)nranks, n, buf, s)) { abort(); return TFIDF_E_HIP; }
+        return TFIDF_OK;
+    }
+    void abort() override { hub->poison(); }
+    const char* name() const override { return "local"; }
+};
+
+}  // namespace
+
+Xport* make_rccl_xport(void* nccl_comm, int rank, int nranks, int device) {
+    RcclXport* x = new RcclXport();
+    x->comm = (ncclComm_t)nccl_comm;
+    x->rank = rank;
+    x->nranks = nranks;
+    x->device = device;
+    return x;
+}
+
+struct tfidf_group {
+    int n = 0;
+    bool local = false;
+    std::vector<tfidf_ctx*> ctx;
+    Hub* hub = nullptr;
+};
+
+extern "C" {
+
+int tfidf_group_open(int nranks, const int* devices, uint32_t flags, tfidf_group** out) {
+    if (!out || nranks < 1 || nranks > 1024) return TFIDF_E_INVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return TFIDF_E_NODEV;
+    std::vector<int> dev((size_t)nranks);
+    for (int r = 0; r < nranks; ++r) {
+        dev[r] = devices ? devices[r] : r;
+        if (dev[r] < 0 || dev[r] >= ndev) return TFIDF_E_NODEV;
+    }
+    bool distinct = true;
+    for (int a = 0; a < nranks && distinct; ++a)
+        for (int b = a + 1; b < nranks; ++b)
+            if (dev[a] == dev[b]) { distinct = false; break; }
+    tfidf_group* g = new tfidf_group();
+    g->n = nranks;
+    g->local = !distinct || (flags & TFIDF_GROUP_LOCAL) != 0;
+    g->ctx.assign((size_t)nranks, nullptr);
+    int rc = TFIDF_OK;
+    for (int r = 0; r < nranks && !rc; ++r) rc = tfidf_open(dev[r], &g->ctx[r]);
+    if (!rc && nranks > 1 && g->local) {
+        g->hub = new Hub();
+        g->hub->n = nranks;
+        g->hub->ptr.assign((size_t)nranks, nullptr);
+        g->hub->dev = dev;
+        g->hub->w.assign(2 * (size_t)nranks, 0);
+        for (int r = 0; r < nranks && !rc; ++r) {
+            LocalXport* x = new LocalXport();
+            x->hub = g->hub;
+            x->rank = r;
+            x->nranks = nranks;
+            x->device = dev[r];
+            rc = tfidf_ctx_attach_xport(g->ctx[r], x);
+        }
+    } else if (!rc) {
+        /* one RCCL communicator per GPU of the clique (a 1-rank group gets one too, so the
+         * exchange path is the same at every size) */
+        std::vector<ncclComm_t> comms((size_t)nranks, nullptr);
+        if (ncclCommInitAll(comms.data(), nranks, dev.data()) != ncclSuccess) rc = TFIDF_E_RCCL;
+        for (int r = 0; r < nranks && !rc; ++r) {
+            rc = tfidf_ctx_attach_xport(g->ctx[r], make_rccl_xport(comms[r], r, nranks, dev[r]));
+            comms[r] = nullptr;
+        }
+        for (ncclComm_t c : comms)
+            if (c) (void)ncclCommDestroy(c);
+    }
+    if (rc) {
+        tfidf_group_close(g);
+        return rc;
+    }
+    *out = g;
+    return TFIDF_OK;
+}
+
+int tfidf_group_size(const tfidf_group* g) { return g ? g->n : 0; }
+
+tfidf_ctx* tfidf_group_ctx(tfidf_group* g, int rank) {
+    return (g && rank >= 0 && rank < g->n) ? g->ctx[rank] : nullptr;
+}
+
+int tfidf_group_run(tfidf_group* g, const tfidf_corpus* shards) {
+    if (!g || !shards) return TFIDF_E_INVAL;
+    std::vector<int> rc((size_t)g->n, TFIDF_OK);
+    std::vector<std::thread> th;
+    for (int r = 1; r < g->n; ++r) th.emplace_back([&, r] { rc[r] = tfidf_run(g->ctx[r], &shards[r]); });
+    rc[0] = tfidf_run(g->ctx[0], &shards[0]);
+    for (auto& t : th) t.join();
+    /* the first rank's own error; TFIDF_E_PEER only when no rank has a better reason */
+    int peer = TFIDF_OK;
+    for (int r = 0; r < g->n; ++r) {
+        if (rc[r] == TFIDF_E_PEER) peer = TFIDF_E_PEER;
+        else if (rc[r]) return rc[r];
+    }
+    return peer;
+}
+
+int tfidf_group_write_output(tfidf_group* g, const char* path) {
+    if (!g || !path) return TFIDF_E_INVAL;
+    std::vector<int> rc((size_t)g->n, TFIDF_OK);
+    std::vector<uint64_t> nb((size_t)g->n, 0);
+    {   /* every GPU formats its shard's lines at once */
+        std::vector<std::thread> th;
+        for (int r = 1; r < g->n; ++r) th.emplace_back([&, r] { rc[r] = tfidf_format(g->ctx[r], &nb[r]); });
+        rc[0] = tfidf_format(g->ctx[0], &nb[0]);
+        for (auto& t : th) t.join();
+    }
+    for (int r = 0; r < g->n; ++r)
+        if (rc[r]) return rc[r];
+    for (int r = 0; r < g->n; ++r) {
+        const int e = tfidf_write_output_gpu(g->ctx[r], path, r > 0);
+        if (e) return e;
+    }
+    return TFIDF_OK;
+}
+
+void tfidf_group_close(tfidf_group* g) {
+    if (!g) return;
+    for (tfidf_ctx* c : g->ctx)
+        if (c) tfidf_close(c);
+    delete g->hub;
+    delete g;
+}
+
+}  // extern "C"

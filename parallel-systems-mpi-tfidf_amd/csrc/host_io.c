@@ -28,6 +28,7 @@ const char* tfidf_strerror(int s) {
     case TFIDF_E_OUTPUT: return "Error Opening File: output.txt";
     case TFIDF_E_CAPACITY: return "capacity exceeded";
     case TFIDF_E_STATE: return "call out of order";
+    case TFIDF_E_PEER: return "another rank failed";
     default: return "unknown error";
     }
 }

@@ -89,11 +89,6 @@ int launch_tokcount_vs(const CorpusDev& c, const uint64_t* chunk_start, const ui
                        uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s);
 #define K1_VS_MAX_CAP (1ull << 28)
 
-/* K1 fast path for whitespace-separated documents (tokcount_ws.hip) */
-int launch_docs_ws_sep(const CorpusDev& c, uint32_t* flag, hipStream_t s);
-int launch_tokcount_ws(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc, uint64_t c0,
-                       uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s);
-
 /* vocabulary finalisation */
 int launch_vocab_flags(const VocabDev& v, uint64_t cap, uint32_t* flags, hipStream_t s);
 int launch_vocab_compact(const VocabDev& v, uint64_t cap, const uint32_t* dense_of_slot, const CorpusDev& c,

@@ -1,0 +1,53 @@
+/*
+ * xport.h — the collectives of the DF exchange, behind one small interface.
+ *
+ * The reference combines per-rank DF with MPI_Reduce(CustomReduce) + MPI_Bcast
+ * (TFIDF.c:209-222,291-326) between OS processes.  Here a context (one GPU shard) talks
+ * to its peers through an Xport:
+ *
+ *   RcclXport   ncclAllGather / ncclAllReduce over xGMI: one communicator rank per GPU,
+ *               either one process per GPU (tfidf_comm_init, torch.distributed launch) or
+ *               one process driving every GPU (tfidf_group_open, ncclCommInitAll).
+ *   LocalXport  contexts of one process that share a device (tfidf_group_open with a
+ *               device listed twice, e.g. K shards on the 1-GPU test box): the same
+ *               operations as device-to-device copies between the contexts' buffers, with
+ *               host barriers.  The engine code above the interface is identical, so the
+ *               union / lookup / scatter / gather kernels and the status agreement run
+ *               unchanged with K > 1 ranks on one GPU.
+ *
+ * Every operation is collective: all ranks call it in the same order.  `words` is the
+ * host-level agreement step (status + sizes), the device operations are stream-ordered.
+ */
+#ifndef TFIDF_XPORT_H
+#define TFIDF_XPORT_H
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+struct tfidf_ctx;
+
+struct Xport {
+    int rank = 0, nranks = 1;
+    virtual ~Xport() {}
+    /* host all-gather of two u64 per rank: all[2 * r + k] = rank r's mine[k] */
+    virtual int words(const uint64_t mine[2], uint64_t* all, hipStream_t s) = 0;
+    /* device all-gather: recv[r * bytes ...] = rank r's send[0 .. bytes) */
+    virtual int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
+    /* in-place device sum of n u32 over the ranks */
+    virtual int allreduce_sum_u32(uint32_t* buf, size_t n, hipStream_t s) = 0;
+    /* a rank failed between collectives: release the peers (they return errors) */
+    virtual void abort() = 0;
+    virtual const char* name() const = 0;
+};
+
+/* engine.cpp: attach (and take ownership of) an Xport; nullptr detaches */
+int tfidf_ctx_attach_xport(tfidf_ctx* ctx, Xport* xp);
+int tfidf_ctx_device(const tfidf_ctx* ctx);
+hipStream_t tfidf_ctx_stream(const tfidf_ctx* ctx);
+
+/* group.cpp */
+Xport* make_rccl_xport(void* nccl_comm, int rank, int nranks, int device);   /* takes the comm */
+int launch_sum_rows_u32(const uint32_t* rows, uint32_t nrows, uint64_t n, uint32_t* out, hipStream_t s);
+
+#endif

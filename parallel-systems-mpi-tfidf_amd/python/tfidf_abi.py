@@ -28,8 +28,12 @@ EXPORTS = [
     "tfidf_stage_name", "tfidf_set_timing", "tfidf_write_output", "tfidf_print_jobs",
     "tfidf_ingest_dir", "tfidf_free", "tfidf_synth_host", "tfidf_synth_device",
     "tfidf_format", "tfidf_copy_text", "tfidf_write_output_gpu", "tfidf_format_f64",
-    "tfidf_ingest_dir_device", "tfidf_hbm_probe",
+    "tfidf_ingest_dir_device", "tfidf_hbm_probe", "tfidf_group_open", "tfidf_group_size", "tfidf_group_ctx",
+    "tfidf_group_run", "tfidf_group_write_output", "tfidf_group_close", "tfidf_plan_dir", "tfidf_plan_free",
+    "tfidf_ingest_shard_device", "tfidf_doc_name_order", "tfidf_shard_split",
 ]
+TFIDF_GROUP_LOCAL = 1
+E_PEER = -11
 
 
 class Corpus(C.Structure):
@@ -57,6 +61,14 @@ class RunInfo(C.Structure):
         ("nterms_global", C.c_uint32), ("nchunks", C.c_uint64), ("partial_records", C.c_uint64),
         ("ndocs", C.c_uint32), ("vocab_capacity", C.c_uint32), ("ms_total", C.c_double),
         ("ms_tokcount", C.c_double), ("ms_stage", C.c_double * 16), ("nstages", C.c_uint32), ("flags", C.c_uint32),
+    ]
+
+
+class DirPlan(C.Structure):
+    _fields_ = [
+        ("ndocs", C.c_uint32), ("nshards", C.c_uint32), ("doc_ids", C.POINTER(C.c_uint32)),
+        ("doc_bytes", C.POINTER(C.c_uint64)), ("shard_first", C.POINTER(C.c_uint32)),
+        ("shard_bytes", C.POINTER(C.c_uint64)),
     ]
 
 
@@ -101,6 +113,21 @@ def lib() -> C.CDLL:
         L.tfidf_ingest_dir_device.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.POINTER(Corpus),
                                               C.POINTER(C.c_uint32), C.POINTER(IngestInfo)]
         L.tfidf_hbm_probe.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        L.tfidf_group_open.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p)]
+        L.tfidf_group_size.argtypes = [C.c_void_p]
+        L.tfidf_group_ctx.argtypes = [C.c_void_p, C.c_int]
+        L.tfidf_group_ctx.restype = C.c_void_p
+        L.tfidf_group_run.argtypes = [C.c_void_p, C.c_void_p]
+        L.tfidf_group_write_output.argtypes = [C.c_void_p, C.c_char_p]
+        L.tfidf_group_close.argtypes = [C.c_void_p]
+        L.tfidf_group_close.restype = None
+        L.tfidf_plan_dir.argtypes = [C.c_char_p, C.c_uint32, C.c_int, C.POINTER(DirPlan), C.POINTER(C.c_uint32)]
+        L.tfidf_plan_free.argtypes = [C.POINTER(DirPlan)]
+        L.tfidf_plan_free.restype = None
+        L.tfidf_ingest_shard_device.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(DirPlan), C.c_uint32, C.c_int,
+                                                C.POINTER(Corpus), C.POINTER(C.c_uint32), C.POINTER(IngestInfo)]
+        L.tfidf_doc_name_order.argtypes = [C.c_uint32, C.c_void_p]
+        L.tfidf_shard_split.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
         _lib = L
     return _lib
 
@@ -138,16 +165,19 @@ def synth_host(seed: int, V: int, mode: int, cdf, doc_ids, ntok):
 class Engine:
     """One GPU context (one HIP stream; optional RCCL communicator)."""
 
-    def __init__(self, device: int = 0):
-        h = C.c_void_p()
-        _chk(lib().tfidf_open(device, C.byref(h)), "tfidf_open")
-        self.h = h
+    def __init__(self, device: int = 0, handle=None):
+        self._owned = handle is None
+        if handle is None:
+            h = C.c_void_p()
+            _chk(lib().tfidf_open(device, C.byref(h)), "tfidf_open")
+            handle = h
+        self.h = handle if isinstance(handle, C.c_void_p) else C.c_void_p(handle)
         self._keep = None
 
     def close(self):
-        if self.h:
+        if self.h and self._owned:
             lib().tfidf_close(self.h)
-            self.h = None
+        self.h = None
 
     def __enter__(self):
         return self
@@ -276,6 +306,93 @@ class Engine:
             return out
         finally:
             lib().tfidf_result_free(C.byref(r))
+
+
+class Group:
+    """Several shards in this process (tfidf_group_*): rank r on devices[r]; RCCL when
+    every rank has its own GPU, the in-process transport when a device is shared (or
+    local=True).  Every run is collective over all ranks."""
+
+    def __init__(self, nranks: int, devices=None, local: bool = False):
+        dev = None if devices is None else (C.c_int * nranks)(*devices)
+        h = C.c_void_p()
+        _chk(lib().tfidf_group_open(nranks, dev, TFIDF_GROUP_LOCAL if local else 0, C.byref(h)), "tfidf_group_open")
+        self.h = h
+        self.n = nranks
+        self.ranks = [Engine(handle=lib().tfidf_group_ctx(h, r)) for r in range(nranks)]
+        self._keep = None
+
+    def close(self):
+        if self.h:
+            lib().tfidf_group_close(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def run(self, shards):
+        """shards: list of Corpus (one per rank)."""
+        arr = (Corpus * self.n)(*shards)
+        _chk(lib().tfidf_group_run(self.h, arr), "tfidf_group_run")
+
+    def run_host(self, shards):
+        """shards: list of (data, doc_off, doc_ids, ndocs_total) host arrays, one per rank."""
+        cs, keep = [], []
+        for data, off, ids, nt in shards:
+            data = np.ascontiguousarray(data, dtype=np.uint8)
+            off = np.ascontiguousarray(off, dtype=np.uint64)
+            ids = None if ids is None else np.ascontiguousarray(ids, dtype=np.uint32)
+            c = Corpus()
+            c.bytes = data.ctypes.data if len(data) else None
+            c.nbytes = len(data)
+            c.doc_off = off.ctypes.data
+            c.doc_ids = None if ids is None else ids.ctypes.data
+            c.ndocs = len(off) - 1
+            c.flags = 0
+            c.ndocs_total = nt
+            cs.append(c)
+            keep.append((data, off, ids))
+        self._keep = keep
+        self.run(cs)
+
+    def write_output(self, path: str):
+        _chk(lib().tfidf_group_write_output(self.h, path.encode()), "tfidf_group_write_output")
+
+
+def plan_dir(path: str, nshards: int, threads: int = 0) -> dict:
+    """tfidf_plan_dir: byte-balanced "docN@"-ordered shards of an input directory."""
+    p, bad = DirPlan(), C.c_uint32(0)
+    rc = lib().tfidf_plan_dir(path.encode(), nshards, threads, C.byref(p), C.byref(bad))
+    if rc:
+        e = TfidfError(rc, "tfidf_plan_dir")
+        e.bad_doc, e.ndocs = bad.value, p.ndocs
+        raise e
+    try:
+        N = int(p.ndocs)
+        ids = np.ctypeslib.as_array(p.doc_ids, shape=(N,)).copy() if N else np.zeros(0, np.uint32)
+        nb = np.ctypeslib.as_array(p.doc_bytes, shape=(N,)).copy() if N else np.zeros(0, np.uint64)
+        first = np.ctypeslib.as_array(p.shard_first, shape=(nshards + 1,)).copy()
+        sb = np.ctypeslib.as_array(p.shard_bytes, shape=(nshards,)).copy()
+        return {"ndocs": N, "doc_ids": ids, "doc_bytes": nb, "shard_first": first, "shard_bytes": sb}
+    finally:
+        lib().tfidf_plan_free(C.byref(p))
+
+
+def doc_name_order(n: int) -> np.ndarray:
+    out = np.zeros(max(n, 1), dtype=np.uint32)
+    _chk(lib().tfidf_doc_name_order(n, out.ctypes.data), "tfidf_doc_name_order")
+    return out[:n]
+
+
+def shard_split(sizes, nshards: int) -> np.ndarray:
+    sizes = np.ascontiguousarray(sizes, dtype=np.uint64)
+    first = np.zeros(nshards + 1, dtype=np.uint32)
+    _chk(lib().tfidf_shard_split(sizes.ctypes.data if len(sizes) else None, len(sizes), nshards, first.ctypes.data),
+         "tfidf_shard_split")
+    return first
 
 
 def format_lines(res: dict) -> bytes:

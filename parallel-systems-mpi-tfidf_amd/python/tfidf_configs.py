@@ -65,12 +65,34 @@ def doc_name_key(ids: np.ndarray) -> np.ndarray:
     return key
 
 
+def shard_cuts(weights, nshards: int) -> np.ndarray:
+    """Balanced contiguous cut of a sequence (the rule of tfidf_shard_split in
+    csrc/ingest.cpp): cut r is the prefix-sum position nearest to r * total / nshards, so
+    every shard weighs at most total / nshards + the heaviest element."""
+    w = np.asarray(weights, dtype=np.uint64)
+    pre = np.zeros(len(w) + 1, dtype=np.uint64)
+    pre[1:] = np.cumsum(w, dtype=np.uint64)
+    total = int(pre[-1])
+    first = np.zeros(nshards + 1, dtype=np.int64)
+    for r in range(1, nshards):
+        target = (total * r) // nshards
+        i = int(np.searchsorted(pre, np.uint64(target), side="left"))
+        i = min(i, len(w))
+        if i > 0 and target - int(pre[i - 1]) < int(pre[i]) - target:
+            i -= 1
+        first[r] = max(i, first[r - 1])
+    first[nshards] = len(w)
+    return first
+
+
 def plan(name: str, scale: float = 1.0, rank: int = 0, nranks: int = 1, weak: bool = False, vocab: int = 0):
     """Returns dict(doc_ids, ntok, cdf, V, mode, seed, ndocs_total).
 
     nranks > 1: documents are sharded in contiguous "docN" strcmp-order ranges, so the
-    concatenation of the shards' outputs is the global output.  weak=True grows the
-    corpus with nranks (fixed per-GPU work); otherwise the corpus is split.
+    concatenation of the shards' outputs is the global output, balanced by bytes (SURVEY
+    §8e; a document's bytes are its token count times the generator's bytes per token,
+    so the cut is taken over token counts).  weak=True grows the corpus with nranks
+    (fixed per-GPU work); otherwise (strong) the config's corpus is split.
     """
     cfg = dict(CONFIGS[name])
     seed = cfg["seed"]
@@ -101,8 +123,7 @@ def plan(name: str, scale: float = 1.0, rank: int = 0, nranks: int = 1, weak: bo
     ndocs_total = len(ids)
     if nranks > 1:
         order = np.argsort(doc_name_key(ids), kind="stable")
-        lo = (len(ids) * rank) // nranks
-        hi = (len(ids) * (rank + 1)) // nranks
-        sel = order[lo:hi]
+        first = shard_cuts(ntok[order], nranks)
+        sel = order[first[rank]:first[rank + 1]]
         ids, ntok = ids[sel], ntok[sel]
     return dict(doc_ids=ids, ntok=ntok, cdf=cdf, V=V, mode=mode, seed=seed, ndocs_total=ndocs_total)

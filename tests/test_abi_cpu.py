@@ -120,3 +120,71 @@ def test_ingest_dir_contract():
         lib.tfidf_free.argtypes = [C.c_void_p]
         lib.tfidf_free(pb)
         lib.tfidf_free(po)
+
+
+def test_doc_name_order_is_strcmp_order():
+    """tfidf_doc_name_order (the shard plan's document order): "docN@" strcmp order."""
+    for n in (1, 9, 10, 12, 100, 2345):
+        got = tfidf_abi.doc_name_order(n).tolist()
+        assert got == sorted(range(1, n + 1), key=lambda i: b"doc%d@" % i)
+
+
+def test_shard_split_is_byte_balanced():
+    """tfidf_shard_split == the Python planner's rule; every shard holds at most
+    total / K + the largest document, shards are contiguous and cover all."""
+    rng = np.random.default_rng(5)
+    cases = [rng.integers(0, 1000, 500), rng.integers(0, 10, 50), np.array([5, 1, 1, 1, 10, 1, 1]),
+             np.array([100_000_000] * 4 + [600] * 5000), np.zeros(7, np.int64), np.array([3])]
+    for sizes in cases:
+        sizes = sizes.astype(np.uint64)
+        for K in (1, 2, 3, 4, 8):
+            first = tfidf_abi.shard_split(sizes, K)
+            assert first.tolist() == tfidf_configs.shard_cuts(sizes, K).tolist()
+            assert first[0] == 0 and first[-1] == len(sizes) and np.all(np.diff(first.astype(np.int64)) >= 0)
+            total = int(sizes.sum())
+            big = int(sizes.max()) if len(sizes) else 0
+            for r in range(K):
+                b = int(sizes[first[r]:first[r + 1]].sum())
+                assert b <= total / K + big
+
+
+def test_c5_plan_balances_the_100mb_documents():
+    """c5 at 8 shards (4 x 100 MB among 1e6 small documents): token-balanced shards."""
+    sh = [tfidf_configs.plan("c5", scale=0.02, rank=r, nranks=8) for r in range(8)]
+    tok = [int(s["ntok"].sum()) for s in sh]
+    big = max(int(s["ntok"].max()) for s in sh)
+    assert max(tok) <= sum(tok) / 8 + big
+    ids = np.concatenate([s["doc_ids"] for s in sh])
+    keys = tfidf_configs.doc_name_key(ids)
+    assert np.all(np.diff(keys.astype(np.int64)) > 0)
+
+
+def test_plan_dir_contract():
+    """tfidf_plan_dir (host only): N counts every entry, the error contract of TFIDF.c:
+    100-103 / 134-138, "docN@" order, byte-balanced shards."""
+    with tempfile.TemporaryDirectory() as td:
+        try:
+            tfidf_abi.plan_dir(os.path.join(td, "nope"), 2)
+            raise AssertionError("expected an error")
+        except tfidf_abi.TfidfError as e:
+            assert e.rc == -6
+        d = os.path.join(td, "input")
+        os.makedirs(d)
+        sizes = [5, 0, 300, 7, 1, 90, 44, 3, 2, 20, 11, 8]
+        for i, n in enumerate(sizes, 1):
+            with open(os.path.join(d, f"doc{i}"), "wb") as f:
+                f.write(b"x" * n)
+        os.makedirs(os.path.join(d, ".hidden"))
+        try:
+            tfidf_abi.plan_dir(d, 2)
+            raise AssertionError("expected an error")
+        except tfidf_abi.TfidfError as e:
+            assert e.rc == -7 and e.bad_doc == 13 and e.ndocs == 13
+        os.rmdir(os.path.join(d, ".hidden"))
+        p = tfidf_abi.plan_dir(d, 3)
+        assert p["ndocs"] == 12
+        assert p["doc_ids"].tolist() == sorted(range(1, 13), key=lambda i: b"doc%d@" % i)
+        assert p["doc_bytes"].tolist() == [sizes[i - 1] for i in p["doc_ids"].tolist()]
+        f = p["shard_first"]
+        assert f.tolist() == tfidf_abi.shard_split(p["doc_bytes"], 3).tolist()
+        assert [int(p["doc_bytes"][f[r]:f[r + 1]].sum()) for r in range(3)] == p["shard_bytes"].tolist()

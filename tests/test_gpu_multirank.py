@@ -1,0 +1,193 @@
+"""GPU parity of the multi-shard product path (engine.cpp exchange_df, group.cpp).
+
+K shards of one corpus run through tfidf_group_* on K contexts.  On the one-GPU test box
+the contexts share device 0 and exchange through the in-process transport (xport.h): the
+engine code is the one the RCCL clique runs — the status/size agreement, the padded key
+all-gather, the union radix sort, k_union_heads / k_union_lookup, the DF scatter, the
+all-reduce and the gather.  Against the single-rank oracle (TFIDF.c:209-222,291-326 DF
+combine; :253-273 gather + sort):
+  * the shards' GPU-formatted texts, concatenated in rank order, are the oracle's
+    output.txt byte for byte;
+  * every pair's count, docSize and global DF, and every score, are bit-exact;
+  * every rank reports the same global vocabulary size = the oracle's distinct terms.
+The 1-rank RCCL communicator case runs the same exchange with ncclAllGather /
+ncclAllReduce (no `nranks > 1` shortcut any more)."""
+import os
+import shutil
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+import oracle_py
+import tfidf_abi
+import tfidf_configs
+from conftest import GOLDEN
+from helpers import assert_same_result, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _shards(cfg, scale, K):
+    shards = []
+    for r in range(K):
+        p = tfidf_configs.plan(cfg, scale=scale, rank=r, nranks=K)
+        d, o = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
+        shards.append((d, o, p["doc_ids"], p["ndocs_total"]))
+    return shards
+
+
+def _full(cfg, scale):
+    p = tfidf_configs.plan(cfg, scale=scale)
+    d, o = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
+    return oracle_py.run(d, o, p["doc_ids"], p["ndocs_total"])
+
+
+def _concat(results):
+    """rank-order concatenation of fetched shard results, terms as bytes"""
+    out = {k: np.concatenate([r[k] for r in results]) for k in ("doc", "count", "docsize", "df", "score")}
+    out["npairs"] = sum(r["npairs"] for r in results)
+    tb = [r["terms"][t] for r in results for t in r["term"].tolist()]
+    uniq = sorted(set(tb))
+    gid = {t: i for i, t in enumerate(uniq)}
+    out["terms"] = uniq
+    out["term"] = np.array([gid[t] for t in tb], dtype=np.uint32)
+    return out
+
+
+def _run_group(shards, K, **kw):
+    with tfidf_abi.Group(K, devices=[0] * K, **kw) as g:
+        g.run_host(shards)
+        texts = [e.text() for e in g.ranks]
+        res = [e.fetch() for e in g.ranks]
+        infos = [e.info() for e in g.ranks]
+    return texts, res, infos
+
+
+@pytest.mark.parametrize("cfg,scale,K", [("c2", 0.003, 2), ("c2", 0.003, 3), ("c5", 0.0005, 2), ("c5", 0.0005, 3),
+                                         ("c4", 0.001, 2), ("c2", 0.003, 5)])
+def test_group_shards_equal_single_rank_oracle(cfg, scale, K):
+    shards = _shards(cfg, scale, K)
+    ora = _full(cfg, scale)
+    texts, res, infos = _run_group(shards, K)
+    assert b"".join(texts) == ora["output_txt"]
+    assert_same_result(_concat(res), ora)
+    # identical global ids on every rank: the union size is the corpus vocabulary
+    assert all(i["nterms_global"] == ora["nterms"] for i in infos)
+    # shards really differ in vocabulary (the 0xEE padding of the all-gather is exercised)
+    assert len({i["nterms"] for i in infos}) > 1
+
+
+def test_group_retry_is_collective(monkeypatch):
+    """A 1024-slot starting vocabulary makes every rank grow its table and repeat the run;
+    the repeats are agreed at the exchange (no rank re-enters the collectives alone)."""
+    monkeypatch.setenv("TFIDF_VCAP", "1024")
+    monkeypatch.setenv("TFIDF_VLOAD", "50")
+    shards = _shards("c2", 0.003, 3)
+    ora = _full("c2", 0.003)
+    texts, res, infos = _run_group(shards, 3)
+    assert b"".join(texts) == ora["output_txt"]
+    assert all(i["vocab_capacity"] > 1024 for i in infos)
+
+
+def test_group_one_rank_retries_alone(monkeypatch):
+    """Only one rank's shard outgrows the starting table: the others repeat with it."""
+    monkeypatch.setenv("TFIDF_VCAP", "4096")
+    monkeypatch.setenv("TFIDF_VLOAD", "50")
+    big = _shards("c2", 0.003, 1)[0]
+    tiny_doc = (np.frombuffer(b"a b c\n", dtype=np.uint8).copy(), np.array([0, 6], dtype=np.uint64),
+                np.array([int(big[2].max()) + 1], dtype=np.uint32))
+    N = len(big[2]) + 1
+    shards = [(big[0], big[1], big[2], N), (tiny_doc[0], tiny_doc[1], tiny_doc[2], N)]
+    texts, res, infos = _run_group(shards, 2)
+    # oracle over the same two shards as one corpus ("doc301@" is not after every id of
+    # shard 0 in strcmp order, so the lines are compared as sorted sets)
+    data = np.concatenate([big[0], tiny_doc[0]])
+    off = np.concatenate([big[1], big[1][-1] + tiny_doc[1][1:]])
+    ids = np.concatenate([big[2], tiny_doc[2]])
+    ora = oracle_py.run(data, off, ids, N)
+    assert sorted(b"".join(texts).split(b"\n")) == sorted(ora["output_txt"].split(b"\n"))
+    # rank 0 grew its table; rank 1 repeated the run with it, at its own size
+    assert infos[0]["vocab_capacity"] > 4096 and infos[1]["vocab_capacity"] == 4096
+
+
+def test_group_empty_shard():
+    """A shard with no documents still takes part in the exchange (V = 0)."""
+    full = _shards("c2", 0.002, 1)[0]
+    N = len(full[2])
+    empty = (np.zeros(0, np.uint8), np.zeros(1, np.uint64), np.zeros(0, np.uint32), N)
+    texts, res, infos = _run_group([full, empty], 2)
+    ora = oracle_py.run(full[0], full[1], full[2], N)
+    assert b"".join(texts) == ora["output_txt"]
+    assert infos[1]["npairs"] == 0 and infos[0]["nterms_global"] == ora["nterms"]
+
+
+def test_group_error_releases_peers():
+    """A rank whose corpus is invalid fails; its peer returns TFIDF_E_PEER instead of
+    waiting in the exchange."""
+    full = _shards("c2", 0.001, 1)[0]
+    bad = (full[0], full[1][:-1] * 0 + np.uint64(1 << 40), full[2][:-1], len(full[2]))   # offsets past the bytes
+    with tfidf_abi.Group(2, devices=[0, 0]) as g:
+        with pytest.raises(tfidf_abi.TfidfError) as ei:
+            g.run_host([full, bad])
+        assert ei.value.rc == -1   # rank 1's own error is reported first... (rank 0 is E_PEER)
+        # the group is usable again afterwards
+        g.run_host(_shards("c2", 0.001, 2))
+
+
+def test_rccl_single_rank_runs_the_exchange():
+    """A 1-rank RCCL communicator: exchange_df runs (agreement, ncclAllGather of the keys,
+    union, ncclAllReduce) and the results are unchanged."""
+    p = tfidf_configs.plan("c2", scale=0.002)
+    data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
+    with tfidf_abi.Engine(0) as e:
+        e.comm_init(tfidf_abi.comm_unique_id(), 0, 1)
+        e.run_host(data, off, p["doc_ids"], p["ndocs_total"])
+        res = e.fetch()
+        assert e.info()["nterms_global"] == res["nterms"]
+        e.run_host(data, off, p["doc_ids"], p["ndocs_total"])   # repeat on the same communicator
+        assert e.fetch()["output_txt"] == res["output_txt"]
+    assert_same_result(res, oracle_py.run(data, off, p["doc_ids"], p["ndocs_total"]))
+
+
+def test_rccl_group_one_gpu():
+    """tfidf_group_open with one rank on its own GPU builds an RCCL clique (ncclCommInitAll)."""
+    shards = _shards("c5", 0.0005, 1)
+    ora = _full("c5", 0.0005)
+    with tfidf_abi.Group(1, devices=[0]) as g:
+        g.run_host(shards)
+        assert g.ranks[0].text() == ora["output_txt"]
+
+
+@pytest.mark.parametrize("case", ["g2_twelve_docs", "g5_w1", "g5_w3", "g3_bytes"])
+@pytest.mark.parametrize("shards", [1, 2, 3])
+def test_cli_shards_drop_in(case, shards):
+    """`tfidf --gpus 1 --shards K`: byte-balanced shards of input/ on one GPU, the same
+    output.txt as the reference for every K (as the reference's is for every -np), and
+    the --debug-jobs lines, split into their blocks and sorted, equal tf_jobs.txt /
+    idf_jobs.txt."""
+    g = load_golden(case)
+    with tempfile.TemporaryDirectory() as td:
+        shutil.copytree(os.path.join(GOLDEN, case, "input"), os.path.join(td, "input"))
+        p = subprocess.run([tfidf_abi.CLI_PATH, "--gpus", "1", "--shards", str(shards), "--debug-jobs"], cwd=td,
+                           capture_output=True, timeout=120)
+        assert p.returncode == 0, p.stderr
+        with open(os.path.join(td, "output.txt"), "rb") as f:
+            assert f.read() == g["output"]
+    tf, idf = split_jobs(p.stdout)
+    assert tf == g["tf_jobs"] and idf == g["idf_jobs"]
+
+
+def split_jobs(stdout: bytes):
+    """TF Job / IDF Job lines of the CLI's stdout (TFIDF.c:200-204,237-239), each block
+    kind sorted (the reference interleaves ranks, so only the sorted sets compare)."""
+    tf, idf, cur = [], [], None
+    for line in stdout.split(b"\n"):
+        if line == b"-------------TF Job-------------":
+            cur = tf
+        elif line == b"------------IDF Job-------------":
+            cur = idf
+        elif line and cur is not None:
+            cur.append(line)
+    return b"".join(x + b"\n" for x in sorted(tf)), b"".join(x + b"\n" for x in sorted(idf))

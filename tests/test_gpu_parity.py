@@ -135,19 +135,6 @@ def test_device_generator_matches_host(engine):
     assert_same_result(res, ora)
 
 
-def test_rccl_single_rank_exchange_path():
-    """Attaching a 1-rank RCCL communicator runs the vocabulary all-gather + DF
-    all-reduce path; results must not change."""
-    p = tfidf_configs.plan("c2", scale=0.002)
-    data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
-    with tfidf_abi.Engine(0) as e:
-        e.comm_init(tfidf_abi.comm_unique_id(), 0, 1)
-        e.run_host(data, off, p["doc_ids"], p["ndocs_total"])
-        res = e.fetch()
-        assert e.info()["nterms_global"] == res["nterms"]
-    assert_same_result(res, oracle_py.run(data, off, p["doc_ids"], p["ndocs_total"]))
-
-
 def test_repeat_runs_identical(engine):
     p = tfidf_configs.plan("c2", scale=0.002)
     data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
@@ -158,28 +145,49 @@ def test_repeat_runs_identical(engine):
     assert outs[0] == outs[1] == outs[2]
 
 
-@pytest.mark.parametrize("case", ["g1_whitespace", "g2_twelve_docs", "g4_config1"])
+@pytest.mark.parametrize("case", golden_cases())
 def test_cli_drop_in(case):
-    """`tfidf` with no arguments in the fixture directory writes the reference output.txt."""
+    """`tfidf` with no arguments in the fixture directory writes the reference output.txt;
+    with --debug-jobs its stdout, split into the TF Job / IDF Job blocks and sorted, is the
+    reference's tf_jobs.txt / idf_jobs.txt (TFIDF.c:199-205,236-239)."""
+    from test_gpu_multirank import split_jobs
+    g = load_golden(case)
     with tempfile.TemporaryDirectory() as td:
         shutil.copytree(os.path.join(GOLDEN, case, "input"), os.path.join(td, "input"))
         p = subprocess.run([tfidf_abi.CLI_PATH], cwd=td, capture_output=True, timeout=120)
         assert p.returncode == 0, p.stderr
         with open(os.path.join(td, "output.txt"), "rb") as f:
-            assert f.read() == load_golden(case)["output"]
+            assert f.read() == g["output"]
         p = subprocess.run([tfidf_abi.CLI_PATH, "--debug-jobs"], cwd=td, capture_output=True, timeout=120)
-        assert b"-------------TF Job-------------" in p.stdout
+        assert p.returncode == 0, p.stderr
+    tf, idf = split_jobs(p.stdout)
+    assert tf == g["tf_jobs"] and idf == g["idf_jobs"]
 
 
 def test_cli_error_contract():
     with tempfile.TemporaryDirectory() as td:
+        # no input/ (TFIDF.c:100-103)
         p = subprocess.run([tfidf_abi.CLI_PATH], cwd=td, capture_output=True, timeout=60)
         assert p.returncode == 1 and p.stdout == b"Directory failed to open\n"
+        # empty input/: N = 0 < workers (TFIDF.c:120-123), no output.txt
         os.makedirs(os.path.join(td, "input"))
+        for args in ([], ["--shards", "2"]):
+            p = subprocess.run([tfidf_abi.CLI_PATH] + args, cwd=td, capture_output=True, timeout=60)
+            assert p.returncode == 0 and p.stdout == b"More workers than input files! Exiting.\n"
+            assert not os.path.exists(os.path.join(td, "output.txt"))
+        # a missing document (TFIDF.c:134-138)
         with open(os.path.join(td, "input", "doc2"), "wb") as f:
             f.write(b"x")
-        p = subprocess.run([tfidf_abi.CLI_PATH], cwd=td, capture_output=True, timeout=60)
-        assert p.returncode == 0 and p.stdout.startswith(b"Error Opening File: input/doc1")
+        for args in ([], ["--shards", "2"]):
+            p = subprocess.run([tfidf_abi.CLI_PATH] + args, cwd=td, capture_output=True, timeout=60)
+            assert p.returncode == 0 and p.stdout.startswith(b"Error Opening File: input/doc1"), p.stdout
+        # output.txt cannot be written (TFIDF.c:274-278): a directory in its place
+        with open(os.path.join(td, "input", "doc1"), "wb") as f:
+            f.write(b"a b a\n")
+        os.makedirs(os.path.join(td, "output.txt"))
+        for args in ([], ["--shards", "2"]):
+            p = subprocess.run([tfidf_abi.CLI_PATH] + args, cwd=td, capture_output=True, timeout=60)
+            assert p.returncode == 0 and p.stdout == b"Error Opening File: output.txt\n", (p.stdout, p.stderr)
 
 
 @pytest.mark.parametrize("cfg", ["c2", "c4", "c5"])
@@ -225,12 +233,12 @@ def test_full_config_properties(cfg):
 
 @pytest.mark.parametrize("cfg,scale", [("c2", 0.002), ("c5", 0.0005), ("c4", 0.001)])
 def test_k1_variants_agree(cfg, scale):
-    """The slot-keyed K1 (default), the general K1 and the whitespace-separated K1 give
-    identical results, equal to the oracle."""
+    """The slot-keyed K1 (default) and the general K1 (unaligned corpora) give identical
+    results, equal to the oracle."""
     p = tfidf_configs.plan(cfg, scale=scale)
     data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
     outs = []
-    for mode, flag in (("auto", 2), ("general", 0), ("ws", 1)):
+    for mode, flag in (("auto", 2), ("general", 0)):
         os.environ["TFIDF_K1"] = mode
         try:
             with tfidf_abi.Engine(0) as e:

@@ -56,3 +56,20 @@ def test_golden_fixture_inventory():
     assert sum(c.startswith("g5_") for c in cases) >= 4
     g = load_golden("g4_config1")
     assert g["meta"]["npairs"] == 32 and g["meta"]["ndocs"] == 8
+
+
+def test_sharded_cpu_baseline_equals_oracle():
+    """oracle_run_sharded (bench.py's CPU baseline: threads per shard + DF combine +
+    shard-order concatenation) produces the single-rank oracle's output.txt."""
+    import numpy as np
+    import tfidf_abi
+    import tfidf_configs
+    p = tfidf_configs.plan("c2", scale=0.002)
+    data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
+    ref = oracle_py.run(data, off, p["doc_ids"], p["ndocs_total"], arrays=False)["output_txt"]
+    order = np.argsort(tfidf_configs.doc_name_key(p["doc_ids"]), kind="stable").astype(np.uint32)
+    sizes = np.diff(off.astype(np.int64))[order]
+    for k in (1, 3, 8):
+        first = tfidf_configs.shard_cuts(sizes, k)
+        txt, npairs = oracle_py.run_sharded(data, off, p["doc_ids"], p["ndocs_total"], order, first)
+        assert txt == ref and npairs == ref.count(b"\n")
