@@ -36,7 +36,10 @@ __device__ __forceinline__ uint32_t vocab_insert_s(uint4* __restrict__ keys, uin
                                                (unsigned long long)KEY_PENDING_HI);
             if (old == KEY_EMPTY_HI) {
                 atomicExch(&slot[0], (unsigned long long)klo);
-                if ((khi >> 56) == 0xFFu) reps[h] = rep;
+                if ((khi >> 56) == 0xFFu) {   /* once per distinct long term */
+                    reps[h] = rep;
+                    atomicOr(status, ST_HAS_LONG);
+                }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 atomicExch(&slot[1], (unsigned long long)khi);
                 return (uint32_t)h;

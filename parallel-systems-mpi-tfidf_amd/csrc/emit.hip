@@ -17,7 +17,8 @@
 namespace {
 
 constexpr int NT = 256;
-inline unsigned grid_for(uint64_t n, int nt = NT) { return (unsigned)((n + nt - 1) / nt); }
+/* at least one workgroup: an empty launch is an error, every kernel bounds-checks its index */
+inline unsigned grid_for(uint64_t n, int nt = NT) { return n ? (unsigned)((n + nt - 1) / nt) : 1u; }
 int ok() { return hipGetLastError() == hipSuccess ? 0 : -1; }
 
 constexpr uint64_t P16 = 10000000000000000ull;

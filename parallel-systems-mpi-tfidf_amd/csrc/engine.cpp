@@ -506,7 +506,7 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     ctx->ntokens = hc[2];
     ctx->nchunks = nchunks;
     ctx->nrec_part = Q;
-    if (st & ST_VOCAB_SPIN) return TFIDF_E_CAPACITY;
+    if (st & (ST_VOCAB_SPIN | ST_TERM_LONG)) return TFIDF_E_CAPACITY;
     bool retry = false;
     if (st & ST_BOUNDS) {
         fprintf(stderr, "tfidf: internal bounds check tripped in K1 (status 0x%x)\n", st);
@@ -573,7 +573,8 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     LCHK(cur);
     ctx->sorted_skey = cur ? ctx->skey1.as<uint4>() : ctx->skey0.as<uint4>();
     ctx->sorted_dense = cur ? ctx->seq1.as<uint32_t>() : ctx->seq0.as<uint32_t>();
-    LCHK(launch_vocab_long_fixup(ctx->sorted_skey, ctx->sorted_dense, ctx->vslot.as<uint32_t>(), vd, c, V, s));
+    if (st & ST_HAS_LONG)   /* terms of >= 16 bytes exist: order the ones tied on 16 bytes */
+        LCHK(launch_vocab_long_fixup(ctx->sorted_skey, ctx->sorted_dense, ctx->vslot.as<uint32_t>(), vd, c, V, ar, s));
     uint16_t* r16 = nullptr;
     if (V <= 65536u) { ENSURE(ctx->rank16, cap * 2); r16 = ctx->rank16.as<uint16_t>(); }
     LCHK(launch_vocab_rank(ctx->sorted_dense, ctx->vslot.as<uint32_t>(), V, ctx->rank_of_slot.as<uint32_t>(),

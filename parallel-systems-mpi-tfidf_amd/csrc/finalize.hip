@@ -19,7 +19,8 @@
 
 namespace {
 constexpr int NT = 256;
-inline unsigned grid_for(uint64_t n, int nt = NT) { return (unsigned)((n + nt - 1) / nt); }
+/* at least one workgroup: an empty launch is an error, every kernel bounds-checks its index */
+inline unsigned grid_for(uint64_t n, int nt = NT) { return n ? (unsigned)((n + nt - 1) / nt) : 1u; }
 inline int ok() { return hipGetLastError() == hipSuccess ? 0 : -1; }
 
 __device__ __forceinline__ uint4 u128_from(uint64_t lo, uint64_t hi) {
@@ -127,10 +128,130 @@ __global__ void k_vocab_long_fixup(const uint4* __restrict__ sk, uint32_t* __res
         sorted_dense[b] = x;
     }
 }
+/* ---- long terms sharing their first 16 bytes, in parallel ----
+ * The vocabulary sort orders long terms by their first 16 bytes only.  Ties (URLs, paths,
+ * identifiers with a common prefix: runs of 1e5+ terms are possible) are resolved by
+ * iterated re-keying, each round a segmented sort on the next 16 bytes:
+ *   h[i]   = 1 where sorted position i starts a group of equal keys so far (h[V] = 1);
+ *   round k: the positions in groups of two or more are compacted (pos[]), each gets
+ *   key = bytes [16k, 16k + 16) of its term ("w\t" then zeros: strcmp of "w\t",
+ *   TFIDF.c:49,245) and seg = its group ordinal; a stable LSD sort by key, then by seg,
+ *   reorders every group in place (groups are contiguous in both orders), and new group
+ *   starts are set where (seg, key) changes.
+ * The loop ends when no group of two or more is left: ceil(common prefix / 16) rounds.
+ * After VLF_MAX_ROUNDS (a 16 KiB common prefix) the single-thread insertion sort above
+ * finishes whatever is left. */
+constexpr uint32_t VLF_MAX_ROUNDS = 1024;
+
+__global__ void k_vlf_heads(const uint4* __restrict__ sk, uint32_t V, uint32_t* __restrict__ h) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > V) return;
+    h[i] = (i == 0 || i == V || !u128_eq(sk[i], sk[i - 1])) ? 1u : 0u;
+}
+/* tied[i]: position i is in a group of two or more */
+__global__ void k_vlf_tied(const uint32_t* __restrict__ h, uint32_t V, uint32_t* __restrict__ tied) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < V) tied[i] = (h[i] && h[i + 1]) ? 0u : 1u;
+}
+__device__ __forceinline__ uint4 vlf_key(const CorpusDev& c, uint64_t rep, uint64_t k) {
+    const uint64_t off = rep & 0xFFFFFFFFFFull, len = rep >> 40;
+    uint64_t a = 0, b = 0;
+    for (int t = 0; t < 16; ++t) {
+        const uint64_t p = 16 * k + (uint64_t)t;
+        const uint64_t x = p < len ? c.bytes[off + p] : (p == len ? 0x09u : 0u);
+        if (t < 8) a = (a << 8) | x; else b = (b << 8) | x;
+    }
+    return u128_from(b, a);
+}
+__global__ void k_vlf_keys(const uint32_t* __restrict__ tied_scan, const uint32_t* __restrict__ hscan,
+                           const uint32_t* __restrict__ h, const uint32_t* __restrict__ sorted_dense,
+                           const uint32_t* __restrict__ vslot, VocabDev v, CorpusDev c, uint32_t V, uint64_t k,
+                           uint32_t* __restrict__ pos, uint4* __restrict__ key, uint4* __restrict__ key_orig,
+                           uint32_t* __restrict__ val, uint64_t* __restrict__ seg, uint32_t* __restrict__ dense_copy) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= V || tied_scan[i + 1] == tied_scan[i]) return;
+    const uint32_t j = tied_scan[i];
+    const uint32_t d = sorted_dense[i];
+    const uint4 kk = vlf_key(c, v.rep[vslot[d]], k);
+    pos[j] = i;
+    key[j] = kk;
+    key_orig[j] = kk;
+    val[j] = j;
+    seg[j] = hscan[i] + h[i];   /* group ordinal (inclusive count of group starts) */
+    dense_copy[j] = d;
+}
+/* item j of the (key, seg)-sorted order came from compacted index o = vals[j] */
+__global__ void k_vlf_seg_of(const uint32_t* __restrict__ vals, const uint64_t* __restrict__ seg, uint32_t m,
+                             uint64_t* __restrict__ seg_sorted) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < m) seg_sorted[j] = seg[vals[j]];
+}
+__global__ void k_vlf_apply(const uint32_t* __restrict__ final_idx, uint32_t m, const uint32_t* __restrict__ pos,
+                            const uint32_t* __restrict__ dense_copy, const uint64_t* __restrict__ seg,
+                            const uint4* __restrict__ key_orig, uint32_t* __restrict__ sorted_dense,
+                            uint32_t* __restrict__ h) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const uint32_t o = final_idx[j], i = pos[j];
+    sorted_dense[i] = dense_copy[o];
+    bool head = j == 0;
+    if (!head) {
+        const uint32_t p = final_idx[j - 1];
+        head = seg[o] != seg[p] || !u128_eq(key_orig[o], key_orig[p]);
+    }
+    h[i] = head ? 1u : 0u;
+}
+
 int launch_vocab_long_fixup(const uint4* sorted_keys, uint32_t* sorted_dense, const uint32_t* vslot,
-                            const VocabDev& v, const CorpusDev& c, uint32_t V, hipStream_t s) {
+                            const VocabDev& v, const CorpusDev& c, uint32_t V, Arena& ar, hipStream_t s) {
     if (V < 2) return 0;
-    k_vocab_long_fixup<<<grid_for(V), NT, 0, s>>>(sorted_keys, sorted_dense, vslot, v, c, V);
+    const size_t m0 = ar.mark();
+    uint32_t* h = (uint32_t*)ar.get(((size_t)V + 1) * 4);
+    uint32_t* hs = (uint32_t*)ar.get(((size_t)V + 2) * 4);
+    uint32_t* ts = (uint32_t*)ar.get(((size_t)V + 2) * 4);
+    if (!h || !hs || !ts) return -2;
+    k_vlf_heads<<<grid_for((uint64_t)V + 1), NT, 0, s>>>(sorted_keys, V, h);
+    uint32_t round = 1;
+    for (; round <= VLF_MAX_ROUNDS; ++round) {
+        k_vlf_tied<<<grid_for(V), NT, 0, s>>>(h, V, ts);
+        if (scan_excl_u32(ts, ts, V, ar, s)) return -2;
+        uint32_t m = 0;
+        if (hipMemcpyAsync(&m, ts + V, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
+        if (hipStreamSynchronize(s) != hipSuccess) return -1;
+        if (m == 0) break;
+        if (scan_excl_u32(h, hs, V, ar, s)) return -2;
+        const size_t mr = ar.mark();
+        uint32_t* pos = (uint32_t*)ar.get((size_t)m * 4);
+        uint4* k0 = (uint4*)ar.get((size_t)m * 16);
+        uint4* k1 = (uint4*)ar.get((size_t)m * 16);
+        uint4* ko = (uint4*)ar.get((size_t)m * 16);
+        uint32_t* v0 = (uint32_t*)ar.get((size_t)m * 4);
+        uint32_t* v1 = (uint32_t*)ar.get((size_t)m * 4);
+        uint64_t* sg = (uint64_t*)ar.get((size_t)m * 8);
+        uint64_t* s0 = (uint64_t*)ar.get((size_t)m * 8);
+        uint64_t* s1 = (uint64_t*)ar.get((size_t)m * 8);
+        uint32_t* dc = (uint32_t*)ar.get((size_t)m * 4);
+        if (!pos || !k0 || !k1 || !ko || !v0 || !v1 || !sg || !s0 || !s1 || !dc) return -2;
+        k_vlf_keys<<<grid_for(V), NT, 0, s>>>(ts, hs, h, sorted_dense, vslot, v, c, V, round, pos, k0, ko, v0, sg, dc);
+        uint32_t vm = 0;
+        if (key_varying_bytes_u128(k0, m, &vm, ar, s)) return -2;
+        int cur = radix_sort_u128(k0, v0, k1, v1, m, vm, ar, s);
+        if (cur < 0) return cur;
+        uint32_t* vk = cur ? v1 : v0;
+        uint32_t* vo = cur ? v0 : v1;
+        k_vlf_seg_of<<<grid_for(m), NT, 0, s>>>(vk, sg, m, s0);
+        /* groups are < 2^32 and numbered in position order: a stable sort on seg */
+        const uint32_t segbytes = 0x0Fu;
+        int cs = radix_sort_u64(s0, vk, s1, vo, m, segbytes, ar, s);
+        if (cs < 0) return cs;
+        const uint32_t* fin = cs ? vo : vk;
+        k_vlf_apply<<<grid_for(m), NT, 0, s>>>(fin, m, pos, dc, sg, ko, sorted_dense, h);
+        if (ok()) return -1;
+        ar.release(mr);
+    }
+    if (round > VLF_MAX_ROUNDS)   /* absurdly long shared prefixes: finish serially */
+        k_vocab_long_fixup<<<grid_for(V), NT, 0, s>>>(sorted_keys, sorted_dense, vslot, v, c, V);
+    ar.release(m0);
     return ok();
 }
 

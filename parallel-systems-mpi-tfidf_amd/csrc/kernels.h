@@ -29,6 +29,8 @@
 #define ST_REC_FULL    4u
 #define ST_PART_FULL   8u
 #define ST_BOUNDS      16u   /* internal consistency guard tripped (a bug, reported as an error) */
+#define ST_HAS_LONG    64u   /* the vocabulary holds terms of >= 16 bytes (their order needs vocab_long_fixup) */
+#define ST_TERM_LONG   32u   /* a term of >= 16 MiB: beyond the 24-bit length of a long key's rep */
 
 /* doc flags */
 #define DF_PARTIAL     1u
@@ -95,8 +97,10 @@ int launch_vocab_compact(const VocabDev& v, uint64_t cap, const uint32_t* dense_
                          uint32_t* vslot, uint4* sortkey, uint32_t* seq, hipStream_t s);
 int launch_vocab_rank(const uint32_t* sorted_dense, const uint32_t* vslot, uint32_t V, uint32_t* rank_of_slot,
                       uint32_t* slot_of_rank, uint16_t* rank16, hipStream_t s);
+/* long terms tied on their first 16 bytes: ordered by iterated segmented sorts (host loop,
+ * one sync per 16 bytes of common prefix); -2 when the arena is too small */
 int launch_vocab_long_fixup(const uint4* sorted_keys, uint32_t* sorted_dense, const uint32_t* vslot,
-                            const VocabDev& v, const CorpusDev& c, uint32_t V, hipStream_t s);
+                            const VocabDev& v, const CorpusDev& c, uint32_t V, Arena& ar, hipStream_t s);
 
 /* partial documents: sort key (doc << 32 | rank) and merge */
 int launch_part_keys(const uint32_t* part_doc, const uint32_t* part_slot, const uint32_t* rank_of_slot, uint64_t n,

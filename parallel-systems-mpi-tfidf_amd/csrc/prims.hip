@@ -338,6 +338,7 @@ __global__ void k_tile_place(const K* __restrict__ tk, const uint32_t* __restric
 
 template <typename K>
 int tile_sort_t(const K* k0, const uint32_t* v0, K* k1, uint32_t* v1, uint64_t n, Arena& ar, hipStream_t s) {
+    if (n == 0) return 1;   /* nothing to sort: the (empty) result is in (k1, v1) */
     const uint32_t nt = (uint32_t)((n + TS_T - 1) / TS_T);
     size_t m = ar.mark();
     K* tk = (K*)ar.get(n * sizeof(K));

@@ -159,6 +159,9 @@ __device__ __forceinline__ uint32_t slow_slot(const uint8_t* __restrict__ bytes,
         return vocab_insert(v, klo, khi, 0, status);
     }
     make_long_key(bytes + p0, n, &klo, &khi);
+    /* rep = (length << 40) | offset holds 24 length bits: a term of 16 MiB or more would be
+     * emitted truncated, so the run fails with TFIDF_E_CAPACITY instead */
+    if (n >= 0xFFFFFFull) atomicOr(status, ST_TERM_LONG);
     const uint64_t rep = ((n < 0xFFFFFFull ? n : 0xFFFFFFull) << 40) | p0;
     return vocab_insert(v, klo, khi, rep, status);
 }

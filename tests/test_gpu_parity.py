@@ -373,3 +373,31 @@ def test_dense_merge_long_documents(engine):
     docs = [bytes(data[int(off[i]):int(off[i + 1])]) for i in range(len(off) - 1)] + [mid]
     d2, o2 = docs_to_arrays(docs)
     check_vs_oracle(engine, d2, o2)
+
+
+def test_many_long_terms_sharing_prefixes(engine):
+    """~1e5 distinct long terms tied on their first 16 (and 32, 48, ...) bytes: URL-like
+    runs, terms that are prefixes of others, a byte < TAB after a shared prefix, and a
+    few terms sharing 200 bytes.  Their order (strcmp of "w\\t") comes from the iterated
+    segmented sort (vocab_long_fixup); against the oracle, bit-exact."""
+    rng = np.random.default_rng(21)
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789_/", dtype=np.uint8)
+    words = set()
+    for pre in (b"https://en.wikipedia.org/wiki/", b"/usr/local/lib/python3/site-packages/", b"x" * 40):
+        while len(words) < 30000 * (1 + [b"https://en.wikipedia.org/wiki/", b"/usr/local/lib/python3/site-packages/",
+                                          b"x" * 40].index(pre)):
+            L = int(rng.integers(0, 12))
+            words.add(pre + bytes(alpha[rng.integers(0, len(alpha), L)]))
+    base = b"q" * 200
+    extra = [base, base + b"a", base + b"\x01", base + b"ab", base[:150] + b"z", b"abcdefghijklmnopq",
+             b"abcdefghijklmnop\x05", b"abcdefghijklmnopqr"]
+    words = sorted(words) + extra
+    order = rng.permutation(len(words))
+    docs, cur = [], []
+    for k, i in enumerate(order):
+        cur.append(words[i])
+        if len(cur) == 700 or k == len(order) - 1:
+            cur += [words[j] for j in rng.integers(0, len(words), 50)]
+            docs.append(b" ".join(cur) + b"\n")
+            cur = []
+    check_vs_oracle(engine, *docs_to_arrays(docs))
