@@ -73,7 +73,8 @@ struct tfidf_ctx {
     Xport* xp = nullptr;    /* peers of the DF exchange (RCCL or in-process); owned */
     int rank = 0, nranks = 1;
     bool timing = true;
-    int k1_mode = 0;        /* 0 auto, 2 general K1 (env TFIDF_K1=general: cross-checks) */
+    int k1_mode = 0;        /* 0 auto (tokcount_st), 1 round-1 kernel (TFIDF_K1=vs), 2 general K1
+                               (TFIDF_K1=general): cross-checks and A/B timing */
     bool stamps_on = false; /* env TFIDF_STAMPS=1 with the diagnostic library build */
     uint32_t ablate = 0;    /* env TFIDF_K1_ABLATE: K1 timing experiments, pipeline stops after K1 */
     DevBuf stamps;
@@ -204,6 +205,7 @@ int tfidf_open(int device, tfidf_ctx** out) {
     ctx->device = device;
     const char* km = getenv("TFIDF_K1");
     if (km && !strcmp(km, "general")) ctx->k1_mode = 2;
+    if (km && !strcmp(km, "vs")) ctx->k1_mode = 1;
     const char* ks = getenv("TFIDF_STAMPS");
     ctx->stamps_on = ks && ks[0] == '1';
     const char* ka = getenv("TFIDF_K1_ABLATE");
@@ -449,7 +451,7 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     /* K1 variant: the slot-keyed kernel (tokcount_vs.hip) needs a 16-byte aligned corpus
      * base; TFIDF_K1=general selects the general kernel (cross-checks) */
     const bool aligned = (((uintptr_t)c.bytes & 15u) == 0);
-    ctx->k1_vs = aligned && ctx->k1_mode == 0;
+    ctx->k1_vs = aligned && ctx->k1_mode <= 1;
     if (ctx->k1_vs && ctx->vcap > K1_VS_MAX_CAP) return TFIDF_E_CAPACITY;
     /* ---- K1 ---- */
     mark(ctx, S_TOKCOUNT);
@@ -478,7 +480,9 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
         HIPCHK(hipMemsetAsync(ctx->stamps.p, 0, 8 * K1_STAMP_WORDS, s));
         o.stamps = ctx->stamps.as<unsigned long long>();
     }
-    if (nchunks && ctx->k1_vs)
+    if (nchunks && ctx->k1_vs && ctx->k1_mode == 0)
+        LCHK(launch_tokcount_st(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
+    else if (nchunks && ctx->k1_vs)
         LCHK(launch_tokcount_vs(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
     else if (nchunks)
         LCHK(launch_tokcount(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));

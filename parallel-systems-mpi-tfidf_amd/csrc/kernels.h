@@ -85,7 +85,12 @@ int launch_plan_chunks(const CorpusDev& c, uint64_t nchunks, uint64_t* chunk_sta
 int launch_tokcount(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc,
                     uint64_t c0, uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s);
 
-/* K1 main path (tokcount_vs.hip): 16-byte aligned corpus base; returns -3 when the
+/* K1 main path (tokcount_st.hip, LDS-staged walk; tokcount_vs.hip: the round-1 kernel,
+ * TFIDF_K1=vs): 16-byte aligned corpus base; return -3 when the vocabulary capacity
+ * exceeds the LDS entry's slot field */
+int launch_tokcount_st(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc, uint64_t c0,
+                       uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s);
+/* K1 round-1 path (tokcount_vs.hip): 16-byte aligned corpus base; returns -3 when the
  * vocabulary capacity exceeds the LDS entry's slot field */
 int launch_tokcount_vs(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc, uint64_t c0,
                        uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s);

@@ -1,0 +1,567 @@
+/*
+ * tokcount_st.hip — K1: fused tokenize + per-document term counting with an LDS-staged
+ * walk.  Replaces the reference's per-rank hot loop TFIDF.c:130-196: fscanf("%s")
+ * tokenising (:141-147), the O(P) strcmp search/append of (word, doc) records (:151-167)
+ * and the per-rank word table (:169-188).
+ *
+ * Work split (as tokcount_vs.hip): a persistent grid takes K0's chunks (~16 KiB of whole
+ * documents, or a piece of a document longer than BIG_DOC) from a global counter; inside
+ * a chunk the four waves of a workgroup run without block barriers, wave w taking the
+ * 1 KiB steps w, w+4, ...; (document, term) pairs are counted in one LDS table per
+ * workgroup and flushed as coalesced records once per chunk.
+ *
+ * What makes a token cheap here — everything positional is settled ONCE per 16-byte group
+ * in the walk, so the per-token round is a straight line:
+ *   walk   each lane classifies its 16 bytes (SWAR C-locale isspace, TFIDF.c:142,147, and
+ *          NUL: strcmp/strcpy stop there, :152,172), finds its document starts and the
+ *          document index of its first byte, and stores its bytes in the wave's LDS stage
+ *          (plus the 16 bytes after the step).  The lane that owns a token start then
+ *          writes one 32-bit token entry: byte offset | term length (distance to the next
+ *          whitespace, document start or NUL — read from its own and the next lane's
+ *          masks) | document index.
+ *   round  64 tokens, one per lane: the entry, ONE unaligned ds_read_b128 of the term's
+ *          bytes from the stage, ONE ds_read_b128 of the v_perm selectors for its length
+ *          (bytes < n kept, byte n = TAB, the rest zero: the 128-bit identity key of
+ *          dev_common.h in four v_perm_b32), the vocabulary hash, two adjacent vocabulary
+ *          slots loaded in one go, then the (document, slot) count in LDS.  The next
+ *          round's vocabulary loads are issued before the current round is counted.
+ * Terms of 16 bytes or more (and tokens running past the 32-byte window) take the HBM
+ * slow path of tokcount_vs.hip.  The flush, the overflow mode (partial records merged by
+ * finalize.hip) and the record layout are tokcount_vs.hip's.
+ *
+ * LDS: 28 KiB table + ~10 KiB walk/document state -> four workgroups (16 waves) per CU.
+ * Requires a 16-byte aligned corpus base (engine.cpp falls back to tokcount.hip).
+ */
+#include "dev_common.h"
+#include "dev_vocab.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int NT = 256;                   /* threads per workgroup */
+constexpr int NWAVE = NT / 64;
+constexpr int WSTEP = 1024;               /* bytes per wave step: one 16-byte group per lane */
+constexpr int TB = 3584;                  /* LDS table entries (u64): 14 per thread */
+constexpr int EPT = TB / NT;
+constexpr uint32_t FILL_LIMIT = TB - NT * 2 - 64; /* claims after which overflow mode starts */
+constexpr int GCAP = 256;                 /* documents per group (doc-in-group: 8 bits) */
+constexpr uint32_t SLOT_BITS = 28;
+constexpr uint32_t CNT_BITS = 24;
+constexpr uint64_t CNT_MASK = (1ull << CNT_BITS) - 1ull;
+constexpr int TLW = 192;                  /* token entries per wave and compaction pass */
+constexpr uint32_t LEN_LONG = 31u;        /* token entry: term of >= 16 bytes or past the window */
+
+struct StShared {
+    unsigned long long T[TB];             /* (doc, slot) -> count */
+    uint64_t gdoc[GCAP + 1];              /* doc_off of the group's documents */
+    uint32_t dsz[GCAP];                   /* docSize accumulators */
+    union {
+        struct {                          /* walk */
+            uint4 stage[NWAVE][WSTEP / 16 + 1];
+            uint32_t tl[NWAVE][TLW];
+        } w;
+        struct {                          /* flush */
+            uint32_t dcnt[GCAP];          /* entries per document */
+            uint32_t doff[GCAP];          /* record offset (complete | partial << 16) */
+            uint32_t drun[GCAP];          /* running record index per document */
+            uint8_t dstate[GCAP];         /* 0 none, 1 partial, 2 complete */
+        } f;
+    };
+    uint4 sel[16];                        /* v_perm selectors of a term of length n */
+    uint8_t dpart[GCAP];                  /* document has overflow records */
+    uint32_t fill;                        /* table claims of the group */
+    uint32_t over;                        /* overflow mode */
+    uint32_t wsum[NWAVE];
+    unsigned long long rec_base, part_base;
+    uint64_t next_chunk;                  /* dynamic chunk schedule */
+};
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4u __attribute__((ext_vector_type(4), aligned(1)));   /* unaligned LDS read */
+
+/* streaming corpus load: clamped to the last 16-byte block, non-temporal (read once) */
+__device__ __forceinline__ uint4 ld16c(const uint8_t* __restrict__ bytes, uint64_t last_blk, uint64_t pos) {
+    const uint64_t p = pos < last_blk ? pos : last_blk;
+    const u32x4 r = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(bytes + p));
+    return make_uint4(r.x, r.y, r.z, r.w);
+}
+
+/* bytes of [pos, pos+16) outside the shard's [lo, hi) read as whitespace */
+__device__ __forceinline__ uint32_t bounds_ws(uint64_t pos, uint64_t lo, uint64_t hi) {
+    const uint32_t a = pos < lo ? (uint32_t)min(lo - pos, (uint64_t)16) : 0u;
+    const uint32_t b = hi > pos ? (uint32_t)min(hi - pos, (uint64_t)16) : 0u;
+    const uint32_t in = b > a ? (((1u << b) - 1u) & ~((1u << a) - 1u)) : 0u;
+    return ~in & 0xFFFFu;
+}
+
+/* bit 7 of every zero byte (exact) */
+__device__ __forceinline__ uint32_t zero_bits(uint32_t x) { return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u; }
+__device__ __forceinline__ uint32_t compress4(uint32_t m) {   /* bits 7, 15, 23, 31 -> bits 0-3 */
+    m >>= 7;
+    m |= m >> 7;
+    m |= m >> 14;
+    return m & 0xFu;
+}
+
+__device__ __forceinline__ uint32_t tbl_hash(uint64_t key) {
+    const uint32_t k = (uint32_t)key ^ (uint32_t)(key >> 28) * 0x9E3779B1u;
+    return (uint32_t)(((uint64_t)(k * 0x85EBCA6Bu) * (uint64_t)TB) >> 32);   /* [0, TB) */
+}
+__device__ __forceinline__ uint32_t tbl_next(uint32_t h) { return h + 1 == (uint32_t)TB ? 0u : h + 1; }
+
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+}
+
+/* term slot of a token whose term is >= 16 bytes (or runs past the 32-byte window): the
+ * token is re-read from HBM (rare for text) */
+__device__ __noinline__ uint32_t slow_slot(const uint8_t* __restrict__ bytes, const VocabDev& v, uint64_t p0,
+                                           uint64_t dend, uint32_t* status) {
+    uint64_t p = p0;
+    while (p < dend && !is_ws(bytes[p])) ++p;
+    uint64_t n = 0;
+    while (p0 + n < p && bytes[p0 + n] != 0) ++n;
+    uint64_t klo, khi;
+    if (n < 16) {
+        uint64_t lo = 0, hi = 0;
+        for (uint32_t k = 0; k < n; ++k) {
+            const uint64_t b = bytes[p0 + k];
+            if (k < 8) lo |= b << (8 * k); else hi |= b << (8 * (k - 8));
+        }
+        make_short_key(lo, hi, (uint32_t)n, &klo, &khi);
+        return vocab_insert(v, klo, khi, 0, status);
+    }
+    make_long_key(bytes + p0, n, &klo, &khi);
+    /* rep = (length << 40) | offset holds 24 length bits: a term of 16 MiB or more would be
+     * emitted truncated, so the run fails with TFIDF_E_CAPACITY instead */
+    if (n >= 0xFFFFFFull) atomicOr(status, ST_TERM_LONG);
+    const uint64_t rep = ((n < 0xFFFFFFull ? n : 0xFFFFFFull) << 40) | p0;
+    return vocab_insert(v, klo, khi, rep, status);
+}
+
+__device__ __noinline__ void overflow_record(unsigned long long* part_alloc, uint64_t part_cap, uint32_t* part_doc,
+                                             uint32_t* part_slot, uint32_t* part_cnt, uint32_t* status, uint32_t doc,
+                                             uint32_t slot) {
+    const unsigned long long q = atomicAdd(part_alloc, 1ull);
+    if (q < part_cap) { part_doc[q] = doc; part_slot[q] = slot; part_cnt[q] = 1u; }
+    else atomicOr(status, ST_PART_FULL);
+}
+
+/* Counts `key` from slot h on (the first probe returned `old`; `nx` is a plain read of the
+ * next slot from the same LDS batch).  Returns 1 when this call claimed an entry.  A probe
+ * run longer than PMAX, or a new pair in overflow mode, becomes a partial record of count
+ * 1 (the merge sums them), so the table never fills or loops. */
+constexpr int PMAX = 64;
+__device__ __forceinline__ uint32_t tbl_count(StShared& S, const K1Out& o, uint64_t key, uint32_t h,
+                                              unsigned long long old, unsigned long long nx, bool over, uint32_t gd0) {
+    const unsigned long long ent = (key << CNT_BITS) | 1ull;
+    if (old != 0ull && (old >> CNT_BITS) != key) {
+        h = tbl_next(h);
+        if ((nx >> CNT_BITS) == key && nx != 0ull) { atomicAdd(&S.T[h], 1ull); return 0u; }
+        old = (nx == 0ull && !over) ? atomicCAS(&S.T[h], 0ull, ent) : nx;
+    }
+    for (int probe = 2;; ++probe) {
+        if (old == 0ull) {
+            if (!over) return 1u;
+            break;
+        }
+        if ((old >> CNT_BITS) == key) { atomicAdd(&S.T[h], 1ull); return 0u; }
+        if (probe >= PMAX) break;
+        h = tbl_next(h);
+        old = over ? S.T[h] : atomicCAS(&S.T[h], 0ull, ent);
+    }
+    const uint32_t rel = (uint32_t)(key >> SLOT_BITS);
+    S.dpart[rel] = 1;
+    overflow_record(o.part_alloc, o.part_cap, o.part_doc, o.part_slot, o.part_cnt, o.status, gd0 + rel,
+                    (uint32_t)key & ((1u << SLOT_BITS) - 1u));
+    return 0u;
+}
+
+__device__ __forceinline__ void wave_agg_add(uint32_t* ctr, uint32_t idx) {
+    const uint32_t i0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);
+    const uint64_t am = __ballot(1);
+    if (__ballot(idx != i0) == 0ull) {
+        if (__builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u)) == 0u)
+            atomicAdd(&ctr[i0], (uint32_t)__popcll(am));
+    } else {
+        atomicAdd(&ctr[idx], 1u);
+    }
+}
+__device__ __forceinline__ uint32_t wave_agg_add_rtn(uint32_t* ctr, uint32_t idx) {
+    const uint32_t i0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);
+    const uint64_t am = __ballot(1);
+    uint32_t k;
+    if (__ballot(idx != i0) == 0ull) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u));
+        uint32_t b = 0;
+        if (rank == 0u) b = atomicAdd(&ctr[i0], (uint32_t)__popcll(am));
+        k = (uint32_t)__builtin_amdgcn_readfirstlane((int)b) + rank;
+    } else {
+        k = atomicAdd(&ctr[idx], 1u);
+    }
+    return k;
+}
+
+/* Emits every table entry of the group as records and clears the table (tokcount_vs.hip's
+ * flush: complete documents to the record stream, documents crossing a chunk edge, over
+ * K5's in-LDS sort size or overflowed to the partial stream). */
+__device__ void st_flush(StShared& S, const K1Out& o, uint32_t gd0, uint32_t ng, uint64_t cs, uint64_t ce) {
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));   /* keep j * NT + tid out of the chunk loop (no spills) */
+    lds_barrier();                  /* every wave's walk is done (the walk state aliases dcnt...) */
+    if (tid < GCAP) { S.f.dcnt[tid] = 0; S.f.drun[tid] = 0; }
+    lds_barrier();
+    unsigned long long e[EPT];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+        e[j] = S.T[j * NT + tid];
+        if (e[j]) wave_agg_add(&S.f.dcnt[0], (uint32_t)(e[j] >> (CNT_BITS + SLOT_BITS)));
+    }
+    lds_barrier();
+    uint32_t packed = 0;
+    if ((uint32_t)tid < ng) {
+        uint8_t st = 0;
+        const uint32_t cnt = S.f.dcnt[tid];
+        const bool part = S.dpart[tid] != 0;
+        if (cnt) {
+            const bool complete = !part && S.gdoc[tid] >= cs && S.gdoc[tid + 1] <= ce && cnt <= (uint32_t)K5_MAX_PAIRS;
+            st = complete ? 2 : 1;
+            packed = complete ? cnt : (cnt << 16);
+        }
+        if (st == 1 || part) o.doc_flags[gd0 + tid] = DF_PARTIAL;
+        S.f.dstate[tid] = st;
+    }
+    uint32_t tot;
+    const uint32_t off = block_excl_scan<NT, true>(packed, S.wsum, &tot);
+    if ((uint32_t)tid < ng) S.f.doff[tid] = off;
+    const uint32_t nrec = tot & 0xFFFFu, npart = tot >> 16, ntot = nrec + npart;
+    if (tid == 0) {
+        const unsigned long long rb = nrec ? atomicAdd(o.rec_alloc, (unsigned long long)nrec) : 0ull;
+        if (rb + nrec > o.rec_cap) atomicOr(o.status, ST_REC_FULL);
+        S.rec_base = rb;
+    } else if (tid == 64) {
+        const unsigned long long pb = npart ? atomicAdd(o.part_alloc, (unsigned long long)npart) : 0ull;
+        if (pb + npart > o.part_cap) atomicOr(o.status, ST_PART_FULL);
+        S.part_base = pb;
+    }
+    lds_barrier();
+    const unsigned long long rb = S.rec_base, pb = S.part_base;
+    const bool rec_ok = rb + nrec <= o.rec_cap, part_ok = pb + npart <= o.part_cap;
+    if ((uint32_t)tid < ng && S.f.dstate[tid] == 2) {
+        o.doc_recoff[gd0 + tid] = rb + (off & 0xFFFFu);
+        o.doc_npairs[gd0 + tid] = S.f.dcnt[tid];
+    }
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+        if (e[j]) {
+            const uint32_t rel = (uint32_t)(e[j] >> (CNT_BITS + SLOT_BITS));
+            const uint32_t slot = (uint32_t)(e[j] >> CNT_BITS) & ((1u << SLOT_BITS) - 1u);
+            const uint64_t cnt = e[j] & CNT_MASK;
+            const uint32_t k = wave_agg_add_rtn(&S.f.drun[0], rel);
+            const uint32_t dof = S.f.doff[rel];
+            if (S.f.dstate[rel] == 2) S.T[(dof & 0xFFFFu) + k] = slot | (cnt << 32);
+            else S.T[nrec + (dof >> 16) + k] = slot | ((uint64_t)rel << SLOT_BITS) | (cnt << 36);
+        }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+        const uint32_t i = j * NT + tid;
+        if (i < nrec) {
+            const unsigned long long w = S.T[i];
+            if (rec_ok) { o.rec_slot[rb + i] = (uint32_t)w; o.rec_cnt[rb + i] = (uint32_t)(w >> 32); }
+        } else if (i < ntot) {
+            const unsigned long long w = S.T[i];
+            const uint64_t q = pb + (i - nrec);
+            if (part_ok) {
+                o.part_doc[q] = gd0 + ((uint32_t)(w >> SLOT_BITS) & 0xFFu);
+                o.part_slot[q] = (uint32_t)w & ((1u << SLOT_BITS) - 1u);
+                o.part_cnt[q] = (uint32_t)(w >> 36);
+            }
+        }
+        S.T[i] = 0ull;
+    }
+}
+
+/* v_perm selector dword k of a term of length n: byte j of the key dword is data byte j
+ * (4k + j < n), TAB (4k + j == n: byte 0 of the 0x09090909 source) or zero */
+__device__ __forceinline__ uint32_t perm_sel(uint32_t n, uint32_t k) {
+    uint32_t s = 0;
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t p = 4 * k + j;
+        const uint32_t b = p < n ? j : (p == n ? 4u : 12u);
+        s |= b << (8 * j);
+    }
+    return s;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64_t* __restrict__ chunk_start,
+                                                       const uint32_t* __restrict__ chunk_doc, uint64_t c0,
+                                                       uint64_t c1, VocabDev v, K1Out o) {
+    __shared__ __attribute__((aligned(16))) StShared S;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint64_t last_blk = c.nbytes ? ((c.nbytes - 1) & ~(uint64_t)15) : 0;
+    const bool edge_lane = lane == 0 || lane == 63;
+    const uint64_t eoff = lane == 0 ? (uint64_t)0 - 16ull : 16ull;
+
+    for (int j = 0; j < EPT; ++j) S.T[j * NT + tid] = 0ull;
+    if (tid < 64) {
+        const uint32_t n = (uint32_t)tid >> 2, k = (uint32_t)tid & 3u;
+        (&S.sel[n].x)[k] = perm_sel(n, k);
+    }
+    unsigned long long tokens_wg = 0;
+
+    /* one token round of the wave (one token per lane) */
+    struct Round {
+        uint64_t ap;
+        uint32_t k0, k1, k2, k3;   /* identity key (short terms) */
+        uint32_t hv, rel, kind;
+        uint4 s4, t4;              /* the two vocabulary slots loaded for it */
+    };
+    Round pend{};
+    bool pending = false;
+    uint32_t gd0_cur = 0;
+    /* finish a round: vocabulary slot (miss path: lock-free insert / long term), docSize,
+     * LDS (doc, slot) count, overflow accounting */
+    auto finish = [&](const Round& r) {
+        uint32_t slot = INVALID_SLOT;
+        if (r.kind == 1u) {
+            const bool hit0 = r.s4.x == r.k0 && r.s4.y == r.k1 && r.s4.z == r.k2 && r.s4.w == r.k3;
+            const bool hit1 = r.t4.x == r.k0 && r.t4.y == r.k1 && r.t4.z == r.k2 && r.t4.w == r.k3;
+            slot = hit0 ? r.hv : hit1 ? ((r.hv + 1) & (uint32_t)v.mask)
+                                      : vocab_insert(v, ((uint64_t)r.k1 << 32) | r.k0, ((uint64_t)r.k3 << 32) | r.k2, 0,
+                                                     o.status);
+        } else if (r.kind == 2u) {
+            slot = slow_slot(c.bytes, v, r.ap, S.gdoc[r.rel + 1], o.status);
+        }
+        /* docSize: one LDS add per wave when the round's tokens share a document */
+        const uint64_t vm = __ballot(r.kind != 0u);
+        if (vm) {
+            const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.rel);
+            if (__ballot(r.kind != 0u && r.rel != r0) == 0ull) {
+                if (lane == 0) atomicAdd(&S.dsz[r0], (uint32_t)__popcll(vm));
+            } else if (r.kind) {
+                atomicAdd(&S.dsz[r.rel], 1u);
+            }
+        }
+        const uint64_t key = slot == INVALID_SLOT ? ~0ull : (((uint64_t)r.rel << SLOT_BITS) | slot);
+        const uint32_t hl = tbl_hash(key);
+        const bool over = S.over != 0;
+        const bool valid = key != ~0ull;
+        unsigned long long old = 0ull, nx = 0ull;
+        if (valid) {
+            old = over ? S.T[hl] : atomicCAS(&S.T[hl], 0ull, (key << CNT_BITS) | 1ull);
+            nx = S.T[tbl_next(hl)];
+        }
+        const bool hit = valid && old != 0ull && (old >> CNT_BITS) == key;
+        const bool claimed = valid && old == 0ull && !over;
+        if (hit) atomicAdd(&S.T[hl], 1ull);
+        uint32_t claims = claimed ? 1u : 0u;
+        const bool rest = valid && !hit && !claimed;
+        if (__ballot(rest) != 0ull) {
+            if (rest) claims = tbl_count(S, o, key, hl, old, nx, over, gd0_cur);
+        }
+        const uint32_t wc = (uint32_t)__popcll(__ballot(claims != 0u));
+        if (wc && lane == 0) {
+            const uint32_t f = atomicAdd(&S.fill, wc);
+            if (f + wc >= FILL_LIMIT) S.over = 1;
+        }
+    };
+
+    if (tid == 0) S.next_chunk = c0 + atomicAdd(o.chunk_ctr, 1ull);
+    lds_barrier();
+    uint64_t next_claim = 0;
+    uint8_t* const stage = reinterpret_cast<uint8_t*>(&S.w.stage[wid][0]);
+    uint32_t* const tl = S.w.tl[wid];
+    for (uint64_t chunk = uni64(S.next_chunk); chunk < c1; chunk = uni64(S.next_chunk)) {
+        if (tid == 0) next_claim = c0 + atomicAdd(o.chunk_ctr, 1ull);
+        const uint64_t cs = chunk_start[chunk], ce = chunk_start[chunk + 1];
+        const uint32_t dfirst = chunk_doc[chunk], dlast = chunk_doc[chunk + 1];
+        if (cs < ce)
+        for (uint32_t gd0 = dfirst; gd0 <= dlast; gd0 += GCAP) {
+            gd0_cur = gd0;
+            const uint32_t ng = (dlast + 1 - gd0) < (uint32_t)GCAP ? (dlast + 1 - gd0) : (uint32_t)GCAP;
+            for (uint32_t k = tid; k <= ng; k += NT) S.gdoc[k] = c.doc_off[gd0 + k];
+            if (tid < GCAP) { S.dsz[tid] = 0; S.dpart[tid] = 0; }
+            if (tid == 0) { S.fill = 0; S.over = 0; }
+            lds_barrier();
+            const uint64_t g0 = uni64(S.gdoc[0]), gn = uni64(S.gdoc[ng]);
+            const uint64_t gs = g0 > cs ? g0 : cs;
+            const uint64_t ge = gn < ce ? gn : ce;
+            if (gs < ge) {
+                const uint64_t b0 = gs & ~(uint64_t)15;
+                const uint32_t nsteps = (uint32_t)((ge - b0 + WSTEP - 1) / WSTEP);
+                const uint64_t lane_off = 16ull * lane;
+                uint4 pf0 = make_uint4(0, 0, 0, 0), pe0 = pf0;
+                {
+                    const uint64_t a0 = b0 + (uint64_t)wid * WSTEP + lane_off;
+                    pf0 = ld16c(c.bytes, last_blk, a0);
+                    if (edge_lane) pe0 = ld16c(c.bytes, last_blk, a0 + eoff);
+                }
+                uint32_t wr = 0;             /* wave-uniform: document containing the step start */
+                for (uint32_t s = wid; s < nsteps; s += NWAVE) {
+                    const uint64_t sb = b0 + (uint64_t)s * WSTEP;
+                    const uint64_t gpos = sb + lane_off;
+                    const uint4 cur = pf0, edge = pe0;
+                    {
+                        const uint64_t a1 = gpos + 1ull * NWAVE * WSTEP; /* harmless past ge */
+                        pf0 = ld16c(c.bytes, last_blk, a1);
+                        if (edge_lane) pe0 = ld16c(c.bytes, last_blk, a1 + eoff);
+                    }
+                    /* the step's bytes (and the 16 after it) into the wave's stage; this
+                     * wave's reads of the previous step were issued before (LDS in order) */
+                    reinterpret_cast<uint4*>(stage)[lane] = cur;
+                    if (lane == 63) reinterpret_cast<uint4*>(stage)[64] = edge;
+                    /* ---- classify ---- */
+                    const bool inner = sb >= c.lo + 16 && sb + WSTEP + 16 <= c.hi;
+                    uint32_t ws = ws_mask16_swar(cur);
+                    if (!inner) ws |= bounds_ws(gpos, c.lo, c.hi);
+                    /* document starts in [sb, sb + WSTEP + 16) and the document of each
+                     * lane's first byte: a wave-uniform loop over the group's doc_off */
+                    while (wr + 1 < ng && uni64(S.gdoc[wr + 1]) <= sb) ++wr;
+                    uint32_t ds = 0, nds = 0, base = wr;
+                    for (uint32_t k = wr + 1; k <= ng; ++k) {
+                        const uint64_t sk = uni64(S.gdoc[k]);
+                        if (sk >= sb + WSTEP + 16) break;
+                        base += sk < gpos ? 1u : 0u;
+                        if (sk >= gpos && sk < gpos + 16) ds |= 1u << (uint32_t)(sk - gpos);
+                        if (sk >= gpos + 16 && sk < gpos + 32) nds |= 1u << (uint32_t)(sk - gpos - 16);
+                    }
+                    uint32_t prev = (lane_prev(ws) >> 15) & 1u;
+                    if (lane == 0) prev = (gpos > c.lo && gpos - 1 < c.hi) ? (is_ws(edge.w >> 24) ? 1u : 0u) : 1u;
+                    uint32_t own = 0xFFFFu;
+                    if (!(sb >= gs && sb + WSTEP <= ge)) {
+                        own = 0;
+                        if (gpos + 16 > gs && gpos < ge) {
+                            const uint32_t a = gpos < gs ? (uint32_t)(gs - gpos) : 0u;
+                            const uint32_t b = gpos + 16 > ge ? (uint32_t)(ge - gpos) : 16u;
+                            own = ((1u << b) - 1u) & ~((1u << a) - 1u);
+                        }
+                    }
+                    const uint32_t starts = ~ws & ((ws << 1) | prev | ds) & own & 0xFFFFu;
+                    /* NUL bytes end a term (strcmp), not a token: rare, exact masks only
+                     * when the wave holds one */
+                    uint32_t nul = 0, nnul = 0;
+                    {
+                        const uint32_t z = zero_bits(cur.x) | zero_bits(cur.y) | zero_bits(cur.z) | zero_bits(cur.w) |
+                                           (lane == 63 ? (zero_bits(edge.x) | zero_bits(edge.y) | zero_bits(edge.z) |
+                                                          zero_bits(edge.w)) : 0u);
+                        if (__ballot(z != 0u) != 0ull) {
+                            nul = compress4(zero_bits(cur.x)) | (compress4(zero_bits(cur.y)) << 4) |
+                                  (compress4(zero_bits(cur.z)) << 8) | (compress4(zero_bits(cur.w)) << 12);
+                            nnul = lane_next(nul);
+                            if (lane == 63)
+                                nnul = compress4(zero_bits(edge.x)) | (compress4(zero_bits(edge.y)) << 4) |
+                                       (compress4(zero_bits(edge.z)) << 8) | (compress4(zero_bits(edge.w)) << 12);
+                        }
+                    }
+                    const uint32_t stop = ws | ds;
+                    uint32_t nstop = lane_next(stop);
+                    if (lane == 63) {
+                        uint32_t nws = ws_mask16_swar(edge);
+                        if (!inner) nws |= bounds_ws(gpos + 16, c.lo, c.hi);
+                        nstop = nws | nds;
+                    }
+                    /* term end = the first stop after the start byte or the first NUL from
+                     * the start byte on (a NUL start gives the empty term) */
+                    const uint32_t stop32 = stop | (nstop << 16), nul32 = nul | (nnul << 16);
+                    /* ---- token entries (wave prefix sum over the lanes' start counts) ---- */
+                    const uint32_t nmine = (uint32_t)__popc(starts);
+                    const uint32_t incl = wave_incl_scan(nmine);
+                    const uint32_t ntok = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                    if (ntok == 0) continue;
+                    tokens_wg += ntok;
+                    for (uint32_t tb = 0; tb < ntok; tb += TLW) {
+                        {
+                            uint32_t sm = starts, idx = incl - nmine;
+                            while (sm) {
+                                const uint32_t i = __builtin_ctz(sm);
+                                sm &= sm - 1;
+                                if (idx - tb < (uint32_t)TLW) {
+                                    const uint32_t e = ((stop32 >> i) & ~1u) | (nul32 >> i);
+                                    const uint32_t len = e ? (uint32_t)__builtin_ctz(e) : LEN_LONG;
+                                    const uint32_t rel = base + (uint32_t)__popc(ds & ((2u << i) - 1u));
+                                    tl[idx - tb] = ((uint32_t)lane << 4 | i) | ((len < 16u ? len : LEN_LONG) << 10) |
+                                                   (rel << 16);
+                                }
+                                ++idx;
+                            }
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                        const uint32_t cnt = (ntok - tb) < (uint32_t)TLW ? (ntok - tb) : (uint32_t)TLW;
+                        /* ---- rounds of 64 tokens; the vocabulary loads of round r+1 are
+                         * issued before round r is counted ---- */
+                        for (uint32_t t0 = 0; t0 < cnt; t0 += 64) {
+                            Round q;
+                            const uint32_t t = t0 + lane;
+                            const bool val = t < cnt;
+                            const uint32_t e = val ? tl[t] : 0u;
+                            const uint32_t pos = e & 1023u, len = (e >> 10) & 31u;
+                            q.rel = e >> 16;
+                            q.ap = sb + pos;
+                            q.kind = val ? (len == LEN_LONG ? 2u : 1u) : 0u;
+                            const u32x4u raw = *reinterpret_cast<const u32x4u*>(stage + pos);
+                            const uint4 sl = S.sel[len & 15u];
+                            q.k0 = __builtin_amdgcn_perm(0x09090909u, raw.x, sl.x);
+                            q.k1 = __builtin_amdgcn_perm(0x09090909u, raw.y, sl.y);
+                            q.k2 = __builtin_amdgcn_perm(0x09090909u, raw.z, sl.z);
+                            q.k3 = __builtin_amdgcn_perm(0x09090909u, raw.w, sl.w);
+                            q.hv = q.kind == 1u ? (uint32_t)(key_hash(((uint64_t)q.k1 << 32) | q.k0,
+                                                                      ((uint64_t)q.k3 << 32) | q.k2) & v.mask)
+                                                : 0u;
+                            /* the home slot and the next one: a key displaced by one slot
+                             * (linear probing) resolves without a dependent load */
+                            q.s4 = v.keys[q.hv];
+                            q.t4 = v.keys[(q.hv + 1) & (uint32_t)v.mask];
+                            if (pending) finish(pend);
+                            pend = q;
+                            pending = true;
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    }
+                }
+            }
+            if (pending) { finish(pend); pending = false; }
+            /* group end is a document boundary (or the chunk end): emit everything */
+            st_flush(S, o, gd0, ng, cs, ce);
+            if ((uint32_t)tid < ng) {
+                const uint32_t n = S.dsz[tid];
+                if (n) {
+                    const uint32_t d = gd0 + tid;
+                    if (S.gdoc[tid] >= cs && S.gdoc[tid + 1] <= ce) o.doc_size[d] = n;
+                    else atomicAdd(&o.doc_size[d], n);
+                }
+            }
+            lds_barrier();
+            if (gd0 + GCAP < gd0) break; /* overflow guard */
+        }
+        if (tid == 0) S.next_chunk = next_claim;
+        lds_barrier();
+    }
+    if (lane == 0 && tokens_wg) atomicAdd(o.ntokens, tokens_wg);
+}
+
+int launch_tokcount_st(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc, uint64_t c0,
+                       uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s) {
+    if (c1 <= c0) return 0;
+    if (v.mask >= (1ull << SLOT_BITS)) return -3; /* slot must fit the LDS entry */
+    static_assert(sizeof(StShared) <= 40960, "four workgroups per CU");
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+    }
+    const uint64_t wgs = (uint64_t)ncu * 4;
+    const uint64_t grid = (c1 - c0) < wgs ? (c1 - c0) : wgs;
+    k_tokcount_st<<<(unsigned)grid, NT, 0, s>>>(c, chunk_start, chunk_doc, c0, c1, v, o);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
