@@ -36,6 +36,13 @@
 #include "dev_vocab.h"
 #include "kernels.h"
 
+/* timing-only ablation builds (make variant NAME=s1 DEFS=-DK1S_ABL=1; results invalid):
+ * 1 no vocabulary loads/compare (slot from the key), 2 no LDS counting, 4 no token rounds,
+ * 8 no token entries (walk + flush only), 16 no corpus loads */
+#ifndef K1S_ABL
+#define K1S_ABL 0
+#endif
+
 namespace {
 
 constexpr int NT = 256;                   /* threads per workgroup */
@@ -70,10 +77,9 @@ struct StShared {
     uint4 sel[16];                        /* v_perm selectors of a term of length n */
     uint8_t dpart[GCAP];                  /* document has overflow records */
     uint32_t fill;                        /* table claims of the group */
-    uint32_t over;                        /* overflow mode */
+    uint64_t cur_chunk, nxt_chunk;        /* dynamic chunk schedule: this chunk and the next */
     uint32_t wsum[NWAVE];
     unsigned long long rec_base, part_base;
-    uint64_t next_chunk;                  /* dynamic chunk schedule */
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -328,7 +334,9 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
      * LDS (doc, slot) count, overflow accounting */
     auto finish = [&](const Round& r) {
         uint32_t slot = INVALID_SLOT;
-        if (r.kind == 1u) {
+        if (K1S_ABL & 1) {
+            slot = r.kind ? (r.k0 ^ r.k1 * 7u ^ r.k2) & (uint32_t)v.mask : INVALID_SLOT;
+        } else if (r.kind == 1u) {
             const bool hit0 = r.s4.x == r.k0 && r.s4.y == r.k1 && r.s4.z == r.k2 && r.s4.w == r.k3;
             const bool hit1 = r.t4.x == r.k0 && r.t4.y == r.k1 && r.t4.z == r.k2 && r.t4.w == r.k3;
             slot = hit0 ? r.hv : hit1 ? ((r.hv + 1) & (uint32_t)v.mask)
@@ -347,9 +355,10 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                 atomicAdd(&S.dsz[r.rel], 1u);
             }
         }
+        if (K1S_ABL & 2) return;
         const uint64_t key = slot == INVALID_SLOT ? ~0ull : (((uint64_t)r.rel << SLOT_BITS) | slot);
         const uint32_t hl = tbl_hash(key);
-        const bool over = S.over != 0;
+        const bool over = S.fill >= FILL_LIMIT;
         const bool valid = key != ~0ull;
         unsigned long long old = 0ull, nx = 0ull;
         if (valid) {
@@ -366,27 +375,40 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
         }
         const uint32_t wc = (uint32_t)__popcll(__ballot(claims != 0u));
         if (wc && lane == 0) {
-            const uint32_t f = atomicAdd(&S.fill, wc);
-            if (f + wc >= FILL_LIMIT) S.over = 1;
+            /* no return value: the next rounds read fill (claims of up to 4 waves x 64 lanes
+             * in flight fit the table's margin above FILL_LIMIT) */
+            (void)atomicAdd(&S.fill, wc);
         }
     };
 
-    if (tid == 0) S.next_chunk = c0 + atomicAdd(o.chunk_ctr, 1ull);
+    /* chunks come from a global counter, claimed two ahead: the next chunk is known to every
+     * wave while this one runs, so its first step is loaded before this chunk's flush (the
+     * claim's own round trip is waited for only at the chunk end) */
+    if (tid == 0) {
+        S.cur_chunk = c0 + atomicAdd(o.chunk_ctr, 1ull);
+        S.nxt_chunk = c0 + atomicAdd(o.chunk_ctr, 1ull);
+    }
     lds_barrier();
-    uint64_t next_claim = 0;
+    uint64_t claim = 0;
     uint8_t* const stage = reinterpret_cast<uint8_t*>(&S.w.stage[wid][0]);
     uint32_t* const tl = S.w.tl[wid];
-    for (uint64_t chunk = uni64(S.next_chunk); chunk < c1; chunk = uni64(S.next_chunk)) {
-        if (tid == 0) next_claim = c0 + atomicAdd(o.chunk_ctr, 1ull);
+    const uint64_t lane_off = 16ull * lane;
+    uint4 xf = make_uint4(0, 0, 0, 0), xe = xf;   /* the next chunk's first step (this wave's) */
+    uint64_t xb0 = ~0ull;                         /* ... loaded for this step base */
+    for (;;) {
+        const uint64_t chunk = uni64(S.cur_chunk), nxt = uni64(S.nxt_chunk);
+        if (chunk >= c1) break;
+        if (tid == 0) claim = c0 + atomicAdd(o.chunk_ctr, 1ull);
         const uint64_t cs = chunk_start[chunk], ce = chunk_start[chunk + 1];
         const uint32_t dfirst = chunk_doc[chunk], dlast = chunk_doc[chunk + 1];
+        const uint64_t ns = nxt < c1 ? chunk_start[nxt] : 0;
         if (cs < ce)
         for (uint32_t gd0 = dfirst; gd0 <= dlast; gd0 += GCAP) {
             gd0_cur = gd0;
             const uint32_t ng = (dlast + 1 - gd0) < (uint32_t)GCAP ? (dlast + 1 - gd0) : (uint32_t)GCAP;
             for (uint32_t k = tid; k <= ng; k += NT) S.gdoc[k] = c.doc_off[gd0 + k];
             if (tid < GCAP) { S.dsz[tid] = 0; S.dpart[tid] = 0; }
-            if (tid == 0) { S.fill = 0; S.over = 0; }
+            if (tid == 0) S.fill = 0;
             lds_barrier();
             const uint64_t g0 = uni64(S.gdoc[0]), gn = uni64(S.gdoc[ng]);
             const uint64_t gs = g0 > cs ? g0 : cs;
@@ -394,22 +416,35 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
             if (gs < ge) {
                 const uint64_t b0 = gs & ~(uint64_t)15;
                 const uint32_t nsteps = (uint32_t)((ge - b0 + WSTEP - 1) / WSTEP);
-                const uint64_t lane_off = 16ull * lane;
-                uint4 pf0 = make_uint4(0, 0, 0, 0), pe0 = pf0;
+                /* two steps in flight: s + 4 and s + 8 (the first from the previous chunk's
+                 * prefetch when it was for this base) */
+                uint4 pf0 = xf, pe0 = xe, pf1 = make_uint4(0, 0, 0, 0), pe1 = pf1;
                 {
                     const uint64_t a0 = b0 + (uint64_t)wid * WSTEP + lane_off;
-                    pf0 = ld16c(c.bytes, last_blk, a0);
-                    if (edge_lane) pe0 = ld16c(c.bytes, last_blk, a0 + eoff);
+                    if (b0 != xb0) {
+                        pf0 = ld16c(c.bytes, last_blk, a0);
+                        if (edge_lane) pe0 = ld16c(c.bytes, last_blk, a0 + eoff);
+                    }
+                    pf1 = ld16c(c.bytes, last_blk, a0 + 1ull * NWAVE * WSTEP);
+                    if (edge_lane) pe1 = ld16c(c.bytes, last_blk, a0 + 1ull * NWAVE * WSTEP + eoff);
                 }
+                xb0 = ~0ull;
                 uint32_t wr = 0;             /* wave-uniform: document containing the step start */
                 for (uint32_t s = wid; s < nsteps; s += NWAVE) {
                     const uint64_t sb = b0 + (uint64_t)s * WSTEP;
                     const uint64_t gpos = sb + lane_off;
                     const uint4 cur = pf0, edge = pe0;
+                    pf0 = pf1;
+                    pe0 = pe1;
                     {
-                        const uint64_t a1 = gpos + 1ull * NWAVE * WSTEP; /* harmless past ge */
-                        pf0 = ld16c(c.bytes, last_blk, a1);
-                        if (edge_lane) pe0 = ld16c(c.bytes, last_blk, a1 + eoff);
+                        const uint64_t a1 = gpos + 2ull * NWAVE * WSTEP; /* harmless past ge */
+#if K1S_ABL & 16
+                        pf1 = make_uint4(0x20616161u ^ (uint32_t)a1, 0x61612061u, 0x61206161u, 0x20616161u);
+                        pe1 = pf1;
+#else
+                        pf1 = ld16c(c.bytes, last_blk, a1);
+                        if (edge_lane) pe1 = ld16c(c.bytes, last_blk, a1 + eoff);
+#endif
                     }
                     /* the step's bytes (and the 16 after it) into the wave's stage; this
                      * wave's reads of the previous step were issued before (LDS in order) */
@@ -423,10 +458,10 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                      * lane's first byte: a wave-uniform loop over the group's doc_off */
                     while (wr + 1 < ng && uni64(S.gdoc[wr + 1]) <= sb) ++wr;
                     uint32_t ds = 0, nds = 0, base = wr;
-                    for (uint32_t k = wr + 1; k <= ng; ++k) {
+                    for (uint32_t k = wr; k <= ng; ++k) {   /* k = wr: a start AT sb is a start too */
                         const uint64_t sk = uni64(S.gdoc[k]);
                         if (sk >= sb + WSTEP + 16) break;
-                        base += sk < gpos ? 1u : 0u;
+                        base += (k > wr && sk < gpos) ? 1u : 0u;
                         if (sk >= gpos && sk < gpos + 16) ds |= 1u << (uint32_t)(sk - gpos);
                         if (sk >= gpos + 16 && sk < gpos + 32) nds |= 1u << (uint32_t)(sk - gpos - 16);
                     }
@@ -474,6 +509,7 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                     const uint32_t ntok = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
                     if (ntok == 0) continue;
                     tokens_wg += ntok;
+                    if (K1S_ABL & 8) { if (lane == 0) atomicAdd(&S.dsz[base], ntok); continue; }
                     for (uint32_t tb = 0; tb < ntok; tb += TLW) {
                         {
                             uint32_t sm = starts, idx = incl - nmine;
@@ -483,7 +519,12 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                                 if (idx - tb < (uint32_t)TLW) {
                                     const uint32_t e = ((stop32 >> i) & ~1u) | (nul32 >> i);
                                     const uint32_t len = e ? (uint32_t)__builtin_ctz(e) : LEN_LONG;
-                                    const uint32_t rel = base + (uint32_t)__popc(ds & ((2u << i) - 1u));
+                                    /* the document of byte i: the lane's first-byte document,
+                                     * advanced past every start <= i (empty documents share
+                                     * a start, so walk doc_off instead of counting bits) */
+                                    uint32_t rel = base;
+                                    if (ds & ((2u << i) - 1u))
+                                        while (rel + 1 < ng && S.gdoc[rel + 1] <= gpos + i) ++rel;
                                     tl[idx - tb] = ((uint32_t)lane << 4 | i) | ((len < 16u ? len : LEN_LONG) << 10) |
                                                    (rel << 16);
                                 }
@@ -496,7 +537,7 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                         const uint32_t cnt = (ntok - tb) < (uint32_t)TLW ? (ntok - tb) : (uint32_t)TLW;
                         /* ---- rounds of 64 tokens; the vocabulary loads of round r+1 are
                          * issued before round r is counted ---- */
-                        for (uint32_t t0 = 0; t0 < cnt; t0 += 64) {
+                        for (uint32_t t0 = 0; t0 < cnt && !(K1S_ABL & 4); t0 += 64) {
                             Round q;
                             const uint32_t t = t0 + lane;
                             const bool val = t < cnt;
@@ -516,8 +557,13 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                                                 : 0u;
                             /* the home slot and the next one: a key displaced by one slot
                              * (linear probing) resolves without a dependent load */
+#if K1S_ABL & 1
+                            q.s4 = make_uint4(q.k0, q.k1, q.k2, q.k3);
+                            q.t4 = q.s4;
+#else
                             q.s4 = v.keys[q.hv];
                             q.t4 = v.keys[(q.hv + 1) & (uint32_t)v.mask];
+#endif
                             if (pending) finish(pend);
                             pend = q;
                             pending = true;
@@ -529,6 +575,14 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                 }
             }
             if (pending) { finish(pend); pending = false; }
+            /* the last group of the chunk: this wave's first step of the next chunk is loaded
+             * now, so its latency passes during the flush */
+            if (gd0 + GCAP > dlast && nxt < c1) {
+                xb0 = ns & ~(uint64_t)15;
+                const uint64_t a0 = xb0 + (uint64_t)wid * WSTEP + lane_off;
+                xf = ld16c(c.bytes, last_blk, a0);
+                if (edge_lane) xe = ld16c(c.bytes, last_blk, a0 + eoff);
+            }
             /* group end is a document boundary (or the chunk end): emit everything */
             st_flush(S, o, gd0, ng, cs, ce);
             if ((uint32_t)tid < ng) {
@@ -542,7 +596,7 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
             lds_barrier();
             if (gd0 + GCAP < gd0) break; /* overflow guard */
         }
-        if (tid == 0) S.next_chunk = next_claim;
+        if (tid == 0) { S.cur_chunk = nxt; S.nxt_chunk = claim; }
         lds_barrier();
     }
     if (lane == 0 && tokens_wg) atomicAdd(o.ntokens, tokens_wg);
