@@ -38,9 +38,18 @@
 
 /* timing-only ablation builds (make variant NAME=s1 DEFS=-DK1S_ABL=1; results invalid):
  * 1 no vocabulary loads/compare (slot from the key), 2 no LDS counting, 4 no token rounds,
- * 8 no token entries (walk + flush only), 16 no corpus loads */
+ * 8 no token entries (walk + flush only), 16 no corpus loads, 32 flush without record
+ * writes, 64 flush = table clear only */
 #ifndef K1S_ABL
 #define K1S_ABL 0
+#endif
+/* corpus prefetch: ST_PF2 keeps two steps in flight per wave (else one), ST_XPF loads the
+ * next chunk's first step before this chunk's flush */
+#ifndef ST_PF2
+#define ST_PF2 0
+#endif
+#ifndef ST_XPF
+#define ST_XPF 0
 #endif
 
 namespace {
@@ -51,15 +60,14 @@ constexpr int WSTEP = 1024;               /* bytes per wave step: one 16-byte gr
 constexpr int TB = 3584;                  /* LDS table entries (u64): 14 per thread */
 constexpr int EPT = TB / NT;
 constexpr uint32_t FILL_LIMIT = TB - NT * 2 - 64; /* claims after which overflow mode starts */
-constexpr int GCAP = 256;                 /* documents per group (doc-in-group: 8 bits) */
-constexpr uint32_t SLOT_BITS = 28;
-constexpr uint32_t CNT_BITS = 24;
-constexpr uint64_t CNT_MASK = (1ull << CNT_BITS) - 1ull;
+constexpr int GCAP = 256;                 /* documents per group at most (LDS arrays) */
+constexpr uint32_t SLOT_BITS = 28;        /* vocabulary slots < 2^28 */
 constexpr int TLW = 192;                  /* token entries per wave and compaction pass */
 constexpr uint32_t LEN_LONG = 31u;        /* token entry: term of >= 16 bytes or past the window */
 
 struct StShared {
-    unsigned long long T[TB];             /* (doc, slot) -> count */
+    uint32_t TK[TB];                      /* key32 = 1 << 31 | doc-in-group << sb | slot (0: empty) */
+    uint32_t TC[TB];                      /* its count */
     uint64_t gdoc[GCAP + 1];              /* doc_off of the group's documents */
     uint32_t dsz[GCAP];                   /* docSize accumulators */
     union {
@@ -109,11 +117,31 @@ __device__ __forceinline__ uint32_t compress4(uint32_t m) {   /* bits 7, 15, 23,
     return m & 0xFu;
 }
 
-__device__ __forceinline__ uint32_t tbl_hash(uint64_t key) {
-    const uint32_t k = (uint32_t)key ^ (uint32_t)(key >> 28) * 0x9E3779B1u;
-    return (uint32_t)(((uint64_t)(k * 0x85EBCA6Bu) * (uint64_t)TB) >> 32);   /* [0, TB) */
+/* The LDS count table: buckets of 4 slots (TK: 32-bit keys, 0 = empty; TC: counts).  A key
+ * lives in its home bucket unless that bucket was full when it was inserted, then in the
+ * next bucket with room (slots are only emptied by the flush, so a home bucket with an
+ * empty slot proves a key is not further on). */
+constexpr uint32_t NB = TB / 4;
+__device__ __forceinline__ uint32_t bkt_hash(uint32_t key) {
+    return (uint32_t)(((uint64_t)(key * 0x9E3779B1u) * (uint64_t)NB) >> 32);   /* [0, NB) */
 }
-__device__ __forceinline__ uint32_t tbl_next(uint32_t h) { return h + 1 == (uint32_t)TB ? 0u : h + 1; }
+__device__ __forceinline__ uint32_t bkt_next(uint32_t b) { return b + 1 == NB ? 0u : b + 1; }
+__device__ __forceinline__ uint4 bkt_read(StShared& S, uint32_t b) { return reinterpret_cast<const uint4*>(S.TK)[b]; }
+/* slot of `key` in bucket kk (4 if absent) */
+__device__ __forceinline__ uint32_t bkt_match(uint4 kk, uint32_t key) {
+    return kk.x == key ? 0u : kk.y == key ? 1u : kk.z == key ? 2u : kk.w == key ? 3u : 4u;
+}
+/* the first empty slot of bucket kk, scanning from slot key & 3 (different keys spread over
+ * the free slots of a bucket they share), 4 if full */
+__device__ __forceinline__ uint32_t bkt_empty(uint4 kk, uint32_t key) {
+    const uint32_t em = (kk.x == 0u ? 1u : 0u) | (kk.y == 0u ? 2u : 0u) | (kk.z == 0u ? 4u : 0u) | (kk.w == 0u ? 8u : 0u);
+    if (!em) return 4u;
+    const uint32_t r0 = key & 3u;
+    const uint32_t rot = ((em | (em << 4)) >> r0) & 0xFu;
+    return ((uint32_t)__builtin_ctz(rot) + r0) & 3u;
+}
+__device__ __forceinline__ void tbl_read(StShared& S, uint32_t i, uint32_t& key, uint32_t& cnt) { key = S.TK[i]; cnt = S.TC[i]; }
+__device__ __forceinline__ void tbl_clear(StShared& S, uint32_t i) { S.TK[i] = 0u; S.TC[i] = 0u; }
 
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
@@ -154,33 +182,38 @@ __device__ __noinline__ void overflow_record(unsigned long long* part_alloc, uin
     else atomicOr(status, ST_PART_FULL);
 }
 
-/* Counts `key` from slot h on (the first probe returned `old`; `nx` is a plain read of the
- * next slot from the same LDS batch).  Returns 1 when this call claimed an entry.  A probe
- * run longer than PMAX, or a new pair in overflow mode, becomes a partial record of count
- * 1 (the merge sums them), so the table never fills or loops. */
-constexpr int PMAX = 64;
-__device__ __forceinline__ uint32_t tbl_count(StShared& S, const K1Out& o, uint64_t key, uint32_t h,
-                                              unsigned long long old, unsigned long long nx, bool over, uint32_t gd0) {
-    const unsigned long long ent = (key << CNT_BITS) | 1ull;
-    if (old != 0ull && (old >> CNT_BITS) != key) {
-        h = tbl_next(h);
-        if ((nx >> CNT_BITS) == key && nx != 0ull) { atomicAdd(&S.T[h], 1ull); return 0u; }
-        old = (nx == 0ull && !over) ? atomicCAS(&S.T[h], 0ull, ent) : nx;
-    }
-    for (int probe = 2;; ++probe) {
-        if (old == 0ull) {
-            if (!over) return 1u;
-            break;
+/* Counts `key` the slow way, from bucket b on, re-reading each bucket: the home bucket was
+ * full without the key, another lane's claim took the free slot this lane wanted, or the
+ * group is in overflow mode.  Returns 1 when this call claimed a slot.  A key not in the
+ * table in overflow mode, or after PMAX buckets, becomes a partial record of count 1 (the
+ * merge sums them), so the table never fills or loops. */
+constexpr int PMAX = 16;
+#ifndef BKT_SLOW_ATTR
+#define BKT_SLOW_ATTR __forceinline__
+#endif
+__device__ BKT_SLOW_ATTR uint32_t bkt_slow(StShared& S, const K1Out& o, uint32_t key, uint32_t b, bool over,
+                                          uint32_t gd0, uint32_t sb) {
+    for (int probe = 0, tries = 0; probe < PMAX && tries < 64; ++tries) {
+        const uint4 kk = bkt_read(S, b);
+        const uint32_t j = bkt_match(kk, key);
+        if (j < 4u) { atomicAdd(&S.TC[4 * b + j], 1u); return 0u; }
+        const uint32_t e = bkt_empty(kk, key);
+        if (e < 4u) {
+            if (over) break;               /* not in the table: a bucket with room ends the chain */
+            const uint32_t old = atomicCAS(&S.TK[4 * b + e], 0u, key);
+            if (old == 0u || old == key) {
+                atomicAdd(&S.TC[4 * b + e], 1u);
+                return old == 0u ? 1u : 0u;
+            }
+            continue;                      /* lost the slot to another key: re-read this bucket */
         }
-        if ((old >> CNT_BITS) == key) { atomicAdd(&S.T[h], 1ull); return 0u; }
-        if (probe >= PMAX) break;
-        h = tbl_next(h);
-        old = over ? S.T[h] : atomicCAS(&S.T[h], 0ull, ent);
+        b = bkt_next(b);
+        ++probe;
     }
-    const uint32_t rel = (uint32_t)(key >> SLOT_BITS);
+    const uint32_t rel = (key & 0x7FFFFFFFu) >> sb;
     S.dpart[rel] = 1;
     overflow_record(o.part_alloc, o.part_cap, o.part_doc, o.part_slot, o.part_cnt, o.status, gd0 + rel,
-                    (uint32_t)key & ((1u << SLOT_BITS) - 1u));
+                    key & ((1u << sb) - 1u));
     return 0u;
 }
 
@@ -209,20 +242,29 @@ __device__ __forceinline__ uint32_t wave_agg_add_rtn(uint32_t* ctr, uint32_t idx
     return k;
 }
 
-/* Emits every table entry of the group as records and clears the table (tokcount_vs.hip's
- * flush: complete documents to the record stream, documents crossing a chunk edge, over
- * K5's in-LDS sort size or overflowed to the partial stream). */
-__device__ void st_flush(StShared& S, const K1Out& o, uint32_t gd0, uint32_t ng, uint64_t cs, uint64_t ce) {
+/* Emits every table entry of the group as records and clears the table: complete
+ * documents to the record stream, documents crossing a chunk edge, over K5's in-LDS sort
+ * size or overflowed to the partial stream.  Per-document counts (wave-aggregated LDS
+ * adds), a block scan of them, then every entry is written straight to its record slot
+ * (its rank inside its document from a wave-aggregated LDS counter): no LDS staging pass. */
+__device__ void st_flush(StShared& S, const K1Out& o, uint32_t gd0, uint32_t ng, uint64_t cs, uint64_t ce,
+                         uint32_t sb) {
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));   /* keep j * NT + tid out of the chunk loop (no spills) */
     lds_barrier();                  /* every wave's walk is done (the walk state aliases dcnt...) */
+    if (K1S_ABL & 64) {
+        for (int j = 0; j < EPT; ++j) tbl_clear(S, j * NT + tid);
+        lds_barrier();
+        return;
+    }
     if (tid < GCAP) { S.f.dcnt[tid] = 0; S.f.drun[tid] = 0; }
     lds_barrier();
-    unsigned long long e[EPT];
+    const uint32_t smask = (1u << sb) - 1u;
+    uint32_t ek[EPT], ec[EPT];
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
-        e[j] = S.T[j * NT + tid];
-        if (e[j]) wave_agg_add(&S.f.dcnt[0], (uint32_t)(e[j] >> (CNT_BITS + SLOT_BITS)));
+        tbl_read(S, j * NT + tid, ek[j], ec[j]);
+        if (ek[j]) wave_agg_add(&S.f.dcnt[0], (ek[j] & 0x7FFFFFFFu) >> sb);
     }
     lds_barrier();
     uint32_t packed = 0;
@@ -241,7 +283,7 @@ __device__ void st_flush(StShared& S, const K1Out& o, uint32_t gd0, uint32_t ng,
     uint32_t tot;
     const uint32_t off = block_excl_scan<NT, true>(packed, S.wsum, &tot);
     if ((uint32_t)tid < ng) S.f.doff[tid] = off;
-    const uint32_t nrec = tot & 0xFFFFu, npart = tot >> 16, ntot = nrec + npart;
+    const uint32_t nrec = tot & 0xFFFFu, npart = tot >> 16;
     if (tid == 0) {
         const unsigned long long rb = nrec ? atomicAdd(o.rec_alloc, (unsigned long long)nrec) : 0ull;
         if (rb + nrec > o.rec_cap) atomicOr(o.status, ST_REC_FULL);
@@ -260,33 +302,21 @@ __device__ void st_flush(StShared& S, const K1Out& o, uint32_t gd0, uint32_t ng,
     }
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
-        if (e[j]) {
-            const uint32_t rel = (uint32_t)(e[j] >> (CNT_BITS + SLOT_BITS));
-            const uint32_t slot = (uint32_t)(e[j] >> CNT_BITS) & ((1u << SLOT_BITS) - 1u);
-            const uint64_t cnt = e[j] & CNT_MASK;
+        const uint32_t key = ek[j];
+        if ((K1S_ABL & 32) && key) { tbl_clear(S, j * NT + tid); continue; }
+        if (key) {
+            const uint32_t rel = (key & 0x7FFFFFFFu) >> sb;
             const uint32_t k = wave_agg_add_rtn(&S.f.drun[0], rel);
             const uint32_t dof = S.f.doff[rel];
-            if (S.f.dstate[rel] == 2) S.T[(dof & 0xFFFFu) + k] = slot | (cnt << 32);
-            else S.T[nrec + (dof >> 16) + k] = slot | ((uint64_t)rel << SLOT_BITS) | (cnt << 36);
-        }
-    }
-    lds_barrier();
-#pragma unroll
-    for (int j = 0; j < EPT; ++j) {
-        const uint32_t i = j * NT + tid;
-        if (i < nrec) {
-            const unsigned long long w = S.T[i];
-            if (rec_ok) { o.rec_slot[rb + i] = (uint32_t)w; o.rec_cnt[rb + i] = (uint32_t)(w >> 32); }
-        } else if (i < ntot) {
-            const unsigned long long w = S.T[i];
-            const uint64_t q = pb + (i - nrec);
-            if (part_ok) {
-                o.part_doc[q] = gd0 + ((uint32_t)(w >> SLOT_BITS) & 0xFFu);
-                o.part_slot[q] = (uint32_t)w & ((1u << SLOT_BITS) - 1u);
-                o.part_cnt[q] = (uint32_t)(w >> 36);
+            if (S.f.dstate[rel] == 2) {
+                const uint64_t q = rb + (dof & 0xFFFFu) + k;
+                if (rec_ok) { o.rec_slot[q] = key & smask; o.rec_cnt[q] = ec[j]; }
+            } else {
+                const uint64_t q = pb + (dof >> 16) + k;
+                if (part_ok) { o.part_doc[q] = gd0 + rel; o.part_slot[q] = key & smask; o.part_cnt[q] = ec[j]; }
             }
+            tbl_clear(S, j * NT + tid);
         }
-        S.T[i] = 0ull;
     }
 }
 
@@ -306,14 +336,14 @@ __device__ __forceinline__ uint32_t perm_sel(uint32_t n, uint32_t k) {
 
 __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64_t* __restrict__ chunk_start,
                                                        const uint32_t* __restrict__ chunk_doc, uint64_t c0,
-                                                       uint64_t c1, VocabDev v, K1Out o) {
+                                                       uint64_t c1, VocabDev v, K1Out o, uint32_t sb, uint32_t gcap) {
     __shared__ __attribute__((aligned(16))) StShared S;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint64_t last_blk = c.nbytes ? ((c.nbytes - 1) & ~(uint64_t)15) : 0;
     const bool edge_lane = lane == 0 || lane == 63;
     const uint64_t eoff = lane == 0 ? (uint64_t)0 - 16ull : 16ull;
 
-    for (int j = 0; j < EPT; ++j) S.T[j * NT + tid] = 0ull;
+    for (int j = 0; j < EPT; ++j) tbl_clear(S, j * NT + tid);
     if (tid < 64) {
         const uint32_t n = (uint32_t)tid >> 2, k = (uint32_t)tid & 3u;
         (&S.sel[n].x)[k] = perm_sel(n, k);
@@ -330,9 +360,9 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
     Round pend{};
     bool pending = false;
     uint32_t gd0_cur = 0;
-    /* finish a round: vocabulary slot (miss path: lock-free insert / long term), docSize,
-     * LDS (doc, slot) count, overflow accounting */
-    auto finish = [&](const Round& r) {
+    /* resolve a round: vocabulary slot (miss path: lock-free insert / long term) and
+     * docSize; returns the LDS table key (0: no token) */
+    auto resolve = [&](const Round& r) -> uint32_t {
         uint32_t slot = INVALID_SLOT;
         if (K1S_ABL & 1) {
             slot = r.kind ? (r.k0 ^ r.k1 * 7u ^ r.k2) & (uint32_t)v.mask : INVALID_SLOT;
@@ -355,30 +385,52 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                 atomicAdd(&S.dsz[r.rel], 1u);
             }
         }
-        if (K1S_ABL & 2) return;
-        const uint64_t key = slot == INVALID_SLOT ? ~0ull : (((uint64_t)r.rel << SLOT_BITS) | slot);
-        const uint32_t hl = tbl_hash(key);
+        if (K1S_ABL & 2) return 0u;
+        return slot == INVALID_SLOT ? 0u : (0x80000000u | (r.rel << sb) | slot);
+    };
+    /* The LDS count of a round: ONE ds_read_b128 of the key's home bucket; a match is
+     * counted with a non-returning add, a new key claims a free slot of the bucket with one
+     * CAS (then adds); the rare rest (full bucket, a lost race, overflow mode) takes
+     * bkt_slow.  (A linear-probing table of u64 entries, CAS first, took the same time at
+     * about twice the instructions.) */
+    auto count = [&](uint32_t key) {
         const bool over = S.fill >= FILL_LIMIT;
-        const bool valid = key != ~0ull;
-        unsigned long long old = 0ull, nx = 0ull;
-        if (valid) {
-            old = over ? S.T[hl] : atomicCAS(&S.T[hl], 0ull, (key << CNT_BITS) | 1ull);
-            nx = S.T[tbl_next(hl)];
+        const uint32_t b = bkt_hash(key);
+        uint32_t claims = 0u;
+        bool slow = false;
+        if (key) {
+            const uint4 kk = bkt_read(S, b);
+            const uint32_t j = bkt_match(kk, key);
+            if (j < 4u) {
+                atomicAdd(&S.TC[4 * b + j], 1u);
+            } else {
+                const uint32_t e = bkt_empty(kk, key);
+                if (e < 4u && !over) {
+                    const uint32_t old = atomicCAS(&S.TK[4 * b + e], 0u, key);
+                    if (old == 0u || old == key) {
+                        atomicAdd(&S.TC[4 * b + e], 1u);
+                        claims = old == 0u ? 1u : 0u;
+                    } else {
+                        slow = true;
+                    }
+                } else {
+                    slow = true;
+                }
+            }
         }
-        const bool hit = valid && old != 0ull && (old >> CNT_BITS) == key;
-        const bool claimed = valid && old == 0ull && !over;
-        if (hit) atomicAdd(&S.T[hl], 1ull);
-        uint32_t claims = claimed ? 1u : 0u;
-        const bool rest = valid && !hit && !claimed;
-        if (__ballot(rest) != 0ull) {
-            if (rest) claims = tbl_count(S, o, key, hl, old, nx, over, gd0_cur);
+        if (__ballot(slow) != 0ull) {
+            if (slow) claims = bkt_slow(S, o, key, b, over, gd0_cur, sb);
         }
         const uint32_t wc = (uint32_t)__popcll(__ballot(claims != 0u));
         if (wc && lane == 0) {
-            /* no return value: the next rounds read fill (claims of up to 4 waves x 64 lanes
-             * in flight fit the table's margin above FILL_LIMIT) */
+            /* no return value: later rounds read fill (claims of up to 4 waves x 64 lanes in
+             * flight fit the table's margin above FILL_LIMIT) */
             (void)atomicAdd(&S.fill, wc);
         }
+    };
+    auto finish = [&](const Round& r) { count(resolve(r)); };
+    auto drain = [&]() {
+        if (pending) { finish(pend); pending = false; }
     };
 
     /* chunks come from a global counter, claimed two ahead: the next chunk is known to every
@@ -403,9 +455,9 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
         const uint32_t dfirst = chunk_doc[chunk], dlast = chunk_doc[chunk + 1];
         const uint64_t ns = nxt < c1 ? chunk_start[nxt] : 0;
         if (cs < ce)
-        for (uint32_t gd0 = dfirst; gd0 <= dlast; gd0 += GCAP) {
+        for (uint32_t gd0 = dfirst; gd0 <= dlast; gd0 += gcap) {
             gd0_cur = gd0;
-            const uint32_t ng = (dlast + 1 - gd0) < (uint32_t)GCAP ? (dlast + 1 - gd0) : (uint32_t)GCAP;
+            const uint32_t ng = (dlast + 1 - gd0) < gcap ? (dlast + 1 - gd0) : gcap;
             for (uint32_t k = tid; k <= ng; k += NT) S.gdoc[k] = c.doc_off[gd0 + k];
             if (tid < GCAP) { S.dsz[tid] = 0; S.dpart[tid] = 0; }
             if (tid == 0) S.fill = 0;
@@ -418,15 +470,20 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                 const uint32_t nsteps = (uint32_t)((ge - b0 + WSTEP - 1) / WSTEP);
                 /* two steps in flight: s + 4 and s + 8 (the first from the previous chunk's
                  * prefetch when it was for this base) */
-                uint4 pf0 = xf, pe0 = xe, pf1 = make_uint4(0, 0, 0, 0), pe1 = pf1;
+                uint4 pf0 = xf, pe0 = xe;
+#if ST_PF2
+                uint4 pf1 = make_uint4(0, 0, 0, 0), pe1 = pf1;
+#endif
                 {
                     const uint64_t a0 = b0 + (uint64_t)wid * WSTEP + lane_off;
                     if (b0 != xb0) {
                         pf0 = ld16c(c.bytes, last_blk, a0);
                         if (edge_lane) pe0 = ld16c(c.bytes, last_blk, a0 + eoff);
                     }
+#if ST_PF2
                     pf1 = ld16c(c.bytes, last_blk, a0 + 1ull * NWAVE * WSTEP);
                     if (edge_lane) pe1 = ld16c(c.bytes, last_blk, a0 + 1ull * NWAVE * WSTEP + eoff);
+#endif
                 }
                 xb0 = ~0ull;
                 uint32_t wr = 0;             /* wave-uniform: document containing the step start */
@@ -434,18 +491,29 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                     const uint64_t sb = b0 + (uint64_t)s * WSTEP;
                     const uint64_t gpos = sb + lane_off;
                     const uint4 cur = pf0, edge = pe0;
+#if ST_PF2
                     pf0 = pf1;
                     pe0 = pe1;
                     {
                         const uint64_t a1 = gpos + 2ull * NWAVE * WSTEP; /* harmless past ge */
-#if K1S_ABL & 16
-                        pf1 = make_uint4(0x20616161u ^ (uint32_t)a1, 0x61612061u, 0x61206161u, 0x20616161u);
-                        pe1 = pf1;
-#else
                         pf1 = ld16c(c.bytes, last_blk, a1);
                         if (edge_lane) pe1 = ld16c(c.bytes, last_blk, a1 + eoff);
+                    }
+#else
+                    {
+                        const uint64_t a1 = gpos + 1ull * NWAVE * WSTEP; /* harmless past ge */
+#if K1S_ABL & 16
+                        /* timing only: text-like bytes without memory traffic */
+                        const uint32_t hsh = (uint32_t)(a1 >> 4) * 0x9E3779B1u;
+                        pf0 = make_uint4(0x20616263u ^ (hsh & 0x0F0F0F00u), 0x63202061u ^ (hsh & 0x000F0F00u),
+                                         0x61626320u ^ (hsh & 0x00000F0Fu), 0x20206162u ^ (hsh & 0x0F000000u));
+                        pe0 = pf0;
+#else
+                        pf0 = ld16c(c.bytes, last_blk, a1);
+                        if (edge_lane) pe0 = ld16c(c.bytes, last_blk, a1 + eoff);
 #endif
                     }
+#endif
                     /* the step's bytes (and the 16 after it) into the wave's stage; this
                      * wave's reads of the previous step were issued before (LDS in order) */
                     reinterpret_cast<uint4*>(stage)[lane] = cur;
@@ -574,17 +642,17 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                     }
                 }
             }
-            if (pending) { finish(pend); pending = false; }
+            drain();
             /* the last group of the chunk: this wave's first step of the next chunk is loaded
              * now, so its latency passes during the flush */
-            if (gd0 + GCAP > dlast && nxt < c1) {
+            if (ST_XPF && gd0 + gcap > dlast && nxt < c1) {
                 xb0 = ns & ~(uint64_t)15;
                 const uint64_t a0 = xb0 + (uint64_t)wid * WSTEP + lane_off;
                 xf = ld16c(c.bytes, last_blk, a0);
                 if (edge_lane) xe = ld16c(c.bytes, last_blk, a0 + eoff);
             }
             /* group end is a document boundary (or the chunk end): emit everything */
-            st_flush(S, o, gd0, ng, cs, ce);
+            st_flush(S, o, gd0, ng, cs, ce, sb);
             if ((uint32_t)tid < ng) {
                 const uint32_t n = S.dsz[tid];
                 if (n) {
@@ -594,7 +662,7 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                 }
             }
             lds_barrier();
-            if (gd0 + GCAP < gd0) break; /* overflow guard */
+            if (gd0 + gcap < gd0) break; /* overflow guard */
         }
         if (tid == 0) { S.cur_chunk = nxt; S.nxt_chunk = claim; }
         lds_barrier();
@@ -616,6 +684,9 @@ int launch_tokcount_st(const CorpusDev& c, const uint64_t* chunk_start, const ui
     }
     const uint64_t wgs = (uint64_t)ncu * 4;
     const uint64_t grid = (c1 - c0) < wgs ? (c1 - c0) : wgs;
-    k_tokcount_st<<<(unsigned)grid, NT, 0, s>>>(c, chunk_start, chunk_doc, c0, c1, v, o);
+    /* key32 = 1 << 31 | doc-in-group << sb | slot: the group size follows the slot bits */
+    const uint32_t sb = (uint32_t)__builtin_popcountll(v.mask);
+    const uint32_t gcap = (31u - sb) >= 8u ? (uint32_t)GCAP : (1u << (31u - sb));
+    k_tokcount_st<<<(unsigned)grid, NT, 0, s>>>(c, chunk_start, chunk_doc, c0, c1, v, o, sb, gcap);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

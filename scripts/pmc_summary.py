@@ -14,7 +14,7 @@ from collections import defaultdict
 def main():
     d, sub = sys.argv[1], (sys.argv[2] if len(sys.argv) > 2 else "")
     vals = defaultdict(list)
-    for f in sorted(glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True)):
+    for f in sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)):
         for r in csv.DictReader(open(f)):
             if sub in r["Kernel_Name"]:
                 vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
