@@ -440,7 +440,7 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     ENSURE(ctx->doc_flags, (size_t)N + 1);
     unsigned long long* cnt = ctx->counters.as<unsigned long long>(); /* rec, part, ntok, status */
     HIPCHK(hipMemsetAsync(ctx->vkeys.p, 0xEE, ctx->vcap * 16, s));
-    HIPCHK(hipMemsetAsync(cnt, 0, 64, s));
+    HIPCHK(hipMemsetAsync(cnt, 0, 256, s));   /* K1 counters, status, the sharded chunk counters */
     HIPCHK(hipMemsetAsync(ctx->doc_npairs.p, 0, (size_t)N * 4 + 4, s));
     HIPCHK(hipMemsetAsync(ctx->doc_size.p, 0, (size_t)N * 4 + 4, s));
     HIPCHK(hipMemsetAsync(ctx->doc_flags.p, 0, (size_t)N + 1, s));
@@ -472,6 +472,7 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     o.doc_flags = ctx->doc_flags.as<uint8_t>();
     o.ntokens = cnt + 2;
     o.chunk_ctr = cnt + 5;
+    o.chunk_shard = cnt + 16;
     o.status = (uint32_t*)(cnt + 3);
     o.stamps = nullptr;
     o.ablate = ctx->ablate;

@@ -43,20 +43,36 @@
 #ifndef K1S_ABL
 #define K1S_ABL 0
 #endif
-/* corpus prefetch: ST_PF2 keeps two steps in flight per wave (else one), ST_XPF loads the
- * next chunk's first step before this chunk's flush */
-#ifndef ST_PF2
-#define ST_PF2 0
-#endif
-#ifndef ST_XPF
-#define ST_XPF 0
+
+/* Diagnostic build only (-DK1_STAMPS, make variant NAME=stamps DEFS=-DK1_STAMPS, run with
+ * TFIDF_STAMPS=1): lane 0 of every wave sums s_memtime cycles per phase — 0 chunk set-up
+ * (claim, metadata, group set-up up to its barrier), 1 walk and rounds, 2 drain + flush,
+ * 3 document sizes + chunk end — plus the chunk count; never in the measured library. */
+#ifdef K1_STAMPS
+#define STP(k)                                                              \
+    do {                                                                    \
+        if (lane == 0) {                                                    \
+            __builtin_amdgcn_sched_barrier(0);                              \
+            const uint64_t t_ = __builtin_amdgcn_s_memtime();               \
+            __builtin_amdgcn_s_waitcnt(0xC07F);                             \
+            if (st_prev) st_acc[st_ph] += t_ - st_prev;                     \
+            st_prev = t_;                                                   \
+            st_ph = (k);                                                    \
+            __builtin_amdgcn_sched_barrier(0);                              \
+        }                                                                   \
+    } while (0)
+#else
+#define STP(k) do { } while (0)
 #endif
 
 namespace {
 
 constexpr int NT = 256;                   /* threads per workgroup */
 constexpr int NWAVE = NT / 64;
-constexpr int WSTEP = 1024;               /* bytes per wave step: one 16-byte group per lane */
+constexpr int WSTEP = 992;                /* bytes a wave step owns: lanes 1..62, one 16-byte group each;
+                                             lane 0 holds the 16 bytes before (the byte before
+                                             the step), lane 63 the 16 after (terms crossing the
+                                             step end): no separate edge loads or edge lanes */
 constexpr int TB = 3584;                  /* LDS table entries (u64): 14 per thread */
 constexpr int EPT = TB / NT;
 constexpr uint32_t FILL_LIMIT = TB - NT * 2 - 64; /* claims after which overflow mode starts */
@@ -72,7 +88,7 @@ struct StShared {
     uint32_t dsz[GCAP];                   /* docSize accumulators */
     union {
         struct {                          /* walk */
-            uint4 stage[NWAVE][WSTEP / 16 + 1];
+            uint4 stage[NWAVE][64];       /* the step's 64 groups: [sb - 16, sb + 1008) */
             uint32_t tl[NWAVE][TLW];
         } w;
         struct {                          /* flush */
@@ -142,6 +158,25 @@ __device__ __forceinline__ uint32_t bkt_empty(uint4 kk, uint32_t key) {
 }
 __device__ __forceinline__ void tbl_read(StShared& S, uint32_t i, uint32_t& key, uint32_t& cnt) { key = S.TK[i]; cnt = S.TC[i]; }
 __device__ __forceinline__ void tbl_clear(StShared& S, uint32_t i) { S.TK[i] = 0u; S.TC[i] = 0u; }
+
+/* The next chunk for a workgroup whose current counter shard is `sh`.  One device-scope
+ * counter saturates at ~88 claims per microsecond (MI355X_MICROARCH.md, price list
+ * "dequeue"): c2's 57 442 chunks alone would take 0.65 ms through it.  The chunks are cut
+ * into 8 contiguous shards with a counter each; a workgroup claims from its home shard
+ * (blockIdx.x & 7) and moves on to the next shard once that one is exhausted, so every
+ * chunk is claimed exactly once and a finished shard costs each workgroup one extra
+ * atomic.  Returns c0 + n when nothing is left. */
+__device__ __forceinline__ uint64_t claim_chunk(unsigned long long* ctr, uint32_t& sh, uint64_t c0, uint64_t n) {
+    for (int t = 0; t < 8; ++t) {
+        const uint64_t lo = n * sh / 8, hi = n * (sh + 1) / 8;
+        if (hi > lo) {
+            const uint64_t v = atomicAdd(&ctr[sh], 1ull);
+            if (lo + v < hi) return c0 + lo + v;
+        }
+        sh = (sh + 1) & 7u;
+    }
+    return c0 + n;
+}
 
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
@@ -340,8 +375,6 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
     __shared__ __attribute__((aligned(16))) StShared S;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint64_t last_blk = c.nbytes ? ((c.nbytes - 1) & ~(uint64_t)15) : 0;
-    const bool edge_lane = lane == 0 || lane == 63;
-    const uint64_t eoff = lane == 0 ? (uint64_t)0 - 16ull : 16ull;
 
     for (int j = 0; j < EPT; ++j) tbl_clear(S, j * NT + tid);
     if (tid < 64) {
@@ -349,6 +382,10 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
         (&S.sel[n].x)[k] = perm_sel(n, k);
     }
     unsigned long long tokens_wg = 0;
+#ifdef K1_STAMPS
+    uint64_t st_acc[5] = {0, 0, 0, 0, 0}, st_prev = 0;
+    uint32_t st_ph = 0;
+#endif
 
     /* one token round of the wave (one token per lane) */
     struct Round {
@@ -433,110 +470,127 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
         if (pending) { finish(pend); pending = false; }
     };
 
-    /* chunks come from a global counter, claimed two ahead: the next chunk is known to every
-     * wave while this one runs, so its first step is loaded before this chunk's flush (the
-     * claim's own round trip is waited for only at the chunk end) */
+    /* Chunks come from sharded counters (claim_chunk), claimed two ahead, so the next chunk is known to
+     * every wave while this one runs.  What a chunk needs before its first token — its
+     * bounds, its documents' offsets and the first step of corpus bytes — is fetched during
+     * the previous chunk: the bounds at its start (scalar loads), the offsets before its
+     * flush (one u64 per thread), and each wave's last step prefetch of the chunk is aimed at
+     * the next chunk's first step instead of past the end.  A chunk then starts without a
+     * dependent HBM round trip. */
+    uint32_t shard = blockIdx.x & 7u;   /* thread 0's current counter shard */
     if (tid == 0) {
-        S.cur_chunk = c0 + atomicAdd(o.chunk_ctr, 1ull);
-        S.nxt_chunk = c0 + atomicAdd(o.chunk_ctr, 1ull);
+        S.cur_chunk = claim_chunk(o.chunk_shard, shard, c0, c1 - c0);
+        S.nxt_chunk = claim_chunk(o.chunk_shard, shard, c0, c1 - c0);
     }
     lds_barrier();
     uint64_t claim = 0;
     uint8_t* const stage = reinterpret_cast<uint8_t*>(&S.w.stage[wid][0]);
     uint32_t* const tl = S.w.tl[wid];
     const uint64_t lane_off = 16ull * lane;
-    uint4 xf = make_uint4(0, 0, 0, 0), xe = xf;   /* the next chunk's first step (this wave's) */
-    uint64_t xb0 = ~0ull;                         /* ... loaded for this step base */
-    for (;;) {
-        const uint64_t chunk = uni64(S.cur_chunk), nxt = uni64(S.nxt_chunk);
-        if (chunk >= c1) break;
-        if (tid == 0) claim = c0 + atomicAdd(o.chunk_ctr, 1ull);
-        const uint64_t cs = chunk_start[chunk], ce = chunk_start[chunk + 1];
-        const uint32_t dfirst = chunk_doc[chunk], dlast = chunk_doc[chunk + 1];
-        const uint64_t ns = nxt < c1 ? chunk_start[nxt] : 0;
+    uint4 pf0 = make_uint4(0, 0, 0, 0);             /* the wave's next step of corpus bytes */
+    uint64_t pfb = ~0ull;                           /* step base pf0 holds step `wid` of, if any */
+    uint64_t dpre = 0;                              /* doc_off[dfirst + tid] of this chunk ... */
+    bool dpre_ok = false;                           /* ... when fetched during the previous one */
+    unsigned long long pend_v = 0;                  /* thread 0: the claim issued at chunk start */
+    uint64_t chunk = uni64(S.cur_chunk), nxt = uni64(S.nxt_chunk);
+    uint64_t cs = 0, ce = 0;
+    uint32_t dfirst = 0, dlast = 0;
+    if (chunk < c1) {
+        cs = chunk_start[chunk];
+        ce = chunk_start[chunk + 1];
+        dfirst = chunk_doc[chunk];
+        dlast = chunk_doc[chunk + 1];
+    }
+    const uint64_t nchunk = c1 - c0;
+    while (chunk < c1) {
+        STP(0);
+#ifdef K1_STAMPS
+        if (lane == 0) st_acc[4] += 1;
+#endif
+        /* the claim is issued now and its value used at the chunk end (no wait here) */
+        if (tid == 0) pend_v = atomicAdd(&o.chunk_shard[shard], 1ull);
+        uint64_t ncs = 0, nce = 0;
+        uint32_t ndf = 0, ndl = 0;
+        if (nxt < c1) {
+            ncs = chunk_start[nxt];
+            nce = chunk_start[nxt + 1];
+            ndf = chunk_doc[nxt];
+            ndl = chunk_doc[nxt + 1];
+        }
         if (cs < ce)
         for (uint32_t gd0 = dfirst; gd0 <= dlast; gd0 += gcap) {
             gd0_cur = gd0;
             const uint32_t ng = (dlast + 1 - gd0) < gcap ? (dlast + 1 - gd0) : gcap;
-            for (uint32_t k = tid; k <= ng; k += NT) S.gdoc[k] = c.doc_off[gd0 + k];
+            if (gd0 == dfirst && dpre_ok) {
+                if ((uint32_t)tid <= ng) S.gdoc[tid] = dpre;
+                if (tid == 0 && ng >= (uint32_t)NT) S.gdoc[NT] = c.doc_off[gd0 + NT];
+            } else {
+                for (uint32_t k = tid; k <= ng; k += NT) S.gdoc[k] = c.doc_off[gd0 + k];
+            }
+            dpre_ok = false;
             if (tid < GCAP) { S.dsz[tid] = 0; S.dpart[tid] = 0; }
             if (tid == 0) S.fill = 0;
             lds_barrier();
+            STP(1);
+            const bool last_group = gd0 + gcap > dlast;
+            const bool ahead = last_group && nxt < c1 && ncs < nce;   /* prefetch for the next chunk */
+            const uint64_t nb0 = ncs & ~(uint64_t)15;
             const uint64_t g0 = uni64(S.gdoc[0]), gn = uni64(S.gdoc[ng]);
             const uint64_t gs = g0 > cs ? g0 : cs;
             const uint64_t ge = gn < ce ? gn : ce;
             if (gs < ge) {
                 const uint64_t b0 = gs & ~(uint64_t)15;
                 const uint32_t nsteps = (uint32_t)((ge - b0 + WSTEP - 1) / WSTEP);
-                /* two steps in flight: s + 4 and s + 8 (the first from the previous chunk's
-                 * prefetch when it was for this base) */
-                uint4 pf0 = xf, pe0 = xe;
-#if ST_PF2
-                uint4 pf1 = make_uint4(0, 0, 0, 0), pe1 = pf1;
-#endif
-                {
-                    const uint64_t a0 = b0 + (uint64_t)wid * WSTEP + lane_off;
-                    if (b0 != xb0) {
-                        pf0 = ld16c(c.bytes, last_blk, a0);
-                        if (edge_lane) pe0 = ld16c(c.bytes, last_blk, a0 + eoff);
-                    }
-#if ST_PF2
-                    pf1 = ld16c(c.bytes, last_blk, a0 + 1ull * NWAVE * WSTEP);
-                    if (edge_lane) pe1 = ld16c(c.bytes, last_blk, a0 + 1ull * NWAVE * WSTEP + eoff);
-#endif
-                }
-                xb0 = ~0ull;
+                if (b0 != pfb) pf0 = ld16c(c.bytes, last_blk, b0 + (uint64_t)wid * WSTEP + lane_off - 16ull);
+                pfb = ~0ull;
                 uint32_t wr = 0;             /* wave-uniform: document containing the step start */
+                uint64_t wcur = g0, wnext = ng > 1 ? uni64(S.gdoc[1]) : gn;   /* gdoc[wr], gdoc[wr + 1] */
                 for (uint32_t s = wid; s < nsteps; s += NWAVE) {
-                    const uint64_t sb = b0 + (uint64_t)s * WSTEP;
-                    const uint64_t gpos = sb + lane_off;
-                    const uint4 cur = pf0, edge = pe0;
-#if ST_PF2
-                    pf0 = pf1;
-                    pe0 = pe1;
+                    const uint64_t sb = b0 + (uint64_t)s * WSTEP;     /* first owned byte */
+                    const uint64_t gpos = sb + lane_off - 16ull;      /* this lane's group */
+                    const uint4 cur = pf0;
                     {
-                        const uint64_t a1 = gpos + 2ull * NWAVE * WSTEP; /* harmless past ge */
-                        pf1 = ld16c(c.bytes, last_blk, a1);
-                        if (edge_lane) pe1 = ld16c(c.bytes, last_blk, a1 + eoff);
-                    }
-#else
-                    {
-                        const uint64_t a1 = gpos + 1ull * NWAVE * WSTEP; /* harmless past ge */
+                        /* the wave's next step, or after its last one the next chunk's first */
+                        const bool redirect = ahead && s + NWAVE >= nsteps;
+                        const uint64_t a1 = redirect ? nb0 + (uint64_t)wid * WSTEP + lane_off - 16ull
+                                                     : gpos + 1ull * NWAVE * WSTEP; /* harmless past ge */
+                        if (redirect) pfb = nb0;
 #if K1S_ABL & 16
                         /* timing only: text-like bytes without memory traffic */
                         const uint32_t hsh = (uint32_t)(a1 >> 4) * 0x9E3779B1u;
                         pf0 = make_uint4(0x20616263u ^ (hsh & 0x0F0F0F00u), 0x63202061u ^ (hsh & 0x000F0F00u),
                                          0x61626320u ^ (hsh & 0x00000F0Fu), 0x20206162u ^ (hsh & 0x0F000000u));
-                        pe0 = pf0;
 #else
                         pf0 = ld16c(c.bytes, last_blk, a1);
-                        if (edge_lane) pe0 = ld16c(c.bytes, last_blk, a1 + eoff);
 #endif
                     }
-#endif
-                    /* the step's bytes (and the 16 after it) into the wave's stage; this
-                     * wave's reads of the previous step were issued before (LDS in order) */
+                    /* the step's 64 groups into the wave's stage; this wave's reads of the
+                     * previous step were issued before (LDS in order) */
                     reinterpret_cast<uint4*>(stage)[lane] = cur;
-                    if (lane == 63) reinterpret_cast<uint4*>(stage)[64] = edge;
-                    /* ---- classify ---- */
+                    /* ---- classify (bytes outside the shard read as whitespace) ---- */
                     const bool inner = sb >= c.lo + 16 && sb + WSTEP + 16 <= c.hi;
                     uint32_t ws = ws_mask16_swar(cur);
                     if (!inner) ws |= bounds_ws(gpos, c.lo, c.hi);
-                    /* document starts in [sb, sb + WSTEP + 16) and the document of each
-                     * lane's first byte: a wave-uniform loop over the group's doc_off */
-                    while (wr + 1 < ng && uni64(S.gdoc[wr + 1]) <= sb) ++wr;
-                    uint32_t ds = 0, nds = 0, base = wr;
-                    for (uint32_t k = wr; k <= ng; ++k) {   /* k = wr: a start AT sb is a start too */
-                        const uint64_t sk = uni64(S.gdoc[k]);
-                        if (sk >= sb + WSTEP + 16) break;
-                        base += (k > wr && sk < gpos) ? 1u : 0u;
-                        if (sk >= gpos && sk < gpos + 16) ds |= 1u << (uint32_t)(sk - gpos);
-                        if (sk >= gpos + 16 && sk < gpos + 32) nds |= 1u << (uint32_t)(sk - gpos - 16);
+                    /* document starts in the window [sb - 16, sb + WSTEP + 16) and the
+                     * document of each lane's first byte.  Most steps hold no document start
+                     * (wnext past the window): no loop then */
+                    while (wr + 1 < ng && wnext <= sb) {
+                        ++wr;
+                        wcur = wnext;
+                        wnext = uni64(S.gdoc[wr + 1]);
                     }
-                    uint32_t prev = (lane_prev(ws) >> 15) & 1u;
-                    if (lane == 0) prev = (gpos > c.lo && gpos - 1 < c.hi) ? (is_ws(edge.w >> 24) ? 1u : 0u) : 1u;
-                    uint32_t own = 0xFFFFu;
-                    if (!(sb >= gs && sb + WSTEP <= ge)) {
+                    uint32_t ds = 0, base = wr;
+                    if (wnext < sb + WSTEP + 16 || wcur + 16 >= sb) {
+                        for (uint32_t k = wr; k <= ng; ++k) {   /* k = wr: a start AT sb is a start too */
+                            const uint64_t sk = uni64(S.gdoc[k]);
+                            if (sk >= sb + WSTEP + 16) break;
+                            base += (k > wr && sk < gpos) ? 1u : 0u;
+                            if (sk >= gpos && sk < gpos + 16) ds |= 1u << (uint32_t)(sk - gpos);
+                        }
+                    }
+                    const uint32_t prev = (lane_prev(ws) >> 15) & 1u;
+                    uint32_t own = (lane >= 1 && lane <= 62) ? 0xFFFFu : 0u;
+                    if (!(sb >= gs && sb + WSTEP <= ge) && own) {
                         own = 0;
                         if (gpos + 16 > gs && gpos < ge) {
                             const uint32_t a = gpos < gs ? (uint32_t)(gs - gpos) : 0u;
@@ -547,30 +601,15 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                     const uint32_t starts = ~ws & ((ws << 1) | prev | ds) & own & 0xFFFFu;
                     /* NUL bytes end a term (strcmp), not a token: rare, exact masks only
                      * when the wave holds one */
-                    uint32_t nul = 0, nnul = 0;
-                    {
-                        const uint32_t z = zero_bits(cur.x) | zero_bits(cur.y) | zero_bits(cur.z) | zero_bits(cur.w) |
-                                           (lane == 63 ? (zero_bits(edge.x) | zero_bits(edge.y) | zero_bits(edge.z) |
-                                                          zero_bits(edge.w)) : 0u);
-                        if (__ballot(z != 0u) != 0ull) {
-                            nul = compress4(zero_bits(cur.x)) | (compress4(zero_bits(cur.y)) << 4) |
-                                  (compress4(zero_bits(cur.z)) << 8) | (compress4(zero_bits(cur.w)) << 12);
-                            nnul = lane_next(nul);
-                            if (lane == 63)
-                                nnul = compress4(zero_bits(edge.x)) | (compress4(zero_bits(edge.y)) << 4) |
-                                       (compress4(zero_bits(edge.z)) << 8) | (compress4(zero_bits(edge.w)) << 12);
-                        }
-                    }
+                    uint32_t nul = 0;
+                    if (__ballot((zero_bits(cur.x) | zero_bits(cur.y) | zero_bits(cur.z) | zero_bits(cur.w)) != 0u) != 0ull)
+                        nul = compress4(zero_bits(cur.x)) | (compress4(zero_bits(cur.y)) << 4) |
+                              (compress4(zero_bits(cur.z)) << 8) | (compress4(zero_bits(cur.w)) << 12);
                     const uint32_t stop = ws | ds;
-                    uint32_t nstop = lane_next(stop);
-                    if (lane == 63) {
-                        uint32_t nws = ws_mask16_swar(edge);
-                        if (!inner) nws |= bounds_ws(gpos + 16, c.lo, c.hi);
-                        nstop = nws | nds;
-                    }
                     /* term end = the first stop after the start byte or the first NUL from
-                     * the start byte on (a NUL start gives the empty term) */
-                    const uint32_t stop32 = stop | (nstop << 16), nul32 = nul | (nnul << 16);
+                     * the start byte on (a NUL start gives the empty term); the next lane's
+                     * masks extend the window to 32 bytes */
+                    const uint32_t stop32 = stop | (lane_next(stop) << 16), nul32 = nul | (lane_next(nul) << 16);
                     /* ---- token entries (wave prefix sum over the lanes' start counts) ---- */
                     const uint32_t nmine = (uint32_t)__popc(starts);
                     const uint32_t incl = wave_incl_scan(nmine);
@@ -594,7 +633,7 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                                     if (ds & ((2u << i) - 1u))
                                         while (rel + 1 < ng && S.gdoc[rel + 1] <= gpos + i) ++rel;
                                     tl[idx - tb] = ((uint32_t)lane << 4 | i) | ((len < 16u ? len : LEN_LONG) << 10) |
-                                                   (rel << 16);
+                                                   (rel << 16);   /* offset in the stage */
                                 }
                                 ++idx;
                             }
@@ -612,7 +651,7 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                             const uint32_t e = val ? tl[t] : 0u;
                             const uint32_t pos = e & 1023u, len = (e >> 10) & 31u;
                             q.rel = e >> 16;
-                            q.ap = sb + pos;
+                            q.ap = sb - 16ull + pos;
                             q.kind = val ? (len == LEN_LONG ? 2u : 1u) : 0u;
                             const u32x4u raw = *reinterpret_cast<const u32x4u*>(stage + pos);
                             const uint4 sl = S.sel[len & 15u];
@@ -643,16 +682,15 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                 }
             }
             drain();
-            /* the last group of the chunk: this wave's first step of the next chunk is loaded
-             * now, so its latency passes during the flush */
-            if (ST_XPF && gd0 + gcap > dlast && nxt < c1) {
-                xb0 = ns & ~(uint64_t)15;
-                const uint64_t a0 = xb0 + (uint64_t)wid * WSTEP + lane_off;
-                xf = ld16c(c.bytes, last_blk, a0);
-                if (edge_lane) xe = ld16c(c.bytes, last_blk, a0 + eoff);
+            STP(2);
+            if (ahead) {   /* the next chunk's document offsets, in flight during this flush */
+                const uint32_t nng = (ndl + 1 - ndf) < gcap ? (ndl + 1 - ndf) : gcap;
+                dpre = (uint32_t)tid <= nng ? c.doc_off[ndf + tid] : 0ull;
+                dpre_ok = true;
             }
             /* group end is a document boundary (or the chunk end): emit everything */
             st_flush(S, o, gd0, ng, cs, ce, sb);
+            STP(3);
             if ((uint32_t)tid < ng) {
                 const uint32_t n = S.dsz[tid];
                 if (n) {
@@ -664,10 +702,27 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
             lds_barrier();
             if (gd0 + gcap < gd0) break; /* overflow guard */
         }
-        if (tid == 0) { S.cur_chunk = nxt; S.nxt_chunk = claim; }
+        if (tid == 0) {
+            const uint64_t lo = nchunk * shard / 8, hi = nchunk * (shard + 1) / 8;
+            claim = lo + pend_v < hi ? c0 + lo + pend_v : claim_chunk(o.chunk_shard, shard, c0, nchunk);
+            S.cur_chunk = nxt;
+            S.nxt_chunk = claim;
+        }
         lds_barrier();
+        chunk = nxt;
+        nxt = uni64(S.nxt_chunk);
+        cs = ncs;
+        ce = nce;
+        dfirst = ndf;
+        dlast = ndl;
     }
     if (lane == 0 && tokens_wg) atomicAdd(o.ntokens, tokens_wg);
+#ifdef K1_STAMPS
+    STP(0);
+    if (lane == 0 && o.stamps)
+        for (int k = 0; k < 5; ++k) atomicAdd(&o.stamps[k], (unsigned long long)st_acc[k]);
+    if (lane == 0 && o.stamps) atomicAdd(&o.stamps[5], 1ull);
+#endif
 }
 
 int launch_tokcount_st(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc, uint64_t c0,

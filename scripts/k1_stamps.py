@@ -1,0 +1,30 @@
+"""K1 phase cycles (diagnostic build lib/libtfidf_hip_stamps.so, tokcount_st.hip K1_STAMPS):
+per-wave average s_memtime cycles in chunk set-up / walk+rounds / flush / chunk end, over
+one c2 run.  Usage (GPU box): TFIDF_LIB=stamps TFIDF_STAMPS=1 python scripts/k1_stamps.py"""
+import ctypes as C
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "parallel-systems-mpi-tfidf_amd", "python"))
+import tfidf_abi  # noqa: E402
+import tfidf_configs  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
+p = tfidf_configs.plan(cfg)
+L = tfidf_abi.lib()
+L.tfidf_debug_k1_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+with tfidf_abi.Engine(0) as e:
+    c = e.synth_device(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"], p["ndocs_total"])
+    for _ in range(3):
+        e.run_corpus(c)
+    info = e.info()
+    buf = (C.c_uint64 * 22)()
+    n = L.tfidf_debug_k1_stamps(e.h, buf, 22)
+    v = list(buf)[:n]
+waves = v[5] or 1
+names = ["setup", "walk+rounds", "drain+flush", "chunk end"]
+tot = sum(v[:4])
+print(cfg, "K1 ms", round(info["ms_tokcount"], 4), "waves", waves, "chunk visits/wave", round(v[4] / waves, 1))
+for k, nm in enumerate(names):
+    print("  %-12s %10.0f cycles/wave  %5.1f %%" % (nm, v[k] / waves, 100.0 * v[k] / max(tot, 1)))
