@@ -67,13 +67,20 @@
 
 namespace {
 
-constexpr int NT = 256;                   /* threads per workgroup */
+#ifndef K1S_NT
+#define K1S_NT 256
+#endif
+#ifndef K1S_TB
+#define K1S_TB 3584
+#endif
+constexpr int NT = K1S_NT;                /* threads per workgroup */
+constexpr int WG_PER_CU = 1024 / NT;      /* 16 waves per CU */
 constexpr int NWAVE = NT / 64;
 constexpr int WSTEP = 992;                /* bytes a wave step owns: lanes 1..62, one 16-byte group each;
                                              lane 0 holds the 16 bytes before (the byte before
                                              the step), lane 63 the 16 after (terms crossing the
                                              step end): no separate edge loads or edge lanes */
-constexpr int TB = 3584;                  /* LDS table entries (u64): 14 per thread */
+constexpr int TB = K1S_TB;                /* LDS table entries (u32 key + u32 count): 14 per thread */
 constexpr int EPT = TB / NT;
 constexpr uint32_t FILL_LIMIT = TB - NT * 2 - 64; /* claims after which overflow mode starts */
 constexpr int GCAP = 256;                 /* documents per group at most (LDS arrays) */
@@ -99,6 +106,7 @@ struct StShared {
         } f;
     };
     uint4 sel[16];                        /* v_perm selectors of a term of length n */
+    uint64_t fbase[8];                    /* st_flush_few: first record of each document */
     uint8_t dpart[GCAP];                  /* document has overflow records */
     uint32_t fill;                        /* table claims of the group */
     uint64_t cur_chunk, nxt_chunk;        /* dynamic chunk schedule: this chunk and the next */
@@ -349,6 +357,122 @@ __device__ void st_flush(StShared& S, const K1Out& o, uint32_t gd0, uint32_t ng,
             } else {
                 const uint64_t q = pb + (dof >> 16) + k;
                 if (part_ok) { o.part_doc[q] = gd0 + rel; o.part_slot[q] = key & smask; o.part_cnt[q] = ec[j]; }
+            }
+            tbl_clear(S, j * NT + tid);
+        }
+    }
+}
+
+/* The flush of a group of at most FEW documents (most c2 chunks hold one or two): every
+ * thread counts its entries per document in 16-bit fields of FEW/2 words, one block scan
+ * of those words gives each thread its first rank in every document and the documents'
+ * totals, one thread allocates the records, and every entry is written at document base
+ * + rank with no LDS atomic.  Same output as st_flush. */
+constexpr uint32_t FEW = 8;
+__device__ void st_flush_few(StShared& S, const K1Out& o, uint32_t gd0, uint32_t ng, uint64_t cs, uint64_t ce,
+                             uint32_t sb) {
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, w = tid >> 6;
+    lds_barrier();                  /* every wave's walk is done */
+    const uint32_t smask = (1u << sb) - 1u;
+    uint32_t ek[EPT], ec[EPT];
+    uint32_t pk[FEW / 2] = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+        tbl_read(S, j * NT + tid, ek[j], ec[j]);
+        if (ek[j]) {
+            const uint32_t rel = (ek[j] & 0x7FFFFFFFu) >> sb;
+#pragma unroll
+            for (uint32_t q = 0; q < FEW / 2; ++q)
+                pk[q] += (rel >> 1) == q ? (1u << (16 * (rel & 1u))) : 0u;
+        }
+    }
+    /* block exclusive scan of the FEW/2 packed words (fields never carry: totals <= TB) */
+    uint32_t inc[FEW / 2];
+#pragma unroll
+    for (uint32_t q = 0; q < FEW / 2; ++q) {
+        inc[q] = wave_incl_scan(pk[q]);
+        if (lane == 63) S.f.dcnt[w * (FEW / 2) + q] = inc[q];
+    }
+    lds_barrier();
+    uint32_t rank[FEW / 2], tot[FEW / 2];
+#pragma unroll
+    for (uint32_t q = 0; q < FEW / 2; ++q) {
+        uint32_t base = 0, t = 0;
+#pragma unroll
+        for (int k = 0; k < NWAVE; ++k) {
+            const uint32_t x = S.f.dcnt[k * (FEW / 2) + q];
+            base += k < w ? x : 0u;
+            t += x;
+        }
+        rank[q] = base + inc[q] - pk[q];
+        tot[q] = t;
+    }
+    /* per document (lane d of wave 0): complete (record stream) or partial; one wave scan
+     * of the documents' counts gives their offsets; lanes 0 and 32 allocate the records */
+    if (w == 0) {
+        const uint32_t d = (uint32_t)lane;
+        uint32_t cnt = 0, packed = 0;
+        uint8_t st = 0;
+        bool part = false;
+        if (d < ng) {
+#pragma unroll
+            for (uint32_t q = 0; q < FEW / 2; ++q)
+                if ((d >> 1) == q) cnt = (tot[q] >> (16 * (d & 1u))) & 0xFFFFu;
+            part = S.dpart[d] != 0;
+            if (cnt) {
+                const bool complete = !part && S.gdoc[d] >= cs && S.gdoc[d + 1] <= ce && cnt <= (uint32_t)K5_MAX_PAIRS;
+                st = complete ? 2 : 1;
+                packed = complete ? cnt : (cnt << 16);
+            }
+            if (st == 1 || part) o.doc_flags[gd0 + d] = DF_PARTIAL;
+        }
+        const uint32_t incl = wave_incl_scan(packed);
+        const uint32_t all = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        const uint32_t off = incl - packed;
+        const uint32_t nrec = all & 0xFFFFu, npart = all >> 16;
+        unsigned long long a0 = 0, a1 = 0;
+        if (lane == 0 && nrec) a0 = atomicAdd(o.rec_alloc, (unsigned long long)nrec);
+        if (lane == 32 && npart) a1 = atomicAdd(o.part_alloc, (unsigned long long)npart);
+        const unsigned long long rb = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(a0 >> 32), 0) << 32) |
+                                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a0, 0);
+        const unsigned long long pb = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(a1 >> 32), 32) << 32) |
+                                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a1, 32);
+        const bool rec_ok = rb + nrec <= o.rec_cap, part_ok = pb + npart <= o.part_cap;
+        if (lane == 0 && !rec_ok) atomicOr(o.status, ST_REC_FULL);
+        if (lane == 0 && !part_ok) atomicOr(o.status, ST_PART_FULL);
+        if (d < ng) {
+            uint64_t fb = ~0ull;   /* first record of document d, ~0 when its stream overflowed */
+            if (st == 2) {
+                fb = rec_ok ? rb + (off & 0xFFFFu) : ~0ull;
+                o.doc_recoff[gd0 + d] = rb + (off & 0xFFFFu);
+                o.doc_npairs[gd0 + d] = cnt;
+            } else if (st == 1) {
+                fb = part_ok ? pb + (off >> 16) : ~0ull;
+            }
+            S.fbase[d] = fb;
+            S.f.dstate[d] = st;
+        }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+        const uint32_t key = ek[j];
+        if (key) {
+            const uint32_t rel = (key & 0x7FFFFFFFu) >> sb;
+            uint32_t r = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < FEW / 2; ++q)
+                if ((rel >> 1) == q) {
+                    r = (rank[q] >> (16 * (rel & 1u))) & 0xFFFFu;
+                    rank[q] += 1u << (16 * (rel & 1u));
+                }
+            const uint64_t fb = S.fbase[rel];
+            if (fb != ~0ull) {
+                const uint64_t qq = fb + r;
+                if (S.f.dstate[rel] == 2) { o.rec_slot[qq] = key & smask; o.rec_cnt[qq] = ec[j]; }
+                else { o.part_doc[qq] = gd0 + rel; o.part_slot[qq] = key & smask; o.part_cnt[qq] = ec[j]; }
             }
             tbl_clear(S, j * NT + tid);
         }
@@ -689,7 +813,8 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                 dpre_ok = true;
             }
             /* group end is a document boundary (or the chunk end): emit everything */
-            st_flush(S, o, gd0, ng, cs, ce, sb);
+            if (ng <= FEW) st_flush_few(S, o, gd0, ng, cs, ce, sb);
+            else st_flush(S, o, gd0, ng, cs, ce, sb);
             STP(3);
             if ((uint32_t)tid < ng) {
                 const uint32_t n = S.dsz[tid];
@@ -729,7 +854,8 @@ int launch_tokcount_st(const CorpusDev& c, const uint64_t* chunk_start, const ui
                        uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s) {
     if (c1 <= c0) return 0;
     if (v.mask >= (1ull << SLOT_BITS)) return -3; /* slot must fit the LDS entry */
-    static_assert(sizeof(StShared) <= 40960, "four workgroups per CU");
+    static_assert(sizeof(StShared) * WG_PER_CU <= 163840, "16 waves per CU");
+    static_assert(TB % NT == 0 && TB % 4 == 0, "table rows");
     static int ncu = 0;
     if (!ncu) {
         int dev = 0;
@@ -737,7 +863,7 @@ int launch_tokcount_st(const CorpusDev& c, const uint64_t* chunk_start, const ui
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
             ncu = 256;
     }
-    const uint64_t wgs = (uint64_t)ncu * 4;
+    const uint64_t wgs = (uint64_t)ncu * WG_PER_CU;
     const uint64_t grid = (c1 - c0) < wgs ? (c1 - c0) : wgs;
     /* key32 = 1 << 31 | doc-in-group << sb | slot: the group size follows the slot bits */
     const uint32_t sb = (uint32_t)__builtin_popcountll(v.mask);
