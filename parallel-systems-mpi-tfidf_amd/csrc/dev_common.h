@@ -26,6 +26,20 @@
 #define KEY_LONG_TAG   0xFF00000000000000ull
 #define DOC_NONE       0xFFFFFFFFu
 
+/* Explicitly global (address space 1) loads and stores.  A pointer that reaches a load
+ * through a struct or a lambda capture can lose its address space, and the compiler then
+ * emits a flat_ instruction: flat loads count in lgkmcnt as well as vmcnt, so every later
+ * LDS wait (lgkmcnt(0)) also waits for the gather in flight. */
+#define GLOBAL_AS __attribute__((address_space(1)))
+template <class T> __device__ __forceinline__ T gload(const T* p) { return *(const GLOBAL_AS T*)p; }
+template <class T> __device__ __forceinline__ void gstore(T* p, T v) { *(GLOBAL_AS T*)p = v; }
+/* uint4 is a class type whose copy goes through a generic pointer: load a native vector */
+typedef unsigned int g_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 gload(const uint4* p) {
+    const g_u32x4 r = *(const GLOBAL_AS g_u32x4*)p;
+    return make_uint4(r.x, r.y, r.z, r.w);
+}
+
 /* C-locale isspace(): the byte set fscanf("%s") stops at (TFIDF.c:142,147) */
 __device__ __forceinline__ bool is_ws(uint32_t c) { return c == 0x20u || (c - 0x09u) <= 4u; }
 

@@ -17,6 +17,12 @@
 #include "kernels.h"
 #include "synth.h"
 
+#include <type_traits>
+/* global (address space 1) view of a pointer: K5Args travels by reference into helpers, so
+ * its pointers reach loads as generic (flat) pointers, whose loads also count in lgkmcnt and
+ * make every LDS wait wait for them too */
+#define G(p) ((GLOBAL_AS std::remove_pointer_t<decltype(p)>*)(p))
+
 namespace {
 constexpr int NT = 256;
 /* at least one workgroup: an empty launch is an error, every kernel bounds-checks its index */
@@ -907,9 +913,9 @@ __global__ void k_idf_of_rank(const uint32_t* __restrict__ df_of_rank, const uin
  * df of a pair are per-document / per-term values the fetch expands on the host. */
 __device__ __forceinline__ void k5_emit(const K5Args& a, uint64_t o, double ds, uint32_t rank, uint32_t cnt) {
     const double tf = (double)cnt / ds;   /* TFIDF.c:202 */
-    a.out_term[o] = rank;
-    a.out_cnt[o] = cnt;
-    a.out_score[o] = tf * a.idf_rank[rank]; /* TFIDF.c:243-244 (idf from the host-libm LUT) */
+    G(a.out_term)[o] = rank;
+    G(a.out_cnt)[o] = cnt;
+    G(a.out_score)[o] = tf * G(a.idf_rank)[rank]; /* TFIDF.c:243-244 (idf from the host-libm LUT) */
 }
 
 /* records hold term ranks once the DF pass has run (k_df_hist_* rewrite them in place) */
@@ -993,16 +999,16 @@ __device__ __noinline__ void k5_radix(const K5Args& a, uint32_t* buf0, uint32_t*
         }
 #pragma unroll
         for (int q = 0; q < K5_BATCH; ++q) {
-            cnt[q] = a.rec_cnt[rb + (key[q] & ((1u << K5_IDX_BITS) - 1u))];
-            idf[q] = a.idf_rank[key[q] >> K5_IDX_BITS];
+            cnt[q] = G(a.rec_cnt)[rb + (key[q] & ((1u << K5_IDX_BITS) - 1u))];
+            idf[q] = G(a.idf_rank)[key[q] >> K5_IDX_BITS];
         }
 #pragma unroll
         for (int q = 0; q < K5_BATCH; ++q) {
             const uint32_t j = j0 + 64 * q + lane;
             if (j < n) {
-                a.out_term[ob + j] = key[q] >> K5_IDX_BITS;
-                a.out_cnt[ob + j] = cnt[q];
-                a.out_score[ob + j] = ((double)cnt[q] / ds) * idf[q]; /* TFIDF.c:202,243-244 */
+                G(a.out_term)[ob + j] = key[q] >> K5_IDX_BITS;
+                G(a.out_cnt)[ob + j] = cnt[q];
+                G(a.out_score)[ob + j] = ((double)cnt[q] / ds) * idf[q]; /* TFIDF.c:202,243-244 */
             }
         }
     }
@@ -1028,8 +1034,8 @@ __device__ __forceinline__ void k5_prefetch(const K5Args& a, const uint4& m, uin
     for (int q = 0; q < K5_PF; ++q) {
         const uint32_t j = 64u * q + lane;
         const bool v = ok && j < n;
-        s[q] = v ? a.rec_slot[rb + j] : 0u;
-        c[q] = v ? a.rec_cnt[rb + j] : 0u;
+        s[q] = v ? G(a.rec_slot)[rb + j] : 0u;
+        c[q] = v ? G(a.rec_cnt)[rb + j] : 0u;
     }
 }
 
@@ -1045,9 +1051,9 @@ __global__ __launch_bounds__(NT, K5_WPS) void k_score_wave(K5Args a) {
     uint32_t* buf1 = kb[w][1];
     uint32_t* h = hist[w];
     uint32_t i = blockIdx.x * (NT / 64) + w;
-    uint4 m_cur = i < a.ndocs ? a.meta[i] : make_uint4(0, 0, 0, 0);
-    uint4 m_nxt = i + stride < a.ndocs ? a.meta[i + stride] : make_uint4(0, 0, 0, 0);
-    uint64_t ob_cur = i < a.ndocs ? a.out_off[i] : 0ull;
+    uint4 m_cur = i < a.ndocs ? gload(a.meta + (i)) : make_uint4(0, 0, 0, 0);
+    uint4 m_nxt = i + stride < a.ndocs ? gload(a.meta + (i + stride)) : make_uint4(0, 0, 0, 0);
+    uint64_t ob_cur = i < a.ndocs ? G(a.out_off)[i] : 0ull;
     uint32_t s_cur[K5_PF], c_cur[K5_PF];
     k5_prefetch(a, m_cur, lane, s_cur, c_cur);
     for (; i < a.ndocs; i += stride) {
@@ -1072,8 +1078,8 @@ __global__ __launch_bounds__(NT, K5_WPS) void k_score_wave(K5Args a) {
 #pragma unroll
             for (int q = K5_PF; q < K5_RQ; ++q) {
                 const uint32_t j = 64u * q + lane;
-                sx[q - K5_PF] = j < n ? a.rec_slot[rb + j] : 0u;
-                if (j < n) buf0[j] = a.rec_cnt[rb + j];
+                sx[q - K5_PF] = j < n ? G(a.rec_slot)[rb + j] : 0u;
+                if (j < n) buf0[j] = G(a.rec_cnt)[rb + j];
             }
 #pragma unroll
             for (int q = K5_PF; q < K5_RQ; ++q) {
@@ -1089,13 +1095,13 @@ __global__ __launch_bounds__(NT, K5_WPS) void k_score_wave(K5Args a) {
         {
             const uint32_t inx = i + stride;
             m_cur = m_nxt;
-            ob_cur = inx < a.ndocs ? a.out_off[inx] : 0ull;
-            m_nxt = inx + stride < a.ndocs ? a.meta[inx + stride] : make_uint4(0, 0, 0, 0);
+            ob_cur = inx < a.ndocs ? G(a.out_off)[inx] : 0ull;
+            m_nxt = inx + stride < a.ndocs ? gload(a.meta + (inx + stride)) : make_uint4(0, 0, 0, 0);
             k5_prefetch(a, m_cur, lane, s_cur, c_cur);
         }
         if (n == 0) continue;
         if (!k5_by_wave(a, n, presorted)) { /* k_score_large's document */
-            if (WIDE && lane == 0) a.large_list[atomicAdd(a.large_count, 1u)] = i; /* else listed up front */
+            if (WIDE && lane == 0) G(a.large_list)[atomicAdd(a.large_count, 1u)] = i; /* else listed up front */
             continue;
         }
         if (rb + n > a.rec_total) { if (lane == 0) atomicOr(a.status, ST_BOUNDS); continue; }
@@ -1138,16 +1144,16 @@ __global__ __launch_bounds__(NT, K5_WPS) void k_score_wave(K5Args a) {
             }
             double idf[QC];
 #pragma unroll
-            for (int q = 0; q < QC; ++q) idf[q] = (64u * q + lane < n) ? a.idf_rank[r[q]] : 0.0;
+            for (int q = 0; q < QC; ++q) idf[q] = (64u * q + lane < n) ? G(a.idf_rank)[r[q]] : 0.0;
 #pragma unroll
             for (int q = 0; q < QC; ++q) {
                 const uint32_t j = 64u * q + lane;
                 if (j < n) {
                     const uint64_t o = ob + pos[q];
                     const uint32_t cnt = buf0[j];
-                    a.out_term[o] = r[q];
-                    a.out_cnt[o] = cnt;
-                    a.out_score[o] = ((double)cnt / ds) * idf[q];   /* TFIDF.c:202,243-244 */
+                    G(a.out_term)[o] = r[q];
+                    G(a.out_cnt)[o] = cnt;
+                    G(a.out_score)[o] = ((double)cnt / ds) * idf[q];   /* TFIDF.c:202,243-244 */
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1196,7 +1202,7 @@ __global__ __launch_bounds__(NT, K5_WPS) void k_score_wave(K5Args a) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const bool wide = WIDE && a.rank_bits + K5_IDX_BITS > 32;
         if (gmax > K5_GROUP_MAX && wide) { /* skewed and too wide for packed keys: k_score_large */
-            if (lane == 0) a.large_list[atomicAdd(a.large_count, 1u)] = i;
+            if (lane == 0) G(a.large_list)[atomicAdd(a.large_count, 1u)] = i;
             continue;
         }
 #ifndef K5_NO_WIDE
@@ -1232,15 +1238,15 @@ __global__ __launch_bounds__(NT, K5_WPS) void k_score_wave(K5Args a) {
                         pos[e] = gs + less;
                         cnt[e] = buf0[j];
                     }
-                    idf[e] = j < n ? a.idf_rank[rk] : 0.0;
+                    idf[e] = j < n ? G(a.idf_rank)[rk] : 0.0;
                 }
 #pragma unroll
                 for (int e = 0; e < EB; ++e) {
                     if (64u * (q0 + e) + lane < n) {
                         const uint64_t o = ob + pos[e];
-                        a.out_term[o] = r[q0 + e];
-                        a.out_cnt[o] = cnt[e];
-                        a.out_score[o] = ((double)cnt[e] / ds) * idf[e];   /* TFIDF.c:202,243-244 */
+                        G(a.out_term)[o] = r[q0 + e];
+                        G(a.out_cnt)[o] = cnt[e];
+                        G(a.out_score)[o] = ((double)cnt[e] / ds) * idf[e];   /* TFIDF.c:202,243-244 */
                     }
                 }
             }
@@ -1303,14 +1309,14 @@ __global__ __launch_bounds__(NT, K5_WPS) void k_score_wave(K5Args a) {
                 cnt[q] = j < n ? buf0[key[q] & ((1u << K5_IDX_BITS) - 1u)] : 0u;
             }
 #pragma unroll
-            for (int q = 0; q < EB; ++q) idf[q] = a.idf_rank[key[q] >> K5_IDX_BITS];
+            for (int q = 0; q < EB; ++q) idf[q] = G(a.idf_rank)[key[q] >> K5_IDX_BITS];
 #pragma unroll
             for (int q = 0; q < EB; ++q) {
                 const uint32_t j = j0 + 64 * q + lane;
                 if (j < n) {
-                    a.out_term[ob + j] = key[q] >> K5_IDX_BITS;
-                    a.out_cnt[ob + j] = cnt[q];
-                    a.out_score[ob + j] = ((double)cnt[q] / ds) * idf[q]; /* TFIDF.c:202,243-244 */
+                    G(a.out_term)[ob + j] = key[q] >> K5_IDX_BITS;
+                    G(a.out_cnt)[ob + j] = cnt[q];
+                    G(a.out_score)[ob + j] = ((double)cnt[q] / ds) * idf[q]; /* TFIDF.c:202,243-244 */
                 }
             }
         }
@@ -1331,24 +1337,24 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t nlarge = *a.large_count;
     for (uint32_t li = blockIdx.x; li < nlarge; li += gridDim.x) {
-    const uint32_t i = a.large_list[li];
-    const uint32_t d = a.order[i];
-    const uint32_t n = a.doc_npairs[d];
-    const bool presorted = (a.doc_flags[d] & DF_PRESORTED) != 0;
-    const uint64_t ob = a.out_off[i], rb = a.doc_recoff[d];
-    const double ds = (double)a.doc_size[d];
+    const uint32_t i = G(a.large_list)[li];
+    const uint32_t d = G(a.order)[i];
+    const uint32_t n = G(a.doc_npairs)[d];
+    const bool presorted = (G(a.doc_flags)[d] & DF_PRESORTED) != 0;
+    const uint64_t ob = G(a.out_off)[i], rb = G(a.doc_recoff)[d];
+    const double ds = (double)G(a.doc_size)[d];
     if (rb + n > a.rec_total) { /* never expected: report instead of reading past the records */
         if (tid == 0) atomicOr(a.status, ST_BOUNDS);
         continue;
     }
     if (presorted || n > (uint32_t)K5_MAX) {
         if (n > (uint32_t)K5_MAX && !presorted) { if (tid == 0) atomicOr(a.status, ST_BOUNDS); continue; }
-        for (uint32_t j = tid; j < n; j += NT) k5_emit(a, ob + j, ds, k5_rank(a, a.rec_slot[rb + j]), a.rec_cnt[rb + j]);
+        for (uint32_t j = tid; j < n; j += NT) k5_emit(a, ob + j, ds, k5_rank(a, G(a.rec_slot)[rb + j]), G(a.rec_cnt)[rb + j]);
         continue;
     }
     for (uint32_t j = tid; j < n; j += NT) {
-        kbuf[0][j] = k5_rank(a, a.rec_slot[rb + j]);
-        vbuf[0][j] = a.rec_cnt[rb + j];
+        kbuf[0][j] = k5_rank(a, G(a.rec_slot)[rb + j]);
+        vbuf[0][j] = G(a.rec_cnt)[rb + j];
     }
     const uint64_t lt = (1ull << lane) - 1ull;
     int cur = 0;
@@ -1404,7 +1410,7 @@ __global__ void k_large_list(K5Args a) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     bool big = false;
     if (i < a.ndocs) {
-        const uint4 m = a.meta[i];
+        const uint4 m = gload(a.meta + (i));
         const uint32_t n = m.z & 0x3FFFFFFFu;
         big = n != 0u && !k5_by_wave(a, n, ((m.z >> 30) & DF_PRESORTED) != 0);
     }
@@ -1414,7 +1420,7 @@ __global__ void k_large_list(K5Args a) {
     uint32_t base = 0;
     if (lane == leader) base = atomicAdd(a.large_count, (uint32_t)__popcll(bm));
     base = (uint32_t)__shfl(base, (int)leader);
-    if (big) a.large_list[base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull))] = i;
+    if (big) G(a.large_list)[base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull))] = i;
 }
 int launch_score_order(const K5Args& a, hipStream_t s, hipStream_t s2, hipEvent_t ev_fork, hipEvent_t ev_join) {
     if (!a.ndocs) return 0;

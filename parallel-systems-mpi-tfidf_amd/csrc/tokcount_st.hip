@@ -39,15 +39,18 @@
 /* timing-only ablation builds (make variant NAME=s1 DEFS=-DK1S_ABL=1; results invalid):
  * 1 no vocabulary loads/compare (slot from the key), 2 no LDS counting, 4 no token rounds,
  * 8 no token entries (walk + flush only), 16 no corpus loads, 32 flush without record
- * writes, 64 flush = table clear only */
+ * writes, 64 flush = table clear only, 128 corpus bytes from the first MiB (no HBM latency) */
 #ifndef K1S_ABL
 #define K1S_ABL 0
 #endif
 
 /* Diagnostic build only (-DK1_STAMPS, make variant NAME=stamps DEFS=-DK1_STAMPS, run with
  * TFIDF_STAMPS=1): lane 0 of every wave sums s_memtime cycles per phase — 0 chunk set-up
- * (claim, metadata, group set-up up to its barrier), 1 walk and rounds, 2 drain + flush,
- * 3 document sizes + chunk end — plus the chunk count; never in the measured library. */
+ * (claim, metadata, group set-up up to its barrier), 1 walk (classify, token entries),
+ * 2 token rounds, 3 drain, 4 wait at the flush barrier (the other waves' walks), 5 flush,
+ * 6 document sizes + chunk end — then the chunk count (word 7) and the wave count (word
+ * 8); never in the measured library. */
+#define K1S_NPH 7
 #ifdef K1_STAMPS
 #define STP(k)                                                              \
     do {                                                                    \
@@ -86,7 +89,10 @@ constexpr uint32_t FILL_LIMIT = TB - NT * 2 - 64; /* claims after which overflow
 constexpr int GCAP = 256;                 /* documents per group at most (LDS arrays) */
 constexpr uint32_t SLOT_BITS = 28;        /* vocabulary slots < 2^28 */
 constexpr int TLW = 192;                  /* token entries per wave and compaction pass */
-constexpr uint32_t LEN_LONG = 31u;        /* token entry: term of >= 16 bytes or past the window */
+constexpr uint32_t LEN_LONG = 31u;
+#ifndef K1S_ENT
+#define K1S_ENT 0                         /* 1: unrolled token entries (A/B: more spills, slower) */
+#endif        /* token entry: term of >= 16 bytes or past the window */
 
 struct StShared {
     uint32_t TK[TB];                      /* key32 = 1 << 31 | doc-in-group << sb | slot (0: empty) */
@@ -507,7 +513,7 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
     }
     unsigned long long tokens_wg = 0;
 #ifdef K1_STAMPS
-    uint64_t st_acc[5] = {0, 0, 0, 0, 0}, st_prev = 0;
+    uint64_t st_acc[K1S_NPH + 1] = {}, st_prev = 0;
     uint32_t st_ph = 0;
 #endif
 
@@ -629,7 +635,7 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
     while (chunk < c1) {
         STP(0);
 #ifdef K1_STAMPS
-        if (lane == 0) st_acc[4] += 1;
+        if (lane == 0) st_acc[K1S_NPH] += 1;
 #endif
         /* the claim is issued now and its value used at the chunk end (no wait here) */
         if (tid == 0) pend_v = atomicAdd(&o.chunk_shard[shard], 1ull);
@@ -679,7 +685,11 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                         const uint64_t a1 = redirect ? nb0 + (uint64_t)wid * WSTEP + lane_off - 16ull
                                                      : gpos + 1ull * NWAVE * WSTEP; /* harmless past ge */
                         if (redirect) pfb = nb0;
-#if K1S_ABL & 16
+#if K1S_ABL & 128
+                        /* timing only: every step's bytes come from the corpus's first MiB
+                         * (L2/MALL-resident): the cost of the HBM latency of the prefetch */
+                        pf0 = ld16c(c.bytes, last_blk, a1 & ((1ull << 20) - 1ull));
+#elif K1S_ABL & 16
                         /* timing only: text-like bytes without memory traffic */
                         const uint32_t hsh = (uint32_t)(a1 >> 4) * 0x9E3779B1u;
                         pf0 = make_uint4(0x20616263u ^ (hsh & 0x0F0F0F00u), 0x63202061u ^ (hsh & 0x000F0F00u),
@@ -703,13 +713,20 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                         wcur = wnext;
                         wnext = uni64(S.gdoc[wr + 1]);
                     }
-                    uint32_t ds = 0, base = wr;
+                    uint32_t ds = 0, dsn = 0, base = wr;   /* dsn: the starts of documents after wr */
+                    bool wemp = false;   /* wave-uniform: two documents start at one byte (an empty one) */
                     if (wnext < sb + WSTEP + 16 || wcur + 16 >= sb) {
+                        uint64_t sprev = ~0ull;
                         for (uint32_t k = wr; k <= ng; ++k) {   /* k = wr: a start AT sb is a start too */
                             const uint64_t sk = uni64(S.gdoc[k]);
                             if (sk >= sb + WSTEP + 16) break;
+                            wemp |= sk == sprev;
+                            sprev = sk;
                             base += (k > wr && sk < gpos) ? 1u : 0u;
-                            if (sk >= gpos && sk < gpos + 16) ds |= 1u << (uint32_t)(sk - gpos);
+                            if (sk >= gpos && sk < gpos + 16) {
+                                ds |= 1u << (uint32_t)(sk - gpos);
+                                dsn |= k > wr ? 1u << (uint32_t)(sk - gpos) : 0u;
+                            }
                         }
                     }
                     const uint32_t prev = (lane_prev(ws) >> 15) & 1u;
@@ -742,6 +759,37 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                     tokens_wg += ntok;
                     if (K1S_ABL & 8) { if (lane == 0) atomicAdd(&S.dsz[base], ntok); continue; }
                     for (uint32_t tb = 0; tb < ntok; tb += TLW) {
+#if K1S_ENT
+                        if (!wemp) {
+                            /* straight-line: a lane's first four tokens unrolled (a 16-byte
+                             * group rarely holds more), the document by counting the group's
+                             * document starts at or before the token (every start is a
+                             * distinct document when none is empty) */
+                            uint32_t sm = starts, idx = incl - nmine - tb;
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                const uint32_t i = (uint32_t)__builtin_ctz(sm | 0x10000u);
+                                sm &= sm - 1u;
+                                const uint32_t e = ((stop32 >> i) & ~1u) | (nul32 >> i);
+                                const uint32_t tz = (uint32_t)__builtin_ctz(e | 0x80000000u);
+                                const uint32_t len = (e && tz < 16u) ? tz : LEN_LONG;
+                                const uint32_t rel = base + (uint32_t)__popc(dsn & ((2u << i) - 1u));
+                                if (i < 16u && idx < (uint32_t)TLW)
+                                    tl[idx] = ((uint32_t)lane << 4 | i) | (len << 10) | (rel << 16);
+                                ++idx;
+                            }
+                            while (sm) {   /* the rare fifth token and beyond */
+                                const uint32_t i = (uint32_t)__builtin_ctz(sm);
+                                sm &= sm - 1u;
+                                const uint32_t e = ((stop32 >> i) & ~1u) | (nul32 >> i);
+                                const uint32_t tz = (uint32_t)__builtin_ctz(e | 0x80000000u);
+                                const uint32_t len = (e && tz < 16u) ? tz : LEN_LONG;
+                                const uint32_t rel = base + (uint32_t)__popc(dsn & ((2u << i) - 1u));
+                                if (idx < (uint32_t)TLW) tl[idx] = ((uint32_t)lane << 4 | i) | (len << 10) | (rel << 16);
+                                ++idx;
+                            }
+                        } else
+#endif
                         {
                             uint32_t sm = starts, idx = incl - nmine;
                             while (sm) {
@@ -766,6 +814,7 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                         __builtin_amdgcn_wave_barrier();
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                         const uint32_t cnt = (ntok - tb) < (uint32_t)TLW ? (ntok - tb) : (uint32_t)TLW;
+                        STP(2);
                         /* ---- rounds of 64 tokens; the vocabulary loads of round r+1 are
                          * issued before round r is counted ---- */
                         for (uint32_t t0 = 0; t0 < cnt && !(K1S_ABL & 4); t0 += 64) {
@@ -792,8 +841,8 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                             q.s4 = make_uint4(q.k0, q.k1, q.k2, q.k3);
                             q.t4 = q.s4;
 #else
-                            q.s4 = v.keys[q.hv];
-                            q.t4 = v.keys[(q.hv + 1) & (uint32_t)v.mask];
+                            q.s4 = gload(v.keys + q.hv);
+                            q.t4 = gload(v.keys + ((q.hv + 1) & (uint32_t)v.mask));
 #endif
                             if (pending) finish(pend);
                             pend = q;
@@ -802,20 +851,26 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
                         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                         __builtin_amdgcn_wave_barrier();
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                        STP(1);
                     }
                 }
             }
+            STP(3);
             drain();
-            STP(2);
+            STP(4);
             if (ahead) {   /* the next chunk's document offsets, in flight during this flush */
                 const uint32_t nng = (ndl + 1 - ndf) < gcap ? (ndl + 1 - ndf) : gcap;
                 dpre = (uint32_t)tid <= nng ? c.doc_off[ndf + tid] : 0ull;
                 dpre_ok = true;
             }
             /* group end is a document boundary (or the chunk end): emit everything */
+#ifdef K1_STAMPS
+            lds_barrier();
+#endif
+            STP(5);
             if (ng <= FEW) st_flush_few(S, o, gd0, ng, cs, ce, sb);
             else st_flush(S, o, gd0, ng, cs, ce, sb);
-            STP(3);
+            STP(6);
             if ((uint32_t)tid < ng) {
                 const uint32_t n = S.dsz[tid];
                 if (n) {
@@ -845,8 +900,8 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
 #ifdef K1_STAMPS
     STP(0);
     if (lane == 0 && o.stamps)
-        for (int k = 0; k < 5; ++k) atomicAdd(&o.stamps[k], (unsigned long long)st_acc[k]);
-    if (lane == 0 && o.stamps) atomicAdd(&o.stamps[5], 1ull);
+        for (int k = 0; k <= K1S_NPH; ++k) atomicAdd(&o.stamps[k], (unsigned long long)st_acc[k]);
+    if (lane == 0 && o.stamps) atomicAdd(&o.stamps[K1S_NPH + 1], 1ull);
 #endif
 }
 

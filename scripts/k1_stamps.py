@@ -1,5 +1,5 @@
 """K1 phase cycles (diagnostic build lib/libtfidf_hip_stamps.so, tokcount_st.hip K1_STAMPS):
-per-wave average s_memtime cycles in chunk set-up / walk+rounds / flush / chunk end, over
+per-wave average s_memtime cycles per phase (tokcount_st.hip K1_STAMPS), over
 one c2 run.  Usage (GPU box): TFIDF_LIB=stamps TFIDF_STAMPS=1 python scripts/k1_stamps.py"""
 import ctypes as C
 import os
@@ -22,9 +22,10 @@ with tfidf_abi.Engine(0) as e:
     buf = (C.c_uint64 * 22)()
     n = L.tfidf_debug_k1_stamps(e.h, buf, 22)
     v = list(buf)[:n]
-waves = v[5] or 1
-names = ["setup", "walk+rounds", "drain+flush", "chunk end"]
-tot = sum(v[:4])
-print(cfg, "K1 ms", round(info["ms_tokcount"], 4), "waves", waves, "chunk visits/wave", round(v[4] / waves, 1))
+names = ["setup", "walk", "rounds", "drain", "flush wait", "flush", "chunk end"]
+NPH = len(names)
+waves = v[NPH + 1] or 1
+tot = sum(v[:NPH])
+print(cfg, "K1 ms", round(info["ms_tokcount"], 4), "waves", waves, "chunk visits/wave", round(v[NPH] / waves, 1))
 for k, nm in enumerate(names):
     print("  %-12s %10.0f cycles/wave  %5.1f %%" % (nm, v[k] / waves, 100.0 * v[k] / max(tot, 1)))
