@@ -50,7 +50,7 @@ def k1_source_sha() -> str:
     """Digest of the K1 source: a committed PMC figure is valid only for the kernel it was
     measured on."""
     import hashlib
-    with open(os.path.join(REPO, "parallel-systems-mpi-tfidf_amd", "csrc", "tokcount_vs.hip"), "rb") as f:
+    with open(os.path.join(REPO, "parallel-systems-mpi-tfidf_amd", "csrc", "tokcount_st.hip"), "rb") as f:
         return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
@@ -257,7 +257,7 @@ def main():
             "stage_ms": {k: round(v, 4) for k, v in info["stages"].items()},
             "k1_work": {"chunks": int(info["nchunks"]), "partial_records": int(info["partial_records"]),
                         "vocab_capacity": int(info["vocab_capacity"]), "terms": int(info["nterms"])},
-            "roofline": {"bound": "hbm", "kernel": "k_tokcount_vs (K1)", "achieved": round(achieved, 2),
+            "roofline": {"bound": "hbm", "kernel": "k_tokcount_st (K1)", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "alg_bytes_per_launch": int(alg_bytes),

@@ -11,7 +11,7 @@ T=${1:-round}
 OUT=$R/gpurun_out/$T
 mkdir -p $OUT
 bash $R/scripts/prof_k1.sh $T > $OUT/pmc.log 2>&1
-python3 $R/scripts/traffic_k1.py $R/gpurun_out/prof_$T $R/profiles/k1_pmc_traffic.json $OUT/k1_pmc_traffic.json
+python3 $R/scripts/traffic_k1.py $R/gpurun_out/prof_$T ${KEY:-c2} $OUT/k1_pmc_traffic.json
 bash $R/scripts/kstats.sh $T > $OUT/kernel_stats.txt 2>&1
 cp $(find $R/gpurun_out/ks_$T -name "*kernel_stats.csv" | head -1) $OUT/kernel_stats.csv
 cd $R && timeout -k 10 300 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err

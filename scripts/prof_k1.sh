@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-/root/repo}
 T=${1:-k1}
 OUT=$R/gpurun_out/prof_$T
 mkdir -p $OUT
-CMD="python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-emit"
+CMD="python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-emit --no-probe ${BENCH_ARGS:-}"
 PASSES=${PASSES:-5}
 i=0
 for pmc in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \

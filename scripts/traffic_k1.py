@@ -1,26 +1,38 @@
 #!/usr/bin/env python3
-"""HBM traffic per K1 launch from rocprofv3 PMC passes (scripts/prof_k1.sh output).
+"""HBM traffic per K1 launch from rocprofv3 PMC passes (scripts/prof_k1.sh output), stored
+per config in profiles/k1_pmc_traffic.json, the table bench.py's roofline.traffic reads.
 
 traffic = 2 x FETCH_SIZE + WRITE_SIZE per dispatch (KB -> bytes), the gfx950 correction
 of MI355X_MICROARCH.md §HBM (FETCH_SIZE reads half the bytes of a wide streaming read;
 applied to all reads, so for K1's 16-byte vocabulary gathers it is an upper bound).
-Steady-state value = median over the dispatches after the first.
+Steady-state value = median over the dispatches after the first.  Each entry carries the
+digest of the K1 source it was measured on (bench.py ignores an entry of another source).
 
-    python3 scripts/traffic_k1.py <prof_dir> <out.json> [<out2.json> ...]
+    python3 scripts/traffic_k1.py <prof_dir> <key> <table.json> [<copy.json> ...]
+      key: bench.py's key of the run (c2, c4, c5, c3_strong_g8 ...)
 """
 import csv
 import glob
+import hashlib
 import json
 import os
 import statistics
 import sys
 
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = "k_tokcount_st"
+
+
+def k1_source_sha() -> str:
+    with open(os.path.join(REPO, "parallel-systems-mpi-tfidf_amd", "csrc", "tokcount_st.hip"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
 
 def per_launch(prof_dir, counter):
     vals = []
-    for f in glob.glob(os.path.join(prof_dir, "p*", "*_counter_collection.csv")):
+    for f in glob.glob(os.path.join(prof_dir, "p*", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "k_tokcount_vs" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 vals.append(float(r["Counter_Value"]))
     if not vals:
         return None
@@ -28,20 +40,27 @@ def per_launch(prof_dir, counter):
 
 
 def main():
-    prof_dir, outs = sys.argv[1], sys.argv[2:]
+    prof_dir, key, table, copies = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4:]
     fetch = per_launch(prof_dir, "FETCH_SIZE")
     write = per_launch(prof_dir, "WRITE_SIZE")
-    doc = {"kernel": "k_tokcount_vs", "fetch_size_kb": fetch, "write_size_kb": write,
-           "hbm_bytes_per_launch": None,
-           "formula": "2*FETCH_SIZE + WRITE_SIZE (KB*1024); x2 on reads per MI355X_MICROARCH.md §HBM "
-                      "(exact for the 16-B streaming corpus reads, an upper bound for the vocabulary gathers)"}
+    e = {"kernel": KERNEL, "k1_source_sha": k1_source_sha(), "fetch_size_kb": fetch, "write_size_kb": write,
+         "hbm_bytes_per_launch": None, "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes ({key})",
+         "formula": "2*FETCH_SIZE + WRITE_SIZE (KB*1024); x2 on reads per MI355X_MICROARCH.md §HBM "
+                    "(exact for the 16-B streaming corpus reads, an upper bound for the vocabulary gathers)"}
     if fetch is not None and write is not None:
-        doc["hbm_bytes_per_launch"] = int((2.0 * fetch + write) * 1024)
-    for o in outs:
+        e["hbm_bytes_per_launch"] = int((2.0 * fetch + write) * 1024)
+    tab = {}
+    if os.path.exists(table):
+        with open(table) as f:
+            old = json.load(f)
+        if isinstance(old, dict) and "kernel" not in old:
+            tab = old
+    tab[key] = e
+    for o in [table] + copies:
         os.makedirs(os.path.dirname(os.path.abspath(o)), exist_ok=True)
         with open(o, "w") as f:
-            json.dump(doc, f, indent=1)
-    print(json.dumps(doc))
+            json.dump(tab, f, indent=1)
+    print(key, json.dumps(e))
 
 
 if __name__ == "__main__":
