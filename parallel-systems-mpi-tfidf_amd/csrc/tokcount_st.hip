@@ -39,7 +39,9 @@
 /* timing-only ablation builds (make variant NAME=s1 DEFS=-DK1S_ABL=1; results invalid):
  * 1 no vocabulary loads/compare (slot from the key), 2 no LDS counting, 4 no token rounds,
  * 8 no token entries (walk + flush only), 16 no corpus loads, 32 flush without record
- * writes, 64 flush = table clear only, 128 corpus bytes from the first MiB (no HBM latency) */
+ * writes, 64 flush = table clear only, 128 corpus bytes from the first MiB (no HBM latency),
+ * 256 record space without the device atomics (few-document flush), 512 LDS counting with
+ * plain read-modify-writes instead of LDS atomics */
 #ifndef K1S_ABL
 #define K1S_ABL 0
 #endif
@@ -381,6 +383,11 @@ __device__ void st_flush_few(StShared& S, const K1Out& o, uint32_t gd0, uint32_t
     asm volatile("" : "+v"(tid));
     const int lane = tid & 63, w = tid >> 6;
     lds_barrier();                  /* every wave's walk is done */
+    if (K1S_ABL & 64) {
+        for (int j = 0; j < EPT; ++j) tbl_clear(S, j * NT + tid);
+        lds_barrier();
+        return;
+    }
     const uint32_t smask = (1u << sb) - 1u;
     uint32_t ek[EPT], ec[EPT];
     uint32_t pk[FEW / 2] = {0, 0, 0, 0};
@@ -439,8 +446,14 @@ __device__ void st_flush_few(StShared& S, const K1Out& o, uint32_t gd0, uint32_t
         const uint32_t off = incl - packed;
         const uint32_t nrec = all & 0xFFFFu, npart = all >> 16;
         unsigned long long a0 = 0, a1 = 0;
+#if K1S_ABL & 256
+        /* timing only: records at a per-workgroup offset, no device atomic round trip */
+        a0 = (unsigned long long)blockIdx.x * 4096ull % (o.rec_cap > 8192 ? o.rec_cap - 8192 : 1);
+        a1 = (unsigned long long)blockIdx.x * 256ull % (o.part_cap > 8192 ? o.part_cap - 8192 : 1);
+#else
         if (lane == 0 && nrec) a0 = atomicAdd(o.rec_alloc, (unsigned long long)nrec);
         if (lane == 32 && npart) a1 = atomicAdd(o.part_alloc, (unsigned long long)npart);
+#endif
         const unsigned long long rb = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(a0 >> 32), 0) << 32) |
                                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a0, 0);
         const unsigned long long pb = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(a1 >> 32), 32) << 32) |
@@ -569,11 +582,20 @@ __global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64
             const uint4 kk = bkt_read(S, b);
             const uint32_t j = bkt_match(kk, key);
             if (j < 4u) {
+#if K1S_ABL & 512
+                S.TC[4 * b + j] += 1u;   /* timing only: plain read-modify-write */
+#else
                 atomicAdd(&S.TC[4 * b + j], 1u);
+#endif
             } else {
                 const uint32_t e = bkt_empty(kk, key);
                 if (e < 4u && !over) {
+#if K1S_ABL & 512
+                    const uint32_t old = S.TK[4 * b + e];
+                    if (old == 0u) S.TK[4 * b + e] = key;
+#else
                     const uint32_t old = atomicCAS(&S.TK[4 * b + e], 0u, key);
+#endif
                     if (old == 0u || old == key) {
                         atomicAdd(&S.TC[4 * b + e], 1u);
                         claims = old == 0u ? 1u : 0u;
