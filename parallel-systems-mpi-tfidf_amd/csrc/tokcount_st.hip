@@ -79,7 +79,10 @@ namespace {
 #define K1S_TB 3584
 #endif
 constexpr int NT = K1S_NT;                /* threads per workgroup */
-constexpr int WG_PER_CU = 1024 / NT;      /* 16 waves per CU */
+#ifndef K1S_WGCU
+#define K1S_WGCU (1024 / K1S_NT)          /* workgroups per CU: 16 waves per CU */
+#endif
+constexpr int WG_PER_CU = K1S_WGCU;
 constexpr int NWAVE = NT / 64;
 constexpr int WSTEP = 992;                /* bytes a wave step owns: lanes 1..62, one 16-byte group each;
                                              lane 0 holds the 16 bytes before (the byte before
@@ -512,7 +515,7 @@ __device__ __forceinline__ uint32_t perm_sel(uint32_t n, uint32_t k) {
 
 }  // namespace
 
-__global__ __launch_bounds__(NT, 4) void k_tokcount_st(CorpusDev c, const uint64_t* __restrict__ chunk_start,
+__global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, const uint64_t* __restrict__ chunk_start,
                                                        const uint32_t* __restrict__ chunk_doc, uint64_t c0,
                                                        uint64_t c1, VocabDev v, K1Out o, uint32_t sb, uint32_t gcap) {
     __shared__ __attribute__((aligned(16))) StShared S;
@@ -931,7 +934,7 @@ int launch_tokcount_st(const CorpusDev& c, const uint64_t* chunk_start, const ui
                        uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s) {
     if (c1 <= c0) return 0;
     if (v.mask >= (1ull << SLOT_BITS)) return -3; /* slot must fit the LDS entry */
-    static_assert(sizeof(StShared) * WG_PER_CU <= 163840, "16 waves per CU");
+    static_assert(sizeof(StShared) * WG_PER_CU <= 163840, "LDS of WG_PER_CU workgroups per CU");
     static_assert(TB % NT == 0 && TB % 4 == 0, "table rows");
     static int ncu = 0;
     if (!ncu) {
