@@ -481,7 +481,11 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
         HIPCHK(hipMemsetAsync(ctx->stamps.p, 0, 8 * K1_STAMP_WORDS, s));
         o.stamps = ctx->stamps.as<unsigned long long>();
     }
-    if (nchunks && ctx->k1_vs && ctx->k1_mode == 0)
+    /* the LDS-staged kernel is the low-cardinality one: with a vocabulary table past
+     * K1_ST_MAX_CAP slots (config 4: ~1e7 terms, nearly every token a new (doc, term) pair)
+     * its bucketed LDS count table runs full and the round-1 kernel is 2.3x faster (c4:
+     * 11.5 vs 26.2 ms) */
+    if (nchunks && ctx->k1_vs && ctx->k1_mode == 0 && ctx->vcap <= K1_ST_MAX_CAP)
         LCHK(launch_tokcount_st(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
     else if (nchunks && ctx->k1_vs)
         LCHK(launch_tokcount_vs(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
@@ -519,7 +523,7 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     }
     if (st & ST_VOCAB_FULL) {   /* the run stopped inserting early: V unknown */
         if (ctx->vcap >= K1_VS_MAX_CAP) return TFIDF_E_CAPACITY;
-        ctx->vcap = ctx->vcap * 8 < K1_VS_MAX_CAP ? ctx->vcap * 8 : K1_VS_MAX_CAP;
+        ctx->vcap = ctx->vcap * 4 < K1_VS_MAX_CAP ? ctx->vcap * 4 : K1_VS_MAX_CAP;
         retry = true;
     }
     if (st & ST_REC_FULL) { ctx->rec_cap = R_main + R_main / 4 + 4096; retry = true; }
@@ -552,7 +556,10 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     /* keep probes short: the low load pays while the table is L2/MALL-sized (<= 16M slots,
      * 256 MB of keys); past that every probe is an HBM access anyway, so up to 45 % */
     if ((uint64_t)V * 100 > cap * (cap < VOCAB_LOW_LOAD_CAP ? ctx->vload_pct : 45u)) {
-        while ((uint64_t)V * 100 > ctx->vcap * (ctx->vcap < VOCAB_LOW_LOAD_CAP ? ctx->vload_pct : 45u)) ctx->vcap *= 4;
+        /* the smallest table within the load limit: a table twice too large costs its
+         * clear and a sparser compaction pass (c4: 64M -> 32M slots, vocabulary stage
+         * 3.1 -> 2.65 ms) */
+        while ((uint64_t)V * 100 > ctx->vcap * (ctx->vcap < VOCAB_LOW_LOAD_CAP ? ctx->vload_pct : 45u)) ctx->vcap *= 2;
         if (ctx->vcap > K1_VS_MAX_CAP && cap < K1_VS_MAX_CAP) ctx->vcap = K1_VS_MAX_CAP;
         if (ctx->vcap != cap) return 1;
     }

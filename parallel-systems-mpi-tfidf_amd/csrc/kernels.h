@@ -21,7 +21,9 @@
 #ifndef BIG_DOC
 #define BIG_DOC      49152u              /* documents longer than this are split across chunks */
 #endif
+#ifndef K5_MAX_PAIRS
 #define K5_MAX_PAIRS 2048                /* largest complete (unmerged) document K5 sorts in LDS */
+#endif
 
 /* status bits (device word) */
 #define ST_VOCAB_FULL  1u
@@ -96,6 +98,7 @@ int launch_tokcount_st(const CorpusDev& c, const uint64_t* chunk_start, const ui
 int launch_tokcount_vs(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc, uint64_t c0,
                        uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s);
 #define K1_VS_MAX_CAP (1ull << 28)
+#define K1_ST_MAX_CAP (1ull << 22)   /* tokcount_st up to this vocabulary capacity, tokcount_vs beyond */
 
 /* vocabulary finalisation */
 int launch_vocab_flags(const VocabDev& v, uint64_t cap, uint32_t* flags, hipStream_t s);
