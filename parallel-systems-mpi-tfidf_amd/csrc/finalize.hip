@@ -901,6 +901,9 @@ constexpr int K5_BATCH = 8;           /* gathers per lane in flight together */
 constexpr uint32_t K5_NB_BITS = 9;    /* bucket sort: 512 buckets by the rank's top bits */
 constexpr uint32_t K5_NB = 1u << K5_NB_BITS;
 constexpr uint32_t K5_GROUP_MAX = 48; /* larger buckets (skewed ranks): the radix path */
+constexpr uint32_t K5L_NB_BITS = 11;  /* k_score_large: buckets by the rank's top 11 bits */
+constexpr uint32_t K5L_NB = 1u << K5L_NB_BITS;
+constexpr uint32_t K5L_GROUP_MAX = 32;
 
 /* idf of every term rank: one gather per pair in K5 instead of three dependent ones */
 __global__ void k_idf_of_rank(const uint32_t* __restrict__ df_of_rank, const uint32_t* __restrict__ idf_idx,
@@ -1334,6 +1337,8 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
     __shared__ uint32_t hist[256], run[256];
     __shared__ uint32_t wcnt[NT / 64][256];
     __shared__ uint32_t wsum[NT / 64];
+    __shared__ uint32_t bh[K5L_NB];
+    __shared__ uint32_t bmax;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t nlarge = *a.large_count;
     for (uint32_t li = blockIdx.x; li < nlarge; li += gridDim.x) {
@@ -1355,6 +1360,47 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
     for (uint32_t j = tid; j < n; j += NT) {
         kbuf[0][j] = k5_rank(a, G(a.rec_slot)[rb + j]);
         vbuf[0][j] = G(a.rec_cnt)[rb + j];
+    }
+    {
+        /* bucket sort (ranks are distinct within a document): K5L_NB buckets by the rank's
+         * top bits, an element's position = its bucket's start + the smaller keys in its
+         * bucket.  One histogram, one scan, one scatter instead of rank_bits/8 stable radix
+         * passes; skewed documents (a bucket over K5L_GROUP_MAX) keep the radix passes. */
+        const uint32_t hsh = a.rank_bits > K5L_NB_BITS ? a.rank_bits - K5L_NB_BITS : 0u;
+        for (uint32_t q = tid; q < K5L_NB; q += NT) bh[q] = 0u;
+        if (tid == 0) bmax = 0u;
+        __syncthreads();
+        for (uint32_t j = tid; j < n; j += NT) atomicAdd(&bh[kbuf[0][j] >> hsh], 1u);
+        __syncthreads();
+        constexpr uint32_t PER = K5L_NB / NT;
+        uint32_t v[PER], tot = 0, mx = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q) { v[q] = bh[tid * PER + q]; tot += v[q]; mx = v[q] > mx ? v[q] : mx; }
+        uint32_t all;
+        uint32_t run = block_excl_scan<NT>(tot, wsum, &all);
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q) { bh[tid * PER + q] = run; run += v[q]; }
+        mx = wave_max(mx);
+        if (lane == 0) atomicMax(&bmax, mx);
+        __syncthreads();
+        if (bmax <= K5L_GROUP_MAX) {
+            for (uint32_t j = tid; j < n; j += NT) {
+                const uint32_t k = kbuf[0][j];
+                const uint32_t q = atomicAdd(&bh[k >> hsh], 1u);
+                kbuf[1][q] = k;
+                vbuf[1][q] = j;
+            }
+            __syncthreads();   /* bh[d] = bucket d's end = bucket d+1's start */
+            for (uint32_t p = tid; p < n; p += NT) {
+                const uint32_t k = kbuf[1][p], d = k >> hsh;
+                const uint32_t gs = d ? bh[d - 1] : 0u, ge = bh[d];
+                uint32_t less = 0;
+                for (uint32_t f = gs; f < ge; ++f) less += kbuf[1][f] < k ? 1u : 0u;
+                k5_emit(a, ob + gs + less, ds, k, vbuf[0][vbuf[1][p]]);
+            }
+            __syncthreads();   /* the next document reuses the LDS buffers */
+            continue;
+        }
     }
     const uint64_t lt = (1ull << lane) - 1ull;
     int cur = 0;

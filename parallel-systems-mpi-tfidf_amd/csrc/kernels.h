@@ -22,7 +22,7 @@
 #define BIG_DOC      49152u              /* documents longer than this are split across chunks */
 #endif
 #ifndef K5_MAX_PAIRS
-#define K5_MAX_PAIRS 2048                /* largest complete (unmerged) document K5 sorts in LDS */
+#define K5_MAX_PAIRS 4096                /* largest complete (unmerged) document K5 sorts in LDS */
 #endif
 
 /* status bits (device word) */
