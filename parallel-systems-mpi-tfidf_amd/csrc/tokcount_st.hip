@@ -41,7 +41,8 @@
  * 8 no token entries (walk + flush only), 16 no corpus loads, 32 flush without record
  * writes, 64 flush = table clear only, 128 corpus bytes from the first MiB (no HBM latency),
  * 256 record space without the device atomics (few-document flush), 512 LDS counting with
- * plain read-modify-writes instead of LDS atomics */
+ * plain read-modify-writes instead of LDS atomics, 1024 keys whose home bucket is full (or whose
+ * claim was lost) dropped instead of probing on */
 #ifndef K1S_ABL
 #define K1S_ABL 0
 #endif
@@ -97,6 +98,11 @@ constexpr int TLW = 192;                  /* token entries per wave and compacti
 constexpr uint32_t LEN_LONG = 31u;
 #ifndef K1S_ENT
 #define K1S_ENT 0                         /* 1: unrolled token entries (A/B: more spills, slower) */
+#endif
+#ifndef K1S_PIPE
+#define K1S_PIPE 0                        /* 1: the pending round resolved before the next one is built in
+                                             place (no register copy of in-flight loads): 2.37 vs 2.38 ms
+                                             with by-value VocabDev, neither beats the default */
 #endif        /* token entry: term of >= 16 bytes or past the window */
 
 struct StShared {
@@ -152,28 +158,51 @@ __device__ __forceinline__ uint32_t compress4(uint32_t m) {   /* bits 7, 15, 23,
     return m & 0xFu;
 }
 
-/* The LDS count table: buckets of 4 slots (TK: 32-bit keys, 0 = empty; TC: counts).  A key
- * lives in its home bucket unless that bucket was full when it was inserted, then in the
- * next bucket with room (slots are only emptied by the flush, so a home bucket with an
- * empty slot proves a key is not further on). */
-constexpr uint32_t NB = TB / 4;
+/* The LDS count table: buckets of BW slots (TK: 32-bit keys, 0 = empty; TC: counts).  A
+ * key lives in its home bucket unless that bucket was full when it was inserted, then in
+ * the next bucket with room (slots are only emptied by the flush, so a home bucket with an
+ * empty slot proves a key is not further on).  With 4-slot buckets a c2 chunk's ~1000
+ * keys in 896 buckets leave the home bucket full for ~2.6 % of new keys, which sends about
+ * half of all rounds through bkt_slow (0.2 ms of K1, timing-only build K1S_ABL=1024);
+ * 8-slot buckets (two ds_read_b128, K1S_BW=8) make that rare but cost the same in compares
+ * (c2 2.255 vs 2.222 ms, c5 2.441 vs 2.432 ms): 4-slot buckets stay. */
+#ifndef K1S_BW
+#define K1S_BW 4
+#endif
+constexpr uint32_t BW = K1S_BW;
+static_assert(BW == 4 || BW == 8, "bucket width");
+constexpr uint32_t NB = TB / BW;
+struct BktK {
+    uint4 a, b;                           /* slots 0-3, 4-7 (b unused for 4-slot buckets) */
+};
 __device__ __forceinline__ uint32_t bkt_hash(uint32_t key) {
     return (uint32_t)(((uint64_t)(key * 0x9E3779B1u) * (uint64_t)NB) >> 32);   /* [0, NB) */
 }
 __device__ __forceinline__ uint32_t bkt_next(uint32_t b) { return b + 1 == NB ? 0u : b + 1; }
-__device__ __forceinline__ uint4 bkt_read(StShared& S, uint32_t b) { return reinterpret_cast<const uint4*>(S.TK)[b]; }
-/* slot of `key` in bucket kk (4 if absent) */
-__device__ __forceinline__ uint32_t bkt_match(uint4 kk, uint32_t key) {
-    return kk.x == key ? 0u : kk.y == key ? 1u : kk.z == key ? 2u : kk.w == key ? 3u : 4u;
+__device__ __forceinline__ BktK bkt_read(StShared& S, uint32_t b) {
+    const uint4* t = reinterpret_cast<const uint4*>(S.TK) + b * (BW / 4);
+    BktK k;
+    k.a = t[0];
+    k.b = BW == 8 ? t[1] : make_uint4(0, 0, 0, 0);
+    return k;
 }
-/* the first empty slot of bucket kk, scanning from slot key & 3 (different keys spread over
- * the free slots of a bucket they share), 4 if full */
-__device__ __forceinline__ uint32_t bkt_empty(uint4 kk, uint32_t key) {
-    const uint32_t em = (kk.x == 0u ? 1u : 0u) | (kk.y == 0u ? 2u : 0u) | (kk.z == 0u ? 4u : 0u) | (kk.w == 0u ? 8u : 0u);
-    if (!em) return 4u;
-    const uint32_t r0 = key & 3u;
-    const uint32_t rot = ((em | (em << 4)) >> r0) & 0xFu;
-    return ((uint32_t)__builtin_ctz(rot) + r0) & 3u;
+/* slot of `key` in bucket kk (BW if absent) */
+__device__ __forceinline__ uint32_t bkt_match(const BktK& kk, uint32_t key) {
+    uint32_t j = kk.a.x == key ? 0u : kk.a.y == key ? 1u : kk.a.z == key ? 2u : kk.a.w == key ? 3u : 4u;
+    if (BW == 8 && j == 4u)
+        j = kk.b.x == key ? 4u : kk.b.y == key ? 5u : kk.b.z == key ? 6u : kk.b.w == key ? 7u : 8u;
+    return j;
+}
+/* the first empty slot of bucket kk, scanning from slot key % BW (different keys spread over
+ * the free slots of a bucket they share), BW if full */
+__device__ __forceinline__ uint32_t bkt_empty(const BktK& kk, uint32_t key) {
+    uint32_t em = (kk.a.x == 0u ? 1u : 0u) | (kk.a.y == 0u ? 2u : 0u) | (kk.a.z == 0u ? 4u : 0u) | (kk.a.w == 0u ? 8u : 0u);
+    if (BW == 8)
+        em |= (kk.b.x == 0u ? 16u : 0u) | (kk.b.y == 0u ? 32u : 0u) | (kk.b.z == 0u ? 64u : 0u) | (kk.b.w == 0u ? 128u : 0u);
+    if (!em) return BW;
+    const uint32_t r0 = key & (BW - 1u);
+    const uint32_t rot = ((em | (em << BW)) >> r0) & ((1u << BW) - 1u);
+    return ((uint32_t)__builtin_ctz(rot) + r0) & (BW - 1u);
 }
 __device__ __forceinline__ void tbl_read(StShared& S, uint32_t i, uint32_t& key, uint32_t& cnt) { key = S.TK[i]; cnt = S.TC[i]; }
 __device__ __forceinline__ void tbl_clear(StShared& S, uint32_t i) { S.TK[i] = 0u; S.TC[i] = 0u; }
@@ -204,6 +233,9 @@ __device__ __forceinline__ uint64_t uni64(uint64_t x) {
 
 /* term slot of a token whose term is >= 16 bytes (or runs past the 32-byte window): the
  * token is re-read from HBM (rare for text) */
+/* (VocabDev by reference puts the kernel's copy in scratch, so the rounds reload the table
+ * pointer / mask with scratch loads; passed by value it stays in SGPRs, but then 14 more
+ * SGPRs spill and K1 measured 2.37-2.38 vs 2.23 ms on c2: kept by reference) */
 __device__ __noinline__ uint32_t slow_slot(const uint8_t* __restrict__ bytes, const VocabDev& v, uint64_t p0,
                                            uint64_t dend, uint32_t* status) {
     uint64_t p = p0;
@@ -248,15 +280,15 @@ constexpr int PMAX = 16;
 __device__ BKT_SLOW_ATTR uint32_t bkt_slow(StShared& S, const K1Out& o, uint32_t key, uint32_t b, bool over,
                                           uint32_t gd0, uint32_t sb) {
     for (int probe = 0, tries = 0; probe < PMAX && tries < 64; ++tries) {
-        const uint4 kk = bkt_read(S, b);
+        const BktK kk = bkt_read(S, b);
         const uint32_t j = bkt_match(kk, key);
-        if (j < 4u) { atomicAdd(&S.TC[4 * b + j], 1u); return 0u; }
+        if (j < BW) { atomicAdd(&S.TC[BW * b + j], 1u); return 0u; }
         const uint32_t e = bkt_empty(kk, key);
-        if (e < 4u) {
+        if (e < BW) {
             if (over) break;               /* not in the table: a bucket with room ends the chain */
-            const uint32_t old = atomicCAS(&S.TK[4 * b + e], 0u, key);
+            const uint32_t old = atomicCAS(&S.TK[BW * b + e], 0u, key);
             if (old == 0u || old == key) {
-                atomicAdd(&S.TC[4 * b + e], 1u);
+                atomicAdd(&S.TC[BW * b + e], 1u);
                 return old == 0u ? 1u : 0u;
             }
             continue;                      /* lost the slot to another key: re-read this bucket */
@@ -582,25 +614,25 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, cons
         uint32_t claims = 0u;
         bool slow = false;
         if (key) {
-            const uint4 kk = bkt_read(S, b);
+            const BktK kk = bkt_read(S, b);
             const uint32_t j = bkt_match(kk, key);
-            if (j < 4u) {
+            if (j < BW) {
 #if K1S_ABL & 512
-                S.TC[4 * b + j] += 1u;   /* timing only: plain read-modify-write */
+                S.TC[BW * b + j] += 1u;   /* timing only: plain read-modify-write */
 #else
-                atomicAdd(&S.TC[4 * b + j], 1u);
+                atomicAdd(&S.TC[BW * b + j], 1u);
 #endif
             } else {
                 const uint32_t e = bkt_empty(kk, key);
-                if (e < 4u && !over) {
+                if (e < BW && !over) {
 #if K1S_ABL & 512
-                    const uint32_t old = S.TK[4 * b + e];
-                    if (old == 0u) S.TK[4 * b + e] = key;
+                    const uint32_t old = S.TK[BW * b + e];
+                    if (old == 0u) S.TK[BW * b + e] = key;
 #else
-                    const uint32_t old = atomicCAS(&S.TK[4 * b + e], 0u, key);
+                    const uint32_t old = atomicCAS(&S.TK[BW * b + e], 0u, key);
 #endif
                     if (old == 0u || old == key) {
-                        atomicAdd(&S.TC[4 * b + e], 1u);
+                        atomicAdd(&S.TC[BW * b + e], 1u);
                         claims = old == 0u ? 1u : 0u;
                     } else {
                         slow = true;
@@ -610,7 +642,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, cons
                 }
             }
         }
-        if (__ballot(slow) != 0ull) {
+        if (!(K1S_ABL & 1024) && __ballot(slow) != 0ull) {   /* 1024: timing only, slow keys dropped */
             if (slow) claims = bkt_slow(S, o, key, b, over, gd0_cur, sb);
         }
         const uint32_t wc = (uint32_t)__popcll(__ballot(claims != 0u));
@@ -843,7 +875,17 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, cons
                         /* ---- rounds of 64 tokens; the vocabulary loads of round r+1 are
                          * issued before round r is counted ---- */
                         for (uint32_t t0 = 0; t0 < cnt && !(K1S_ABL & 4); t0 += 64) {
+#if K1S_PIPE
+                            /* the pending round is resolved FIRST (its loads were issued one
+                             * round ago), then the next round is built in place and its loads
+                             * fly while the pending round is counted: building into a second
+                             * Round and copying it over (`pend = q`) made the copy wait for
+                             * the loads just issued (s_waitcnt vmcnt(0) every round) */
+                            const uint32_t pkey = pending ? resolve(pend) : 0u;
+                            Round& q = pend;
+#else
                             Round q;
+#endif
                             const uint32_t t = t0 + lane;
                             const bool val = t < cnt;
                             const uint32_t e = val ? tl[t] : 0u;
@@ -869,8 +911,12 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, cons
                             q.s4 = gload(v.keys + q.hv);
                             q.t4 = gload(v.keys + ((q.hv + 1) & (uint32_t)v.mask));
 #endif
+#if K1S_PIPE
+                            if (pending) count(pkey);
+#else
                             if (pending) finish(pend);
                             pend = q;
+#endif
                             pending = true;
                         }
                         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -935,7 +981,7 @@ int launch_tokcount_st(const CorpusDev& c, const uint64_t* chunk_start, const ui
     if (c1 <= c0) return 0;
     if (v.mask >= (1ull << SLOT_BITS)) return -3; /* slot must fit the LDS entry */
     static_assert(sizeof(StShared) * WG_PER_CU <= 163840, "LDS of WG_PER_CU workgroups per CU");
-    static_assert(TB % NT == 0 && TB % 4 == 0, "table rows");
+    static_assert(TB % NT == 0 && TB % BW == 0, "table rows");
     static int ncu = 0;
     if (!ncu) {
         int dev = 0;
