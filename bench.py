@@ -46,18 +46,28 @@ def hip_device_sync():
         raise RuntimeError("hipDeviceSynchronize failed")
 
 
-def k1_source_sha() -> str:
+K1_SOURCES = {"k_tokcount_st": "tokcount_st.hip", "k_tokcount_vs": "tokcount_vs.hip", "k_tokcount": "tokcount.hip"}
+
+
+def k1_kernel(flags: int) -> str:
+    """The tokenize+count kernel the last run used (tfidf_run_info.flags)."""
+    if flags & tfidf_abi.RUN_K1_ST:
+        return "k_tokcount_st"
+    return "k_tokcount_vs" if flags & tfidf_abi.RUN_K1_VS else "k_tokcount"
+
+
+def k1_source_sha(kernel: str) -> str:
     """Digest of the K1 source: a committed PMC figure is valid only for the kernel it was
     measured on."""
     import hashlib
-    with open(os.path.join(REPO, "parallel-systems-mpi-tfidf_amd", "csrc", "tokcount_st.hip"), "rb") as f:
+    with open(os.path.join(REPO, "parallel-systems-mpi-tfidf_amd", "csrc", K1_SOURCES[kernel]), "rb") as f:
         return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
-def load_traffic(cfg: str, strong: bool, ngpu: int):
-    """HBM bytes per K1 launch from the committed rocprofv3 PMC passes of THIS config and
-    THIS K1 source (profiles/k1_pmc_traffic.json, written by scripts/traffic_k1.py), or
-    None: never another config's figure."""
+def load_traffic(cfg: str, strong: bool, ngpu: int, kernel: str):
+    """HBM bytes per K1 launch from the committed rocprofv3 PMC passes of THIS config, THIS
+    K1 kernel and THIS source (profiles/k1_pmc_traffic.json, written by
+    scripts/traffic_k1.py), or None: never another config's or kernel's figure."""
     p = os.path.join(REPO, "profiles", "k1_pmc_traffic.json")
     if not os.path.exists(p):
         return None, None
@@ -65,7 +75,7 @@ def load_traffic(cfg: str, strong: bool, ngpu: int):
         tab = json.load(f)
     key = f"{cfg}{'_strong' if strong else ''}_g{ngpu}" if ngpu > 1 else cfg
     e = tab.get(key) if isinstance(tab, dict) else None
-    if not isinstance(e, dict) or e.get("k1_source_sha") != k1_source_sha():
+    if not isinstance(e, dict) or e.get("kernel") != kernel or e.get("k1_source_sha") != k1_source_sha(kernel):
         return None, None
     return e.get("hbm_bytes_per_launch"), e.get("source")
 
@@ -233,7 +243,8 @@ def main():
         k1_avg_ms = float(np.mean(k1_ms))
         alg_bytes = C_bytes + 12.0 * P_pairs  # per K1 launch on this rank
         achieved = alg_bytes / (k1_avg_ms * 1e-3) / 1e9
-        traffic, traffic_src = load_traffic(args.config, args.strong, ngpu)
+        kern = k1_kernel(int(info["flags"]))
+        traffic, traffic_src = load_traffic(args.config, args.strong, ngpu, kern)
         line = {
             "metric": "corpus GB/s (TF-IDF hot path: tokenize->TF->DF->tf*idf->ordered output)",
             "value": round(C_all * args.steps / elapsed / 1e9, 4),
@@ -257,7 +268,7 @@ def main():
             "stage_ms": {k: round(v, 4) for k, v in info["stages"].items()},
             "k1_work": {"chunks": int(info["nchunks"]), "partial_records": int(info["partial_records"]),
                         "vocab_capacity": int(info["vocab_capacity"]), "terms": int(info["nterms"])},
-            "roofline": {"bound": "hbm", "kernel": "k_tokcount_st (K1)", "achieved": round(achieved, 2),
+            "roofline": {"bound": "hbm", "kernel": f"{kern} (K1)", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "alg_bytes_per_launch": int(alg_bytes),

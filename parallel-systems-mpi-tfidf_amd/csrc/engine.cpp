@@ -79,6 +79,7 @@ struct tfidf_ctx {
     uint32_t ablate = 0;    /* env TFIDF_K1_ABLATE: K1 timing experiments, pipeline stops after K1 */
     DevBuf stamps;
     bool k1_vs = false;     /* last run used the slot-keyed kernel (default) */
+    bool k1_st = false;     /* ... and of those the LDS-staged tokcount_st (else tokcount_vs) */
     hipEvent_t ev[S_NSTAGES + 1];
     Arena arena;
     DevBuf arena_buf;
@@ -485,7 +486,8 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
      * K1_ST_MAX_CAP slots (config 4: ~1e7 terms, nearly every token a new (doc, term) pair)
      * its bucketed LDS count table runs full and the round-1 kernel is 2.3x faster (c4:
      * 11.5 vs 26.2 ms) */
-    if (nchunks && ctx->k1_vs && ctx->k1_mode == 0 && ctx->vcap <= K1_ST_MAX_CAP)
+    ctx->k1_st = ctx->k1_vs && ctx->k1_mode == 0 && ctx->vcap <= K1_ST_MAX_CAP;
+    if (nchunks && ctx->k1_st)
         LCHK(launch_tokcount_st(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
     else if (nchunks && ctx->k1_vs)
         LCHK(launch_tokcount_vs(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
@@ -993,7 +995,7 @@ extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info) {
     info->ms_tokcount = ctx->ms_stage[S_TOKCOUNT];
     for (int i = 0; i < S_NSTAGES; ++i) info->ms_stage[i] = ctx->ms_stage[i];
     info->nstages = S_NSTAGES;
-    info->flags = ctx->k1_vs ? TFIDF_RUN_K1_VS : 0u;
+    info->flags = (ctx->k1_vs ? TFIDF_RUN_K1_VS : 0u) | (ctx->k1_st ? TFIDF_RUN_K1_ST : 0u);
     return TFIDF_OK;
 }
 

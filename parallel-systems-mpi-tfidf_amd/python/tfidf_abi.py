@@ -20,6 +20,8 @@ CLI_PATH = os.path.join(PKG_DIR, "bin", "tfidf")
 
 TFIDF_CORPUS_DEVICE = 1
 UNIQUE_ID_BYTES = 128
+RUN_K1_VS = 2   # tfidf_run_info.flags (include/tfidf.h): slot-keyed K1 ...
+RUN_K1_ST = 4   # ... run as k_tokcount_st (else k_tokcount_vs)
 
 # exported symbols declared by include/tfidf.h
 EXPORTS = [

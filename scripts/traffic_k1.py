@@ -20,30 +20,46 @@ import statistics
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "k_tokcount_st"
+SOURCES = {"k_tokcount_st": "tokcount_st.hip", "k_tokcount_vs": "tokcount_vs.hip", "k_tokcount": "tokcount.hip"}
 
 
-def k1_source_sha() -> str:
-    with open(os.path.join(REPO, "parallel-systems-mpi-tfidf_amd", "csrc", "tokcount_st.hip"), "rb") as f:
+def k1_source_sha(kernel) -> str:
+    with open(os.path.join(REPO, "parallel-systems-mpi-tfidf_amd", "csrc", SOURCES[kernel]), "rb") as f:
         return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
+def kernel_of(name):
+    """k_tokcount_st / k_tokcount_vs / k_tokcount from a demangled kernel name"""
+    for k in ("k_tokcount_st", "k_tokcount_vs"):
+        if k in name:
+            return k
+    return "k_tokcount" if "k_tokcount(" in name else None
+
+
 def per_launch(prof_dir, counter):
-    vals = []
+    """median per-dispatch value of `counter` over the dispatches of the K1 kernel the run
+    ended on (the steady state: a config whose first runs grow the vocabulary table may
+    start on another K1 kernel), and that kernel"""
+    recs = []
     for f in glob.glob(os.path.join(prof_dir, "p*", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
-                vals.append(float(r["Counter_Value"]))
-    if not vals:
-        return None
-    return statistics.median(vals[1:] if len(vals) > 1 else vals)
+            k = kernel_of(r["Kernel_Name"])
+            if k and r["Counter_Name"] == counter:
+                recs.append((int(r.get("Dispatch_Id", 0) or 0), k, float(r["Counter_Value"])))
+    if not recs:
+        return None, None
+    recs.sort()
+    kern = recs[-1][1]
+    vals = [v for _, k, v in recs if k == kern]
+    return statistics.median(vals[1:] if len(vals) > 1 else vals), kern
 
 
 def main():
     prof_dir, key, table, copies = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4:]
-    fetch = per_launch(prof_dir, "FETCH_SIZE")
-    write = per_launch(prof_dir, "WRITE_SIZE")
-    e = {"kernel": KERNEL, "k1_source_sha": k1_source_sha(), "fetch_size_kb": fetch, "write_size_kb": write,
+    fetch, kern = per_launch(prof_dir, "FETCH_SIZE")
+    write, _ = per_launch(prof_dir, "WRITE_SIZE")
+    kern = kern or "k_tokcount_st"
+    e = {"kernel": kern, "k1_source_sha": k1_source_sha(kern), "fetch_size_kb": fetch, "write_size_kb": write,
          "hbm_bytes_per_launch": None, "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes ({key})",
          "formula": "2*FETCH_SIZE + WRITE_SIZE (KB*1024); x2 on reads per MI355X_MICROARCH.md §HBM "
                     "(exact for the 16-B streaming corpus reads, an upper bound for the vocabulary gathers)"}
