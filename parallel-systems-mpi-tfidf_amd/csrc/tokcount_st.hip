@@ -263,7 +263,14 @@ __device__ __noinline__ uint32_t slow_slot(const uint8_t* __restrict__ bytes, co
 __device__ __noinline__ void overflow_record(unsigned long long* part_alloc, uint64_t part_cap, uint32_t* part_doc,
                                              uint32_t* part_slot, uint32_t* part_cnt, uint32_t* status, uint32_t doc,
                                              uint32_t slot) {
-    const unsigned long long q = atomicAdd(part_alloc, 1ull);
+    /* one device atomic per wave and call, not per lane: in overflow mode (config 4: every
+     * token a new pair) millions of lanes would otherwise queue on this one counter */
+    const uint64_t am = __ballot(1);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u));
+    unsigned long long b = 0;
+    if (rank == 0u) b = atomicAdd(part_alloc, (unsigned long long)__popcll(am));
+    const unsigned long long q = (((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(b >> 32)) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b)) + rank;
     if (q < part_cap) { part_doc[q] = doc; part_slot[q] = slot; part_cnt[q] = 1u; }
     else atomicOr(status, ST_PART_FULL);
 }
