@@ -92,7 +92,11 @@ constexpr int WSTEP = 992;                /* bytes a wave step owns: lanes 1..62
 constexpr int TB = K1S_TB;                /* LDS table entries (u32 key + u32 count): 14 per thread */
 constexpr int EPT = TB / NT;
 constexpr uint32_t FILL_LIMIT = TB - NT * 2 - 64; /* claims after which overflow mode starts */
-constexpr int GCAP = 256;                 /* documents per group at most (LDS arrays) */
+#ifndef K1S_GCAP
+#define K1S_GCAP 256
+#endif
+constexpr int GCAP = K1S_GCAP;            /* documents per group at most (LDS arrays) */
+static_assert(GCAP <= NT, "one thread per document of a group");
 constexpr uint32_t SLOT_BITS = 28;        /* vocabulary slots < 2^28 */
 constexpr int TLW = 192;                  /* token entries per wave and compaction pass */
 constexpr uint32_t LEN_LONG = 31u;
@@ -1000,7 +1004,7 @@ int launch_tokcount_st(const CorpusDev& c, const uint64_t* chunk_start, const ui
     const uint64_t grid = (c1 - c0) < wgs ? (c1 - c0) : wgs;
     /* key32 = 1 << 31 | doc-in-group << sb | slot: the group size follows the slot bits */
     const uint32_t sb = (uint32_t)__builtin_popcountll(v.mask);
-    const uint32_t gcap = (31u - sb) >= 8u ? (uint32_t)GCAP : (1u << (31u - sb));
+    const uint32_t gcap = (1u << (31u - sb)) >= (uint32_t)GCAP ? (uint32_t)GCAP : (1u << (31u - sb));
     k_tokcount_st<<<(unsigned)grid, NT, 0, s>>>(c, chunk_start, chunk_doc, c0, c1, v, o, sb, gcap);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
