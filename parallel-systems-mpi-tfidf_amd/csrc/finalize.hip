@@ -901,9 +901,7 @@ constexpr int K5_BATCH = 8;           /* gathers per lane in flight together */
 constexpr uint32_t K5_NB_BITS = 9;    /* bucket sort: 512 buckets by the rank's top bits */
 constexpr uint32_t K5_NB = 1u << K5_NB_BITS;
 constexpr uint32_t K5_GROUP_MAX = 48; /* larger buckets (skewed ranks): the radix path */
-constexpr uint32_t K5L_NB_BITS = 11;  /* k_score_large: buckets by the rank's top 11 bits */
-constexpr uint32_t K5L_NB = 1u << K5L_NB_BITS;
-constexpr uint32_t K5L_GROUP_MAX = 32;
+constexpr uint32_t K5L_GROUP_MAX = 32; /* k_score_large: larger buckets (skewed ranks) take the radix path */
 
 /* idf of every term rank: one gather per pair in K5 instead of three dependent ones */
 __global__ void k_idf_of_rank(const uint32_t* __restrict__ df_of_rank, const uint32_t* __restrict__ idf_idx,
@@ -1331,13 +1329,27 @@ __global__ __launch_bounds__(NT, K5_WPS) void k_score_wave(K5Args a) {
 /* Documents the wave kernel leaves: one workgroup each.  Presorted (merged) runs are
  * scored straight through; others are LSD radix-sorted by rank in LDS, 8-bit digits, with a
  * stable wave64 multisplit (8 ballots) per round of 256 elements. */
+/* Two instances share the list: MAXN = K5_MAX / 2 with 1024 buckets (38 KB of LDS: four
+ * workgroups per CU) takes presorted documents and those of <= K5_MAX / 2 pairs; MAXN =
+ * K5_MAX (72 KB: two per CU) the rest.  The bucket counters alias the radix scratch. */
+template <uint32_t MAXN, uint32_t NBB>
 __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
-    __shared__ uint32_t kbuf[2][K5_MAX];
-    __shared__ uint32_t vbuf[2][K5_MAX];
-    __shared__ uint32_t hist[256], run[256];
-    __shared__ uint32_t wcnt[NT / 64][256];
+    constexpr uint32_t NB = 1u << NBB;
+    __shared__ uint32_t kbuf[2][MAXN];
+    __shared__ uint32_t vbuf[2][MAXN];
+    union Scratch {
+        struct {
+            uint32_t hist[256], run[256];
+            uint32_t wcnt[NT / 64][256];
+        } r;                              /* radix passes */
+        uint32_t bh[NB];                  /* bucket sort */
+    };
+    __shared__ Scratch U;
+    uint32_t (&hist)[256] = U.r.hist;
+    uint32_t (&run)[256] = U.r.run;
+    uint32_t (&wcnt)[NT / 64][256] = U.r.wcnt;
+    uint32_t (&bh)[NB] = U.bh;
     __shared__ uint32_t wsum[NT / 64];
-    __shared__ uint32_t bh[K5L_NB];
     __shared__ uint32_t bmax;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t nlarge = *a.large_count;
@@ -1346,6 +1358,7 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
     const uint32_t d = G(a.order)[i];
     const uint32_t n = G(a.doc_npairs)[d];
     const bool presorted = (G(a.doc_flags)[d] & DF_PRESORTED) != 0;
+    if (MAXN < (uint32_t)K5_MAX ? (!presorted && n > MAXN) : (presorted || n <= (uint32_t)K5_MAX / 2)) continue;
     const uint64_t ob = G(a.out_off)[i], rb = G(a.doc_recoff)[d];
     const double ds = (double)G(a.doc_size)[d];
     if (rb + n > a.rec_total) { /* never expected: report instead of reading past the records */
@@ -1366,13 +1379,13 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
          * top bits, an element's position = its bucket's start + the smaller keys in its
          * bucket.  One histogram, one scan, one scatter instead of rank_bits/8 stable radix
          * passes; skewed documents (a bucket over K5L_GROUP_MAX) keep the radix passes. */
-        const uint32_t hsh = a.rank_bits > K5L_NB_BITS ? a.rank_bits - K5L_NB_BITS : 0u;
-        for (uint32_t q = tid; q < K5L_NB; q += NT) bh[q] = 0u;
+        const uint32_t hsh = a.rank_bits > NBB ? a.rank_bits - NBB : 0u;
+        for (uint32_t q = tid; q < NB; q += NT) bh[q] = 0u;
         if (tid == 0) bmax = 0u;
         __syncthreads();
         for (uint32_t j = tid; j < n; j += NT) atomicAdd(&bh[kbuf[0][j] >> hsh], 1u);
         __syncthreads();
-        constexpr uint32_t PER = K5L_NB / NT;
+        constexpr uint32_t PER = NB / NT;
         uint32_t v[PER], tot = 0, mx = 0;
 #pragma unroll
         for (uint32_t q = 0; q < PER; ++q) { v[q] = bh[tid * PER + q]; tot += v[q]; mx = v[q] > mx ? v[q] : mx; }
@@ -1468,6 +1481,11 @@ __global__ void k_large_list(K5Args a) {
     base = (uint32_t)__shfl(base, (int)leader);
     if (big) G(a.large_list)[base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull))] = i;
 }
+static void launch_score_large(const K5Args& a, uint32_t grid, hipStream_t s) {
+    static_assert(K5_MAX % 2 == 0 && K5_MAX / 2 >= 1024, "k_score_large instances");
+    k_score_large<(uint32_t)K5_MAX / 2, 10><<<grid, NT, 0, s>>>(a);
+    k_score_large<(uint32_t)K5_MAX, 11><<<grid, NT, 0, s>>>(a);
+}
 int launch_score_order(const K5Args& a, hipStream_t s, hipStream_t s2, hipEvent_t ev_fork, hipEvent_t ev_join) {
     if (!a.ndocs) return 0;
     if (hipMemsetAsync(a.large_count, 0, 4, s) != hipSuccess) return -1;
@@ -1485,7 +1503,7 @@ int launch_score_order(const K5Args& a, hipStream_t s, hipStream_t s2, hipEvent_
     const uint32_t grid = a.ndocs < 2048u ? a.ndocs : 2048u; /* persistent over the handed-off list */
     if (a.rank_bits + K5_IDX_BITS > 32) {   /* skewed wide documents are handed off during the run */
         k_score_wave<true><<<wg, NT, 0, s>>>(a);
-        k_score_large<<<grid, NT, 0, s>>>(a);
+        launch_score_large(a, grid, s);
         return ok();
     }
     k_large_list<<<grid_for(a.ndocs), NT, 0, s>>>(a);
@@ -1496,14 +1514,14 @@ int launch_score_order(const K5Args& a, hipStream_t s, hipStream_t s2, hipEvent_
         if (hipEventRecord(ev_fork, s) != hipSuccess) return -1;
         k_score_wave<false><<<wg, NT, 0, s>>>(a);
         if (hipStreamWaitEvent(s2, ev_fork, 0) != hipSuccess) return -1;
-        k_score_large<<<grid, NT, 0, s2>>>(a);
+        launch_score_large(a, grid, s2);
         if (hipEventRecord(ev_join, s2) != hipSuccess) return -1;
         if (hipStreamWaitEvent(s, ev_join, 0) != hipSuccess) return -1;
         return ok();
     }
 #endif
     k_score_wave<false><<<wg, NT, 0, s>>>(a);
-    k_score_large<<<grid, NT, 0, s>>>(a);
+    launch_score_large(a, grid, s);
     return ok();
 }
 
