@@ -157,6 +157,7 @@ typedef struct tfidf_run_info {
                                  kernel of TFIDF_K1=general or an unaligned corpus leaves it clear) */
 #define TFIDF_RUN_K1_ST   4u  /* ... run as the LDS-staged k_tokcount_st (vocabulary table <= 4M slots);
                                  clear with TFIDF_RUN_K1_VS set: k_tokcount_vs (larger tables) */
+#define TFIDF_RUN_K1_SPLIT 8u /* ... run as k_tok_resolve + k_count_slots (TFIDF_K1=split) */
 int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info);
 const char* tfidf_stage_name(int stage);
 /* Enables per-stage HIP event timing (adds a few event records per run). */

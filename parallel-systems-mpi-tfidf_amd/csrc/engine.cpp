@@ -73,13 +73,15 @@ struct tfidf_ctx {
     Xport* xp = nullptr;    /* peers of the DF exchange (RCCL or in-process); owned */
     int rank = 0, nranks = 1;
     bool timing = true;
-    int k1_mode = 0;        /* 0 auto (tokcount_st), 1 round-1 kernel (TFIDF_K1=vs), 2 general K1
-                               (TFIDF_K1=general): cross-checks and A/B timing */
+    int k1_mode = 0;        /* 0 auto (fused LDS-staged tokcount_st), 1 round-1 kernel (TFIDF_K1=vs),
+                               2 general K1 (TFIDF_K1=general), 3 split K1a + K1b (TFIDF_K1=split):
+                               cross-checks and A/B timing */
     bool stamps_on = false; /* env TFIDF_STAMPS=1 with the diagnostic library build */
     uint32_t ablate = 0;    /* env TFIDF_K1_ABLATE: K1 timing experiments, pipeline stops after K1 */
     DevBuf stamps;
     bool k1_vs = false;     /* last run used the slot-keyed kernel (default) */
     bool k1_st = false;     /* ... and of those the LDS-staged tokcount_st (else tokcount_vs) */
+    bool k1_split = false;  /* ... or the split k_tok_resolve + k_count_slots */
     hipEvent_t ev[S_NSTAGES + 1];
     Arena arena;
     DevBuf arena_buf;
@@ -95,6 +97,7 @@ struct tfidf_ctx {
     DevBuf syn_bytes, syn_off, syn_ids, syn_ntok, syn_blkfirst, syn_blkbytes, syn_cdf;
     /* stage buffers */
     DevBuf chunk_start, chunk_doc;
+    DevBuf tokstream, chunk_meta, tok_dlist, tok_dtok;   /* split K1 */
     DevBuf vkeys, vrep;
     /* vocabulary table: K1 is measurably faster at low load (fewer displaced keys behind
      * the two slots it loads per token): 1M slots (16 MB) to start, x4 past 12 % load */
@@ -207,6 +210,7 @@ int tfidf_open(int device, tfidf_ctx** out) {
     const char* km = getenv("TFIDF_K1");
     if (km && !strcmp(km, "general")) ctx->k1_mode = 2;
     if (km && !strcmp(km, "vs")) ctx->k1_mode = 1;
+    if (km && !strcmp(km, "split")) ctx->k1_mode = 3;
     const char* ks = getenv("TFIDF_STAMPS");
     ctx->stamps_on = ks && ks[0] == '1';
     const char* ka = getenv("TFIDF_K1_ABLATE");
@@ -245,7 +249,8 @@ void tfidf_close(tfidf_ctx* ctx) {
     ctx->arena2_buf.release();
     DevBuf* bufs[] = {&ctx->arena_buf, &ctx->in_bytes, &ctx->in_off, &ctx->in_ids, &ctx->syn_bytes, &ctx->syn_off,
                       &ctx->syn_ids, &ctx->syn_ntok, &ctx->syn_blkfirst, &ctx->syn_blkbytes, &ctx->syn_cdf,
-                      &ctx->chunk_start, &ctx->chunk_doc, &ctx->vkeys, &ctx->vrep, &ctx->rec_slot, &ctx->rec_cnt,
+                      &ctx->chunk_start, &ctx->chunk_doc, &ctx->tokstream, &ctx->chunk_meta, &ctx->tok_dlist,
+                      &ctx->tok_dtok, &ctx->vkeys, &ctx->vrep, &ctx->rec_slot, &ctx->rec_cnt,
                       &ctx->part_doc, &ctx->part_slot, &ctx->part_cnt, &ctx->doc_recoff, &ctx->doc_npairs,
                       &ctx->doc_size, &ctx->doc_flags, &ctx->counters, &ctx->dense, &ctx->vslot, &ctx->skey0,
                       &ctx->skey1, &ctx->seq0, &ctx->seq1, &ctx->rank_of_slot, &ctx->slot_of_rank, &ctx->rank16, &ctx->pkey0,
@@ -452,7 +457,7 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     /* K1 variant: the slot-keyed kernel (tokcount_vs.hip) needs a 16-byte aligned corpus
      * base; TFIDF_K1=general selects the general kernel (cross-checks) */
     const bool aligned = (((uintptr_t)c.bytes & 15u) == 0);
-    ctx->k1_vs = aligned && ctx->k1_mode <= 1;
+    ctx->k1_vs = aligned && (ctx->k1_mode <= 1 || ctx->k1_mode == 3);
     if (ctx->k1_vs && ctx->vcap > K1_VS_MAX_CAP) return TFIDF_E_CAPACITY;
     /* ---- K1 ---- */
     mark(ctx, S_TOKCOUNT);
@@ -486,8 +491,26 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
      * K1_ST_MAX_CAP slots (config 4: ~1e7 terms, nearly every token a new (doc, term) pair)
      * its bucketed LDS count table runs full and the round-1 kernel is 2.3x faster (c4:
      * 11.5 vs 26.2 ms) */
+    ctx->k1_split = ctx->k1_vs && ctx->k1_mode == 3 && ctx->vcap <= K1_ST_MAX_CAP;
     ctx->k1_st = ctx->k1_vs && ctx->k1_mode == 0 && ctx->vcap <= K1_ST_MAX_CAP;
-    if (nchunks && ctx->k1_st)
+    if (nchunks && ctx->k1_split) {
+        /* K1a's token stream: span/2 + N + 4 per chunk words bound the tokens (tokcount_split.hip) */
+        const uint64_t tw = tokcount_split_words(span, N, nchunks);
+        ENSURE(ctx->tokstream, tw * 4 + 256);
+        ENSURE(ctx->chunk_meta, (nchunks + 1) * 8);
+        ENSURE(ctx->tok_dlist, ((size_t)N + nchunks + 2) * 4);
+        ENSURE(ctx->tok_dtok, ((size_t)N + nchunks + 2) * 4);
+        K1Split sp{};
+        sp.tok = ctx->tokstream.as<uint32_t>();
+        sp.tok_words = tw;
+        sp.chunk_meta = ctx->chunk_meta.as<uint2>();
+        sp.dlist = ctx->tok_dlist.as<uint32_t>();
+        sp.dtok = ctx->tok_dtok.as<uint32_t>();
+        sp.shard_a = cnt + 16;
+        sp.shard_b = cnt + 24;
+        LCHK(launch_tokcount_split(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), nchunks, vd, o,
+                                   sp, s));
+    } else if (nchunks && ctx->k1_st)
         LCHK(launch_tokcount_st(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
     else if (nchunks && ctx->k1_vs)
         LCHK(launch_tokcount_vs(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
@@ -919,6 +942,19 @@ extern "C" int tfidf_debug_k1_stamps(tfidf_ctx* ctx, uint64_t* out, int n) {
     return m;
 }
 
+/* Diagnostics of the split K1 (tests/debug scripts only): copies the first n words of the
+ * last run's token stream (0), chunk metadata (1: 2 words per chunk), ordinal document list
+ * (2) or ordinal first-token indices (3) to the host. */
+extern "C" int tfidf_debug_split(tfidf_ctx* ctx, int what, uint32_t* out, uint64_t n) {
+    if (!ctx || !out) return TFIDF_E_INVAL;
+    DevBuf* b = what == 0 ? &ctx->tokstream : what == 1 ? &ctx->chunk_meta : what == 2 ? &ctx->tok_dlist
+              : what == 3 ? &ctx->tok_dtok : nullptr;
+    if (!b || !b->p) return TFIDF_E_STATE;
+    if (n * 4 > b->cap) n = b->cap / 4;
+    HIPCHK(hipMemcpy(out, b->p, 4 * (size_t)n, hipMemcpyDeviceToHost));
+    return (int)n;
+}
+
 /* Measured HBM streaming peaks: `iters` timed passes of a read-only stream
  * over nbytes and of an nbytes copy (counted as 2 x nbytes), after one warm-up pass each;
  * the buffers are allocated for the call and released. */
@@ -995,7 +1031,8 @@ extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info) {
     info->ms_tokcount = ctx->ms_stage[S_TOKCOUNT];
     for (int i = 0; i < S_NSTAGES; ++i) info->ms_stage[i] = ctx->ms_stage[i];
     info->nstages = S_NSTAGES;
-    info->flags = (ctx->k1_vs ? TFIDF_RUN_K1_VS : 0u) | (ctx->k1_st ? TFIDF_RUN_K1_ST : 0u);
+    info->flags = (ctx->k1_vs ? TFIDF_RUN_K1_VS : 0u) | (ctx->k1_st ? TFIDF_RUN_K1_ST : 0u) |
+                  (ctx->k1_split ? TFIDF_RUN_K1_SPLIT : 0u);
     return TFIDF_OK;
 }
 
