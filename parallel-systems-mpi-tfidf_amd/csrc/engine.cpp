@@ -491,7 +491,7 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
      * K1_ST_MAX_CAP slots (config 4: ~1e7 terms, nearly every token a new (doc, term) pair)
      * its bucketed LDS count table runs full and the round-1 kernel is 2.3x faster (c4:
      * 11.5 vs 26.2 ms) */
-    ctx->k1_split = ctx->k1_vs && ctx->k1_mode == 3 && ctx->vcap <= K1_ST_MAX_CAP;
+    ctx->k1_split = ctx->k1_vs && ctx->k1_mode == 3;
     ctx->k1_st = ctx->k1_vs && ctx->k1_mode == 0 && ctx->vcap <= K1_ST_MAX_CAP;
     if (nchunks && ctx->k1_split) {
         /* K1a's token stream: span/2 + N + 4 per chunk words bound the tokens (tokcount_split.hip) */

@@ -1,9 +1,9 @@
-"""Ad-hoc GPU diagnostics (not collected by pytest): python tests/debug_gpu.py <what>"""
+"""Ad-hoc GPU diagnostics (GPU box): python scripts/debug_gpu.py <what>"""
 import sys
 import os
 
 sys.path[:0] = [os.path.join(os.path.dirname(__file__), d) for d in
-                ("../parallel-systems-mpi-tfidf_amd/python", "../oracle", ".")]
+                ("../parallel-systems-mpi-tfidf_amd/python", "../oracle", "../tests")]
 import numpy as np  # noqa: E402
 
 import oracle_py  # noqa: E402
