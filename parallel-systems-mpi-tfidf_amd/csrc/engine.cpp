@@ -103,6 +103,7 @@ struct tfidf_ctx {
      * the two slots it loads per token): 1M slots (16 MB) to start, x4 past 12 % load */
     uint64_t vcap = 1ull << 20;
 #define VOCAB_LOW_LOAD_CAP (1ull << 24)
+#define IDF_FULL_MAX (1ull << 24)   /* documents up to which the idf table covers every df */
     uint32_t vload_pct = 12;
     DevBuf rec_slot, rec_cnt;
     uint64_t rec_cap = 0;
@@ -114,6 +115,7 @@ struct tfidf_ctx {
     DevBuf pkey0, pkey1, pseq0, pseq1, phead;
     DevBuf big_list, big_idx, dense_cnt, kcnt, tile_cnt;   /* dense merge of long documents */
     DevBuf df_local, df_global, present, idf_vals;
+    uint64_t idf_full_n = 0;   /* idf_vals holds log(N/df) for df = 0..N of this N (0: not) */
     DevBuf dkey0, dkey1, dseq0, dseq1, npairs_ord, out_off, doc_meta;
     DevBuf out_term, out_cnt, out_score, idf_rank, large_list;
     DevBuf x_mine, x_send, x_recv, x_recv2, x_seq0, x_seq1, x_head, x_grank, x_dfv, x_arena_buf;
@@ -734,24 +736,41 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
     const uint32_t N = ctx->run_N, V = ctx->run_V;
     const uint64_t cap = ctx->run_cap, R_total = ctx->run_R_total;
     unsigned long long* cnt = ctx->counters.as<unsigned long long>();
-    /* ---- idf LUT: log(N/df) on the host's libm for each distinct df (TFIDF.c:243) ----
-     * The distinct df values are listed on the device; their count K, the first
-     * IDF_SPEC of them and the pair total P come back in ONE host round trip together
-     * with the document-order stage below. */
+    /* ---- idf: log(N/df) on the host's libm (TFIDF.c:243) ----
+     * Up to IDF_FULL_MAX documents the host tabulates every possible value, df = 1..N,
+     * once per N (cached with the context and uploaded once): the device then reads
+     * idf[df] directly and the run needs no host round trip between DF and the score.
+     * Above it (c3-size N on one rank) the distinct df values are listed on the device and
+     * come back in one round trip with the pair total. */
     mark(ctx, S_IDF);
-    ENSURE(ctx->present, (Nt + 2) * 4);
-    HIPCHK(hipMemsetAsync(ctx->present.p, 0, (Nt + 2) * 4, s));
-    XCHK(launch_df_mark(ctx->df_global.as<uint32_t>(), V, ctx->present.as<uint32_t>(), s));
-    XCHK(scan_excl_u32(ctx->present.as<uint32_t>(), ctx->present.as<uint32_t>(), Nt + 1, ar, s));
-    uint32_t* vals_dev = (uint32_t*)ar.get((size_t)(Nt + 2) * 4);
-    if (!vals_dev) return TFIDF_E_CAPACITY;   /* checked by run_local: not reachable */
-    XCHK(launch_df_list(ctx->present.as<uint32_t>(), Nt + 1, vals_dev, s));
-    constexpr uint32_t IDF_SPEC = 16384;
-    const uint32_t spec = (uint32_t)((Nt + 1) < IDF_SPEC ? (Nt + 1) : IDF_SPEC);
-    std::vector<uint32_t> vals(spec);
+    const bool full_lut = Nt <= IDF_FULL_MAX;
     uint32_t K = 0;
-    HIPCHK(hipMemcpyAsync(&K, ctx->present.as<uint32_t>() + Nt + 1, 4, hipMemcpyDeviceToHost, s));
-    if (spec) HIPCHK(hipMemcpyAsync(vals.data(), vals_dev, (size_t)spec * 4, hipMemcpyDeviceToHost, s));
+    uint32_t* vals_dev = nullptr;
+    constexpr uint32_t IDF_SPEC = 16384;
+    std::vector<uint32_t> vals;
+    if (full_lut) {
+        if (ctx->idf_full_n != Nt) {
+            ENSURE(ctx->idf_vals, (size_t)(Nt + 1) * 8);
+            std::vector<double> lut(Nt + 1);
+            lut[0] = 0.0;   /* df >= 1 for every term that occurs */
+            for (uint64_t d = 1; d <= Nt; ++d) lut[d] = log(1.0 * (double)Nt / (double)d);
+            HIPCHK(hipMemcpy(ctx->idf_vals.p, lut.data(), (size_t)(Nt + 1) * 8, hipMemcpyHostToDevice));
+            ctx->idf_full_n = Nt;
+        }
+    } else {
+        ctx->idf_full_n = 0;   /* idf_vals is rewritten below */
+        ENSURE(ctx->present, (Nt + 2) * 4);
+        HIPCHK(hipMemsetAsync(ctx->present.p, 0, (Nt + 2) * 4, s));
+        XCHK(launch_df_mark(ctx->df_global.as<uint32_t>(), V, ctx->present.as<uint32_t>(), s));
+        XCHK(scan_excl_u32(ctx->present.as<uint32_t>(), ctx->present.as<uint32_t>(), Nt + 1, ar, s));
+        vals_dev = (uint32_t*)ar.get((size_t)(Nt + 2) * 4);
+        if (!vals_dev) return TFIDF_E_CAPACITY;   /* checked by run_local: not reachable */
+        XCHK(launch_df_list(ctx->present.as<uint32_t>(), Nt + 1, vals_dev, s));
+        const uint32_t spec = (uint32_t)((Nt + 1) < IDF_SPEC ? (Nt + 1) : IDF_SPEC);
+        vals.resize(spec);
+        HIPCHK(hipMemcpyAsync(&K, ctx->present.as<uint32_t>() + Nt + 1, 4, hipMemcpyDeviceToHost, s));
+        if (spec) HIPCHK(hipMemcpyAsync(vals.data(), vals_dev, (size_t)spec * 4, hipMemcpyDeviceToHost, s));
+    }
     /* ---- document order: per-position metadata and pair offsets ---- */
     mark(ctx, S_ORDER);
     ENSURE(ctx->npairs_ord, (size_t)N * 8 + 8);
@@ -762,23 +781,26 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
                             ctx->doc_size.as<uint32_t>(), ctx->doc_flags.as<uint8_t>(), N,
                             ctx->npairs_ord.as<uint64_t>(), ctx->doc_meta.as<uint4>(), s));
     XCHK(scan_excl_u64(ctx->npairs_ord.as<uint64_t>(), ctx->out_off.as<uint64_t>(), N, ar, s));
-    uint64_t P = 0;
-    HIPCHK(hipMemcpyAsync(&P, ctx->out_off.as<uint64_t>() + N, 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    if (K > spec) {
-        vals.resize(K);
-        HIPCHK(hipMemcpy(vals.data() + spec, vals_dev + spec, (size_t)(K - spec) * 4, hipMemcpyDeviceToHost));
+    if (!full_lut) {
+        HIPCHK(hipStreamSynchronize(s));
+        const uint32_t spec = (uint32_t)vals.size();
+        if (K > spec) {
+            vals.resize(K);
+            HIPCHK(hipMemcpy(vals.data() + spec, vals_dev + spec, (size_t)(K - spec) * 4, hipMemcpyDeviceToHost));
+        }
+        ENSURE(ctx->idf_vals, (size_t)K * 8 + 8);
+        std::vector<double> idf(K);
+        for (uint32_t k = 0; k < K; ++k) idf[k] = log(1.0 * (double)Nt / (double)vals[k]);
+        if (K) HIPCHK(hipMemcpyAsync(ctx->idf_vals.p, idf.data(), (size_t)K * 8, hipMemcpyHostToDevice, s));
     }
-    ENSURE(ctx->idf_vals, (size_t)K * 8 + 8);
-    std::vector<double> idf(K);
-    for (uint32_t k = 0; k < K; ++k) idf[k] = log(1.0 * (double)Nt / (double)vals[k]);
-    if (K) HIPCHK(hipMemcpyAsync(ctx->idf_vals.p, idf.data(), (size_t)K * 8, hipMemcpyHostToDevice, s));
-    ctx->npairs = P;
+    /* the output arrays are sized by the record bound (pairs <= records): the pair total P
+     * comes back with the final status word */
+    const uint64_t Pmax = R_total;
     /* ---- score + per-document term order ---- */
     mark(ctx, S_SCORE);
-    ENSURE(ctx->out_term, P * 4 + 4);
-    ENSURE(ctx->out_cnt, P * 4 + 4);
-    ENSURE(ctx->out_score, P * 8 + 8);
+    ENSURE(ctx->out_term, Pmax * 4 + 4);
+    ENSURE(ctx->out_cnt, Pmax * 4 + 4);
+    ENSURE(ctx->out_score, Pmax * 8 + 8);
     ENSURE(ctx->idf_rank, (size_t)V * 8 + 8);
     ENSURE(ctx->large_list, (size_t)N * 4 + 8);
     K5Args a{};
@@ -793,7 +815,7 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
     a.rec_cnt = ctx->rec_cnt.as<uint32_t>();
     a.rank_of_slot = ctx->rank_of_slot.as<uint32_t>();
     a.df_of_rank = ctx->df_global.as<uint32_t>();
-    a.idf_idx = ctx->present.as<uint32_t>();
+    a.idf_idx = full_lut ? nullptr : ctx->present.as<uint32_t>();   /* null: idf indexed by df */
     a.idf = ctx->idf_vals.as<double>();
     a.idf_rank = ctx->idf_rank.as<double>();
     a.large_list = ctx->large_list.as<uint32_t>() + 1;
@@ -810,8 +832,11 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
     XCHK(launch_score_order(a, s, ctx->stream2, ctx->ev_fork, ctx->ev_order));
     mark(ctx, S_NSTAGES);
     uint32_t st_end = 0;
+    uint64_t P = 0;
     HIPCHK(hipMemcpyAsync(&st_end, cnt + 3, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&P, ctx->out_off.as<uint64_t>() + N, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    ctx->npairs = P;
     if (st_end & ST_BOUNDS) {
         fprintf(stderr, "tfidf: internal bounds check tripped (status 0x%x)\n", st_end);
         return TFIDF_E_STATE;

@@ -907,7 +907,7 @@ constexpr uint32_t K5L_GROUP_MAX = 32; /* k_score_large: larger buckets (skewed 
 __global__ void k_idf_of_rank(const uint32_t* __restrict__ df_of_rank, const uint32_t* __restrict__ idf_idx,
                               const double* __restrict__ idf, uint32_t V, double* __restrict__ out) {
     uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r < V) out[r] = idf[idf_idx[df_of_rank[r]]];
+    if (r < V) out[r] = idf_idx ? idf[idf_idx[df_of_rank[r]]] : idf[df_of_rank[r]];   /* null: table over all df */
 }
 
 /* The output is 16 bytes per pair (term rank, count, score): the document, docSize and
