@@ -191,3 +191,50 @@ def split_jobs(stdout: bytes):
         elif line and cur is not None:
             cur.append(line)
     return b"".join(x + b"\n" for x in sorted(tf)), b"".join(x + b"\n" for x in sorted(idf))
+
+
+def test_c3_sharded_over_8_equals_single_rank_oracle():
+    """BASELINE config 3's shape (Zipf V = 5e4, ~4 KB documents) sharded over 8 ranks as the
+    8-GPU run shards it (byte-balanced, docN@-ordered), at 5000 documents: the 8 shards'
+    texts concatenated are the single-rank oracle's output.txt byte for byte."""
+    K = 8
+    shards = _shards("c3", 0.0005, K)
+    ora = _full("c3", 0.0005)
+    texts, res, infos = _run_group(shards, K)
+    assert b"".join(texts) == ora["output_txt"]
+    assert_same_result(_concat(res), ora)
+    assert all(i["nterms_global"] == ora["nterms"] for i in infos)
+
+
+def test_c3_sharded_over_8_properties():
+    """Config 3 at 1e5 documents (~400 MB) over 8 shards, device-generated: the rank-order
+    concatenation obeys the size-independent properties of the single-rank path — counts
+    sum to the tokens, per-document sums = docSize, global DF = pairs per term across all
+    shards, strict strcmp order across shard boundaries, scores recomputed with the global
+    N (<= 1e-12 relative)."""
+    K = 8
+    with tfidf_abi.Group(K, devices=[0] * K) as g:
+        plans = [tfidf_configs.plan("c3", scale=0.01, rank=r, nranks=K) for r in range(K)]
+        corpora = [e.synth_device(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"], p["ndocs_total"])
+                   for e, p in zip(g.ranks, plans)]
+        g.run(corpora)
+        infos = [e.info() for e in g.ranks]
+        res = [e.fetch() for e in g.ranks]
+    ntok = sum(int(p["ntok"].sum()) for p in plans)
+    assert sum(i["ntokens"] for i in infos) == ntok
+    cat = _concat(res)
+    cnt = cat["count"].astype(np.int64)
+    assert cnt.sum() == ntok and cat["npairs"] > 1_000_000
+    starts = np.flatnonzero(np.r_[True, cat["doc"][1:] != cat["doc"][:-1]])
+    assert np.array_equal(np.add.reduceat(cnt, starts), cat["docsize"][starts].astype(np.int64))
+    # global DF: pairs per term over every shard
+    dfc = np.bincount(cat["term"], minlength=len(cat["terms"]))
+    assert np.array_equal(cat["df"], dfc[cat["term"]])
+    assert all(i["nterms_global"] == len(cat["terms"]) for i in infos)
+    # strict order across the concatenation: (document name key, term bytes)
+    dk = tfidf_configs.doc_name_key(cat["doc"]).astype(np.uint64)
+    tr = cat["term"]   # ids of the sorted union: byte order of the terms
+    assert np.all((dk[1:] > dk[:-1]) | ((dk[1:] == dk[:-1]) & (tr[1:] > tr[:-1])))
+    N = plans[0]["ndocs_total"]
+    ref = (cnt / cat["docsize"].astype(np.float64)) * np.log(N / cat["df"].astype(np.float64))
+    np.testing.assert_allclose(cat["score"], ref, rtol=1e-12, atol=1e-300)
