@@ -900,15 +900,6 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, cons
                             const uint32_t t = t0 + lane;
                             const bool val = t < cnt;
                             const uint32_t e = val ? tl[t] : 0u;
-#ifdef K1S_SALU_PAD
-                            {   /* timing only: K1S_SALU_PAD extra scalar adds per round (is the
-                                 * CU's scalar issue a co-bottleneck?) */
-                                uint32_t dz = t0;
-#pragma unroll
-                                for (int z = 0; z < K1S_SALU_PAD; ++z) asm volatile("s_add_u32 %0, %0, 1" : "+s"(dz));
-                                asm volatile("" ::"s"(dz));
-                            }
-#endif
                             const uint32_t pos = e & 1023u, len = (e >> 10) & 31u;
                             q.rel = e >> 16;
                             q.ap = sb - 16ull + pos;
