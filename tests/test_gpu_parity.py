@@ -402,3 +402,19 @@ def test_many_long_terms_sharing_prefixes(engine):
             docs.append(b" ".join(cur) + b"\n")
             cur = []
     check_vs_oracle(engine, *docs_to_arrays(docs))
+
+
+def test_df_histogram_bin_overflow(engine):
+    """17 M one-word documents: every record is the same term, the case where a u16 LDS bin
+    of the DF histogram would wrap if a workgroup took more than 65535 records (k_df_hist_lds
+    caps its share there; a one-workgroup-per-CU split with wrap correction measured slower);
+    df is N for every pair, each score log(N/N) = 0 (TFIDF.c:243-244)."""
+    N = 17_000_000
+    data = np.frombuffer(b"a\n" * N, dtype=np.uint8).copy()
+    off = (np.arange(N + 1, dtype=np.uint64) * 2)
+    engine.run_host(data, off)
+    info = engine.info()
+    assert info["npairs"] == N and info["nterms"] == 1
+    r = engine.fetch()
+    assert np.all(r["df"] == N) and np.all(r["count"] == 1) and np.all(r["docsize"] == 1)
+    assert np.all(r["score"] == 0.0)
