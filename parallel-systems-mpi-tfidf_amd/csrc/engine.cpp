@@ -105,6 +105,7 @@ struct tfidf_ctx {
 #define VOCAB_LOW_LOAD_CAP (1ull << 24)
 #define IDF_FULL_MAX (1ull << 24)   /* documents up to which the idf table covers every df */
     uint32_t vload_pct = 12;
+    uint32_t vload_big_pct = 45;   /* load limit of tables of VOCAB_LOW_LOAD_CAP slots and more */
     DevBuf rec_slot, rec_cnt;
     uint64_t rec_cap = 0;
     DevBuf part_doc, part_slot, part_cnt;
@@ -223,6 +224,11 @@ int tfidf_open(int device, tfidf_ctx** out) {
     if (kv) {
         uint64_t c = strtoull(kv, nullptr, 0);
         if (c >= 1024 && (c & (c - 1)) == 0) ctx->vcap = c;
+    }
+    const char* kb = getenv("TFIDF_VLOAD_BIG");
+    if (kb) {
+        uint32_t l = (uint32_t)strtoul(kb, nullptr, 0);
+        if (l >= 10 && l <= 90) ctx->vload_big_pct = l;
     }
     const char* kl = getenv("TFIDF_VLOAD");
     if (kl) {
@@ -582,11 +588,12 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     ctx->V = V;
     /* keep probes short: the low load pays while the table is L2/MALL-sized (<= 16M slots,
      * 256 MB of keys); past that every probe is an HBM access anyway, so up to 45 % */
-    if ((uint64_t)V * 100 > cap * (cap < VOCAB_LOW_LOAD_CAP ? ctx->vload_pct : 45u)) {
+    if ((uint64_t)V * 100 > cap * (cap < VOCAB_LOW_LOAD_CAP ? ctx->vload_pct : ctx->vload_big_pct)) {
         /* the smallest table within the load limit: a table twice too large costs its
          * clear and a sparser compaction pass (c4: 64M -> 32M slots, vocabulary stage
          * 3.1 -> 2.65 ms) */
-        while ((uint64_t)V * 100 > ctx->vcap * (ctx->vcap < VOCAB_LOW_LOAD_CAP ? ctx->vload_pct : 45u)) ctx->vcap *= 2;
+        while ((uint64_t)V * 100 > ctx->vcap * (ctx->vcap < VOCAB_LOW_LOAD_CAP ? ctx->vload_pct : ctx->vload_big_pct))
+            ctx->vcap *= 2;
         if (ctx->vcap > K1_VS_MAX_CAP && cap < K1_VS_MAX_CAP) ctx->vcap = K1_VS_MAX_CAP;
         if (ctx->vcap != cap) return 1;
     }
