@@ -112,6 +112,10 @@ struct tfidf_ctx {
     uint64_t part_cap = 0;
     DevBuf doc_recoff, doc_npairs, doc_size, doc_flags;
     DevBuf counters;
+    /* pinned host words for the per-run device-to-host reads (corpus bounds, K1 counters,
+     * final status): asynchronous copies on the stream and one synchronisation each, instead
+     * of pageable or synchronous copies (two round trips per run saved) */
+    uint64_t* hpin = nullptr;
     DevBuf dense, vslot, skey0, skey1, seq0, seq1, rank_of_slot, slot_of_rank, rank16;
     DevBuf pkey0, pkey1, pseq0, pseq1, phead;
     DevBuf big_list, big_idx, dense_cnt, kcnt, tile_cnt;   /* dense merge of long documents */
@@ -242,6 +246,7 @@ int tfidf_open(int device, tfidf_ctx** out) {
     for (int i = 0; i <= S_NSTAGES; ++i) HIPCHK(hipEventCreate(&ctx->ev[i]));
     if (arena_reset(ctx, 64ull << 20) != 0) { delete ctx; return TFIDF_E_NOMEM; }
     if (ctx->counters.ensure(256) != 0) { delete ctx; return TFIDF_E_NOMEM; }
+    if (hipHostMalloc((void**)&ctx->hpin, 256, hipHostMallocDefault) != hipSuccess) { delete ctx; return TFIDF_E_NOMEM; }
     *out = ctx;
     return TFIDF_OK;
 }
@@ -272,6 +277,7 @@ void tfidf_close(tfidf_ctx* ctx) {
                       &ctx->tile_cnt};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i <= S_NSTAGES; ++i) (void)hipEventDestroy(ctx->ev[i]);
+    if (ctx->hpin) (void)hipHostFree(ctx->hpin);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -538,11 +544,14 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     ENSURE(ctx->dense, (cap + 1) * 4);
     LCHK(launch_vocab_flags(vd, cap, ctx->dense.as<uint32_t>(), s));
     LCHK(scan_excl_u32(ctx->dense.as<uint32_t>(), ctx->dense.as<uint32_t>(), cap, ar, s));
-    uint32_t V = 0;
-    unsigned long long hc[8];
-    HIPCHK(hipMemcpyAsync(hc, cnt, sizeof hc, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&V, ctx->dense.as<uint32_t>() + cap, 4, hipMemcpyDeviceToHost, s));
+    uint64_t* hp = ctx->hpin;
+    HIPCHK(hipMemcpyAsync(hp, cnt, 64, hipMemcpyDeviceToHost, s));
+    hp[8] = 0;
+    HIPCHK(hipMemcpyAsync(hp + 8, ctx->dense.as<uint32_t>() + cap, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    const uint32_t V = (uint32_t)hp[8];
+    unsigned long long hc[8];
+    for (int i = 0; i < 8; ++i) hc[i] = hp[i];
     const uint64_t R_main = hc[0], Q = hc[1], nbig = hc[6];
     const uint32_t st = (uint32_t)hc[3];
     ctx->ntokens = hc[2];
@@ -664,9 +673,11 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
                                    Q, ctx->big_idx.as<uint32_t>(), ctx->rank_of_slot.as<uint32_t>(), V,
                                    ctx->dense_cnt.as<uint32_t>(), ctx->pkey0.as<uint64_t>(), ctx->pseq0.as<uint32_t>(),
                                    ctx->kcnt.as<uint32_t>(), nkeep, s));
-            uint32_t qk = 0;   /* the sort needs its size on the host: one round trip, dense runs only */
-            HIPCHK(hipMemcpyAsync(&qk, nkeep, 4, hipMemcpyDeviceToHost, s));
+            /* the sort needs its size on the host: one round trip, dense runs only */
+            ctx->hpin[9] = 0;
+            HIPCHK(hipMemcpyAsync(ctx->hpin + 9, nkeep, 4, hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
+            const uint32_t qk = (uint32_t)ctx->hpin[9];
             Qs = qk;
             scnt = ctx->kcnt.as<uint32_t>();
         } else {
@@ -838,11 +849,12 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
     a.out_score = ctx->out_score.as<double>();
     XCHK(launch_score_order(a, s, ctx->stream2, ctx->ev_fork, ctx->ev_order));
     mark(ctx, S_NSTAGES);
-    uint32_t st_end = 0;
-    uint64_t P = 0;
-    HIPCHK(hipMemcpyAsync(&st_end, cnt + 3, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&P, ctx->out_off.as<uint64_t>() + N, 8, hipMemcpyDeviceToHost, s));
+    ctx->hpin[10] = 0;
+    HIPCHK(hipMemcpyAsync(ctx->hpin + 10, cnt + 3, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(ctx->hpin + 11, ctx->out_off.as<uint64_t>() + N, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    const uint32_t st_end = (uint32_t)ctx->hpin[10];
+    const uint64_t P = ctx->hpin[11];
     ctx->npairs = P;
     if (st_end & ST_BOUNDS) {
         fprintf(stderr, "tfidf: internal bounds check tripped (status 0x%x)\n", st_end);
@@ -887,9 +899,12 @@ static int run_prepare(tfidf_ctx* ctx, const tfidf_corpus* in, CorpusDev& c, con
         c.doc_off = in->doc_off;
         dev_ids = in->doc_ids;
         uint64_t e[2] = {0, 0};
-        if (N) {
-            HIPCHK(hipMemcpy(&e[0], in->doc_off, 8, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(&e[1], in->doc_off + N, 8, hipMemcpyDeviceToHost));
+        if (N) {   /* one round trip on the run's stream (after any work already queued on it) */
+            HIPCHK(hipMemcpyAsync(ctx->hpin + 12, in->doc_off, 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(ctx->hpin + 13, in->doc_off + N, 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            e[0] = ctx->hpin[12];
+            e[1] = ctx->hpin[13];
         }
         lo = e[0]; hi = e[1];
     } else {
