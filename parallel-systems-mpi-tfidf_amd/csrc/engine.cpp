@@ -122,7 +122,7 @@ struct tfidf_ctx {
     DevBuf df_local, df_global, present, idf_vals;
     uint64_t idf_full_n = 0;   /* idf_vals holds log(N/df) for df = 0..N of this N (0: not) */
     DevBuf dkey0, dkey1, dseq0, dseq1, npairs_ord, out_off, doc_meta;
-    DevBuf out_term, out_cnt, out_score, idf_rank, large_list;
+    DevBuf out_term, out_cnt, out_score, idf_rank, large_list, split_tasks, cls_off;
     DevBuf x_mine, x_send, x_recv, x_recv2, x_seq0, x_seq1, x_head, x_grank, x_dfv, x_arena_buf;
     Arena x_arena;          /* scratch of the exchange's sort/scan, sized before the exchange */
     /* sizes the local part of a run hands to the exchange and the stages after it */
@@ -271,7 +271,7 @@ void tfidf_close(tfidf_ctx* ctx) {
                       &ctx->present, &ctx->idf_vals, &ctx->dkey0, &ctx->dkey1, &ctx->dseq0, &ctx->dseq1,
                       &ctx->npairs_ord, &ctx->out_off, &ctx->doc_meta, &ctx->t_key, &ctx->t_len, &ctx->doc_tbytes,
                       &ctx->doc_toff, &ctx->text, &ctx->out_term, &ctx->out_cnt,
-                      &ctx->out_score, &ctx->idf_rank, &ctx->large_list, &ctx->x_mine, &ctx->x_send, &ctx->x_recv,
+                      &ctx->out_score, &ctx->idf_rank, &ctx->large_list, &ctx->split_tasks, &ctx->cls_off, &ctx->x_mine, &ctx->x_send, &ctx->x_recv,
                       &ctx->x_recv2, &ctx->x_seq0, &ctx->x_seq1, &ctx->x_head, &ctx->x_grank, &ctx->x_dfv,
                       &ctx->x_arena_buf, &ctx->stamps, &ctx->big_list, &ctx->big_idx, &ctx->dense_cnt, &ctx->kcnt,
                       &ctx->tile_cnt};
@@ -737,7 +737,8 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     ctx->run_R_total = R_total;
     ctx->run_merged = merged_count;
     /* the stages after the exchange take their scratch from what is left of the arena */
-    const size_t post_need = scan_scratch(Nt + 1) + (size_t)(Nt + 2) * 4 + 512 + scan_scratch(N);
+    const size_t post_need = scan_scratch(Nt + 1) + (size_t)(Nt + 2) * 4 + 512 + scan_scratch(N) +
+                             scan_scratch(3ull * ((N + 255) / 256) + 1);   /* K5's document classes */
     if (ar.cap - ar.used < post_need) {
         ar.peak = ar.used + post_need > ar.peak ? ar.used + post_need : ar.peak;
         return 1;
@@ -820,7 +821,7 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
     ENSURE(ctx->out_cnt, Pmax * 4 + 4);
     ENSURE(ctx->out_score, Pmax * 8 + 8);
     ENSURE(ctx->idf_rank, (size_t)V * 8 + 8);
-    ENSURE(ctx->large_list, (size_t)N * 4 + 8);
+    ENSURE(ctx->large_list, (size_t)N * 8 + 16);   /* wide ranks: handed-off documents; then the K5 class list */
     K5Args a{};
     a.order = ctx->order;
     a.meta = ctx->doc_meta.as<uint4>();
@@ -838,6 +839,17 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
     a.idf_rank = ctx->idf_rank.as<double>();
     a.large_list = ctx->large_list.as<uint32_t>() + 1;
     a.large_count = ctx->large_list.as<uint32_t>();
+    a.cls_nblk = (N + 255) / 256;
+    a.cls_list = ctx->large_list.as<uint32_t>() + N + 2;
+    ENSURE(ctx->cls_off, ((size_t)3 * a.cls_nblk + 8) * 4);
+    a.cls_off = ctx->cls_off.as<uint32_t>();
+    {   /* presorted documents over 4096 pairs are emitted in 4096-pair chunks: <= 2 R / 4096 tasks */
+        const uint64_t cap_t = 2 * R_total / 4096 + 64;
+        ENSURE(ctx->split_tasks, cap_t * 8 + 8);
+        a.split_count = ctx->split_tasks.as<uint32_t>();
+        a.split_tasks = ctx->split_tasks.as<uint2>() + 1;
+        a.split_cap = (uint32_t)(cap_t < 0xFFFFFFFFull ? cap_t : 0xFFFFFFFFull);
+    }
     a.ndocs = N;
     a.nterms = V;
     a.rank_bits = V > 1 ? 32u - (uint32_t)__builtin_clz(V - 1) : 1u;
@@ -847,7 +859,7 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
     a.out_term = ctx->out_term.as<uint32_t>();
     a.out_cnt = ctx->out_cnt.as<uint32_t>();
     a.out_score = ctx->out_score.as<double>();
-    XCHK(launch_score_order(a, s, ctx->stream2, ctx->ev_fork, ctx->ev_order));
+    XCHK(launch_score_order(a, ar, s, ctx->stream2, ctx->ev_fork, ctx->ev_order));
     mark(ctx, S_NSTAGES);
     ctx->hpin[10] = 0;
     HIPCHK(hipMemcpyAsync(ctx->hpin + 10, cnt + 3, 4, hipMemcpyDeviceToHost, s));

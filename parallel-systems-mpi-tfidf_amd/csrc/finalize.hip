@@ -889,6 +889,8 @@ int launch_gather_meta(const uint32_t* order, const uint32_t* doc_npairs, const 
 
 constexpr int K5_MAX = K5_MAX_PAIRS;
 constexpr uint32_t K5_SMALL = 64;     /* one wave, bitonic across the lanes */
+constexpr uint32_t K5_SMALL_DOC = 128; /* documents up to this many pairs: k_score_small */
+constexpr uint32_t K5_PS_SPLIT = 4096; /* presorted documents over this many pairs: chunk tasks */
 constexpr uint32_t K5_WAVE = 1024;    /* one wave, LDS radix sort of packed (rank, index) keys */
 constexpr uint32_t K5_IDX_BITS = 11;  /* index bits of a packed key (n <= 2048) */
 constexpr int K5_BATCH = 8;           /* gathers per lane in flight together */
@@ -1051,13 +1053,26 @@ __global__ __launch_bounds__(NT, K5_WPS) void k_score_wave(K5Args a) {
     uint32_t* buf0 = kb[w][0];
     uint32_t* buf1 = kb[w][1];
     uint32_t* h = hist[w];
-    uint32_t i = blockIdx.x * (NT / 64) + w;
-    uint4 m_cur = i < a.ndocs ? gload(a.meta + (i)) : make_uint4(0, 0, 0, 0);
-    uint4 m_nxt = i + stride < a.ndocs ? gload(a.meta + (i + stride)) : make_uint4(0, 0, 0, 0);
-    uint64_t ob_cur = i < a.ndocs ? G(a.out_off)[i] : 0ull;
+    /* the positions this kernel scores: its segment of the class list (k_k5_classify), or
+     * every position (wide ranks) */
+    const uint32_t* L = nullptr;
+    uint32_t lcount = a.ndocs;
+    if (!WIDE && a.cls_list) {
+        const uint32_t lo = G(a.cls_off)[a.cls_nblk];
+        L = a.cls_list + lo;
+        lcount = G(a.cls_off)[2 * a.cls_nblk] - lo;
+    }
+    auto pos_of = [&](uint32_t li) -> uint32_t { return L ? G(L)[li] : li; };
+    uint32_t li = blockIdx.x * (NT / 64) + w;
+    uint32_t i_cur = li < lcount ? pos_of(li) : 0u;
+    uint32_t i_nxt = li + stride < lcount ? pos_of(li + stride) : 0u;
+    uint4 m_cur = li < lcount ? gload(a.meta + (i_cur)) : make_uint4(0, 0, 0, 0);
+    uint4 m_nxt = li + stride < lcount ? gload(a.meta + (i_nxt)) : make_uint4(0, 0, 0, 0);
+    uint64_t ob_cur = li < lcount ? G(a.out_off)[i_cur] : 0ull;
     uint32_t s_cur[K5_PF], c_cur[K5_PF];
     k5_prefetch(a, m_cur, lane, s_cur, c_cur);
-    for (; i < a.ndocs; i += stride) {
+    for (; li < lcount; li += stride) {
+        const uint32_t i = i_cur;
         const uint4 mc = m_cur;
         const uint64_t ob = ob_cur;
         const uint32_t n = mc.z & 0x3FFFFFFFu;
@@ -1094,10 +1109,12 @@ __global__ __launch_bounds__(NT, K5_WPS) void k_score_wave(K5Args a) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         {
-            const uint32_t inx = i + stride;
+            const uint32_t inx = li + stride;
             m_cur = m_nxt;
-            ob_cur = inx < a.ndocs ? G(a.out_off)[inx] : 0ull;
-            m_nxt = inx + stride < a.ndocs ? gload(a.meta + (inx + stride)) : make_uint4(0, 0, 0, 0);
+            i_cur = i_nxt;
+            ob_cur = inx < lcount ? G(a.out_off)[i_cur] : 0ull;
+            i_nxt = inx + stride < lcount ? pos_of(inx + stride) : 0u;
+            m_nxt = inx + stride < lcount ? gload(a.meta + (i_nxt)) : make_uint4(0, 0, 0, 0);
             k5_prefetch(a, m_cur, lane, s_cur, c_cur);
         }
         if (n == 0) continue;
@@ -1352,9 +1369,17 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
     __shared__ uint32_t wsum[NT / 64];
     __shared__ uint32_t bmax;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint32_t nlarge = *a.large_count;
+    const uint32_t* LL = a.large_list;
+    uint32_t nlarge;
+    if (a.cls_list) {   /* its segment of the class list */
+        const uint32_t lo = G(a.cls_off)[2 * a.cls_nblk];
+        LL = a.cls_list + lo;
+        nlarge = G(a.cls_off)[3 * a.cls_nblk] - lo;
+    } else {   /* handed off by the wide wave kernel */
+        nlarge = *a.large_count;
+    }
     for (uint32_t li = blockIdx.x; li < nlarge; li += gridDim.x) {
-    const uint32_t i = G(a.large_list)[li];
+    const uint32_t i = G(LL)[li];
     const uint32_t d = G(a.order)[i];
     const uint32_t n = G(a.doc_npairs)[d];
     const bool presorted = (G(a.doc_flags)[d] & DF_PRESORTED) != 0;
@@ -1463,32 +1488,160 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
     __syncthreads(); /* the next document reuses the LDS buffers */
     }
 }
-/* documents (output positions) the wave kernel leaves to k_score_large, listed before
- * either runs so that k_score_large can start beside the wave kernel */
-__global__ void k_large_list(K5Args a) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    bool big = false;
-    if (i < a.ndocs) {
-        const uint4 m = gload(a.meta + (i));
-        const uint32_t n = m.z & 0x3FFFFFFFu;
-        big = n != 0u && !k5_by_wave(a, n, ((m.z >> 30) & DF_PRESORTED) != 0);
+/* The document classes of K5 (non-wide ranks): 1 small (<= K5_SMALL_DOC pairs:
+ * k_score_small), 2 the wave kernel's, 3 k_score_large's; 0 none (no pairs, or a presorted
+ * run emitted by k_emit_split's chunk tasks, which k_k5_classify lists).  A per-block count,
+ * a scan and a scatter give class-contiguous lists without a device-wide counter (c5: 1e6
+ * small documents appended through one atomic counter took 0.18 ms), listed before any
+ * scoring kernel runs so that k_score_large can start beside the wave kernel. */
+__device__ __forceinline__ uint32_t k5_class(const K5Args& a, uint32_t i) {
+    if (i >= a.ndocs) return 0u;
+    const uint4 m = gload(a.meta + (i));
+    const uint32_t n = m.z & 0x3FFFFFFFu;
+    const bool presorted = ((m.z >> 30) & DF_PRESORTED) != 0;
+    if (n == 0u) return 0u;
+    if (n <= K5_SMALL_DOC) return 1u;
+    if (k5_by_wave(a, n, presorted)) return 2u;
+    if (presorted && n > K5_PS_SPLIT && a.split_count) return 4u;
+    return 3u;
+}
+__global__ __launch_bounds__(256) void k_k5_classify(K5Args a) {
+    __shared__ uint32_t c3[3];
+    if (threadIdx.x < 3) c3[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t c = k5_class(a, i);
+    if (c >= 1u && c <= 3u) atomicAdd(&c3[c - 1u], 1u);
+    if (c == 4u) {
+        /* a presorted run (a merged long document: c5's 100 MB ones) needs no sort: its
+         * emission is split into 4096-pair tasks every workgroup can take (few: atomics) */
+        const uint32_t n = gload(a.meta + (i)).z & 0x3FFFFFFFu;
+        const uint32_t nt = (n + K5_PS_SPLIT - 1) / K5_PS_SPLIT;
+        const uint32_t b = atomicAdd(a.split_count, nt);
+        for (uint32_t k = 0; k < nt; ++k) {
+            if (b + k < a.split_cap) a.split_tasks[b + k] = make_uint2(i, k);
+            else atomicOr(a.status, ST_BOUNDS);
+        }
     }
-    const uint64_t bm = __ballot(big);
-    if (!bm) return;
-    const uint32_t lane = threadIdx.x & 63, leader = (uint32_t)__builtin_ctzll(bm);
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(a.large_count, (uint32_t)__popcll(bm));
-    base = (uint32_t)__shfl(base, (int)leader);
-    if (big) G(a.large_list)[base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull))] = i;
+    __syncthreads();
+    if (threadIdx.x < 3) a.cls_off[threadIdx.x * a.cls_nblk + blockIdx.x] = c3[threadIdx.x];
+    if (blockIdx.x == 0 && threadIdx.x == 3) a.cls_off[3 * a.cls_nblk] = 0u;   /* the scan's total */
+}
+__global__ __launch_bounds__(256) void k_k5_scatter(K5Args a) {
+    __shared__ uint32_t wc[4][3];
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t c = k5_class(a, i);
+    uint32_t rk = 0;
+#pragma unroll
+    for (uint32_t k = 1; k <= 3; ++k) {
+        const uint64_t m = __ballot(c == k);
+        if (lane == 0) wc[w][k - 1] = (uint32_t)__popcll(m);
+        if (c == k) rk = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    }
+    __syncthreads();
+    if (c >= 1u && c <= 3u) {
+        uint32_t base = G(a.cls_off)[(c - 1) * a.cls_nblk + blockIdx.x];
+        for (uint32_t q = 0; q < w; ++q) base += wc[q][c - 1];
+        a.cls_list[base + rk] = i;
+    }
+}
+
+/* Documents of <= K5_SMALL_DOC pairs (c5: 1e6 documents of ~50 pairs), listed by
+ * k_k5_classify: one wave per document over the list, 0.5 KB of LDS per wave and few
+ * registers, so ~3x the documents of the wave kernel are in flight per CU — the path is a
+ * chain of dependent round trips per document (metadata -> records -> idf), and latency
+ * is hidden by the number of documents in flight.  Position of a pair = the number of
+ * smaller ranks in its document (ranks are distinct within a document; presorted runs
+ * keep their order).  TFIDF.c:202,243-245,273. */
+constexpr int K5S_WG = 4;   /* waves per workgroup */
+__global__ __launch_bounds__(256, 8) void k_score_small(K5Args a) {
+    __shared__ __attribute__((aligned(16))) uint32_t kb[K5S_WG][K5_SMALL_DOC + 4];
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t* buf = kb[w];
+    const uint32_t nsmall = G(a.cls_off)[a.cls_nblk];   /* the small segment starts the class list */
+    const uint32_t stride = gridDim.x * K5S_WG;
+    constexpr int Q = K5_SMALL_DOC / 64;
+    for (uint32_t li = blockIdx.x * K5S_WG + w; li < nsmall; li += stride) {
+        const uint32_t i = G(a.cls_list)[li];
+        const uint4 m = gload(a.meta + i);
+        const uint32_t n = m.z & 0x3FFFFFFFu;
+        const bool presorted = ((m.z >> 30) & DF_PRESORTED) != 0;
+        const uint64_t rb = ((uint64_t)m.y << 32) | m.x;
+        const uint64_t ob = G(a.out_off)[i];
+        const double ds = (double)m.w;
+        if (n > K5_SMALL_DOC || rb + n > a.rec_total) { if (lane == 0) atomicOr(a.status, ST_BOUNDS); continue; }
+        uint32_t r[Q], c[Q], pos[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const uint32_t j = 64u * q + lane;
+            const bool v = j < n;
+            r[q] = v ? k5_rank(a, G(a.rec_slot)[rb + j]) : 0xFFFFFFFFu;
+            c[q] = v ? G(a.rec_cnt)[rb + j] : 0u;
+            pos[q] = j;
+        }
+        if (!presorted) {
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const uint32_t j = 64u * q + lane;
+                if (j < n) buf[j] = r[q];
+            }
+            const uint32_t n4 = (n + 3u) & ~3u;
+            if (lane < 4u && n + lane < n4) buf[n + lane] = 0xFFFFFFFFu;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int q = 0; q < Q; ++q) pos[q] = 0u;
+            const uint4* k4p = reinterpret_cast<const uint4*>(buf);
+            for (uint32_t i4 = 0; i4 < n4 / 4u; ++i4) {
+                const uint4 k4 = k4p[i4];
+#pragma unroll
+                for (int q = 0; q < Q; ++q)
+                    pos[q] += (k4.x < r[q] ? 1u : 0u) + (k4.y < r[q] ? 1u : 0u) + (k4.z < r[q] ? 1u : 0u) +
+                              (k4.w < r[q] ? 1u : 0u);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        double idf[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) idf[q] = (64u * q + lane < n) ? G(a.idf_rank)[r[q]] : 0.0;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            if (64u * q + lane < n) {
+                const uint64_t o = ob + pos[q];
+                G(a.out_term)[o] = r[q];
+                G(a.out_cnt)[o] = c[q];
+                G(a.out_score)[o] = ((double)c[q] / ds) * idf[q];   /* TFIDF.c:202,243-244 */
+            }
+        }
+    }
+}
+/* the chunk tasks of long presorted documents: one workgroup per 4096-pair chunk */
+__global__ __launch_bounds__(256) void k_emit_split(K5Args a) {
+    const uint32_t nt = *a.split_count < a.split_cap ? *a.split_count : a.split_cap;
+    for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+        const uint2 tk = a.split_tasks[t];
+        const uint4 m = gload(a.meta + tk.x);
+        const uint32_t n = m.z & 0x3FFFFFFFu;
+        const uint64_t rb = ((uint64_t)m.y << 32) | m.x;
+        const uint64_t ob = G(a.out_off)[tk.x];
+        const double ds = (double)m.w;
+        if (rb + n > a.rec_total) { if (threadIdx.x == 0) atomicOr(a.status, ST_BOUNDS); continue; }
+        const uint32_t j1 = (tk.y + 1) * K5_PS_SPLIT < n ? (tk.y + 1) * K5_PS_SPLIT : n;
+        for (uint32_t j = tk.y * K5_PS_SPLIT + threadIdx.x; j < j1; j += 256)
+            k5_emit(a, ob + j, ds, k5_rank(a, G(a.rec_slot)[rb + j]), G(a.rec_cnt)[rb + j]);
+    }
 }
 static void launch_score_large(const K5Args& a, uint32_t grid, hipStream_t s) {
     static_assert(K5_MAX % 2 == 0 && K5_MAX / 2 >= 1024, "k_score_large instances");
     k_score_large<(uint32_t)K5_MAX / 2, 10><<<grid, NT, 0, s>>>(a);
     k_score_large<(uint32_t)K5_MAX, 11><<<grid, NT, 0, s>>>(a);
 }
-int launch_score_order(const K5Args& a, hipStream_t s, hipStream_t s2, hipEvent_t ev_fork, hipEvent_t ev_join) {
+int launch_score_order(const K5Args& a, Arena& ar, hipStream_t s, hipStream_t s2, hipEvent_t ev_fork,
+                       hipEvent_t ev_join) {
     if (!a.ndocs) return 0;
     if (hipMemsetAsync(a.large_count, 0, 4, s) != hipSuccess) return -1;
+    if (a.split_count && hipMemsetAsync(a.split_count, 0, 4, s) != hipSuccess) return -1;
     k_idf_of_rank<<<grid_for(a.nterms ? a.nterms : 1), NT, 0, s>>>(a.df_of_rank, a.idf_idx, a.idf, a.nterms,
                                                                   a.idf_rank);
     static int ncu = 0;
@@ -1502,11 +1655,18 @@ int launch_score_order(const K5Args& a, hipStream_t s, hipStream_t s2, hipEvent_
     const uint32_t wg = wg_need < (uint32_t)ncu * 4u ? wg_need : (uint32_t)ncu * 4u; /* 36 KB LDS: 4 per CU */
     const uint32_t grid = a.ndocs < 2048u ? a.ndocs : 2048u; /* persistent over the handed-off list */
     if (a.rank_bits + K5_IDX_BITS > 32) {   /* skewed wide documents are handed off during the run */
-        k_score_wave<true><<<wg, NT, 0, s>>>(a);
-        launch_score_large(a, grid, s);
+        K5Args b = a;
+        b.cls_list = nullptr;   /* the wide instance takes every position (and hands off on the fly) */
+        b.split_count = nullptr;
+        k_score_wave<true><<<wg, NT, 0, s>>>(b);
+        launch_score_large(b, grid, s);
         return ok();
     }
-    k_large_list<<<grid_for(a.ndocs), NT, 0, s>>>(a);
+    if (!a.cls_list || !a.cls_off) return -1;
+    k_k5_classify<<<a.cls_nblk, 256, 0, s>>>(a);
+    if (scan_excl_u32(a.cls_off, a.cls_off, 3ull * a.cls_nblk + 1, ar, s)) return -1;
+    k_k5_scatter<<<a.cls_nblk, 256, 0, s>>>(a);
+    k_score_small<<<(unsigned)ncu * 8u, 256, 0, s>>>(a);
 #ifndef K5_SERIAL_LARGE
     if (s2 && ev_fork && ev_join) {
         /* the wave kernel first (its persistent grid takes the CUs), k_score_large on the
@@ -1514,6 +1674,7 @@ int launch_score_order(const K5Args& a, hipStream_t s, hipStream_t s2, hipEvent_
         if (hipEventRecord(ev_fork, s) != hipSuccess) return -1;
         k_score_wave<false><<<wg, NT, 0, s>>>(a);
         if (hipStreamWaitEvent(s2, ev_fork, 0) != hipSuccess) return -1;
+        if (a.split_count) k_emit_split<<<(unsigned)ncu * 4u, 256, 0, s2>>>(a);
         launch_score_large(a, grid, s2);
         if (hipEventRecord(ev_join, s2) != hipSuccess) return -1;
         if (hipStreamWaitEvent(s, ev_join, 0) != hipSuccess) return -1;
@@ -1521,6 +1682,7 @@ int launch_score_order(const K5Args& a, hipStream_t s, hipStream_t s2, hipEvent_
     }
 #endif
     k_score_wave<false><<<wg, NT, 0, s>>>(a);
+    if (a.split_count) k_emit_split<<<(unsigned)ncu * 4u, 256, 0, s>>>(a);
     launch_score_large(a, grid, s);
     return ok();
 }

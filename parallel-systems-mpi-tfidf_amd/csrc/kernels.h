@@ -173,6 +173,15 @@ struct K5Args {
     double* idf_rank;            /* [nterms] scratch: idf of each term rank */
     uint32_t* large_list;        /* [ndocs] scratch: output positions left to k_score_large */
     uint32_t* large_count;
+    uint32_t* cls_list;          /* [ndocs] scratch: output positions by kernel class — small documents
+                                    (k_score_small), then the wave kernel's, then k_score_large's;
+                                    null (wide ranks): the wave kernel takes every position */
+    uint32_t* cls_off;           /* [3 * cls_nblk + 1] scratch: per-block class counts, scanned: the
+                                    segments start at 0, [cls_nblk], [2 cls_nblk], end at [3 cls_nblk] */
+    uint32_t cls_nblk;
+    uint2* split_tasks;          /* (output position, chunk) of presorted documents over K5_PS_SPLIT pairs */
+    uint32_t* split_count;       /*   null: k_score_large emits them whole */
+    uint32_t split_cap;
     uint32_t ndocs;
     uint32_t nterms;
     uint32_t rank_bits;          /* bits of the largest term rank (radix passes) */
@@ -183,7 +192,8 @@ struct K5Args {
     uint32_t* out_cnt;           /*               wordCount */
     double* out_score;           /*               tf * idf */
 };
-int launch_score_order(const K5Args& a, hipStream_t s, hipStream_t s2, hipEvent_t ev_fork, hipEvent_t ev_join);
+int launch_score_order(const K5Args& a, Arena& ar, hipStream_t s, hipStream_t s2, hipEvent_t ev_fork,
+                       hipEvent_t ev_join);
 
 /* multi-GPU vocabulary agreement */
 int launch_keys_by_rank(const uint4* vkeys, const uint32_t* slot_of_rank, uint32_t V, uint4* out, hipStream_t s);
