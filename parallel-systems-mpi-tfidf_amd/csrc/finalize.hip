@@ -904,6 +904,9 @@ constexpr uint32_t K5_NB_BITS = 9;    /* bucket sort: 512 buckets by the rank's 
 constexpr uint32_t K5_NB = 1u << K5_NB_BITS;
 constexpr uint32_t K5_GROUP_MAX = 48; /* larger buckets (skewed ranks): the radix path */
 constexpr uint32_t K5L_GROUP_MAX = 32; /* k_score_large: larger buckets (skewed ranks) take the radix path */
+#ifndef K5L_EB
+#define K5L_EB 8                      /* k_score_large: elements per thread in flight together */
+#endif
 
 /* idf of every term rank: one gather per pair in K5 instead of three dependent ones */
 __global__ void k_idf_of_rank(const uint32_t* __restrict__ df_of_rank, const uint32_t* __restrict__ idf_idx,
@@ -1054,10 +1057,10 @@ __global__ __launch_bounds__(NT, K5_WPS) void k_score_wave(K5Args a) {
     uint32_t* buf1 = kb[w][1];
     uint32_t* h = hist[w];
     /* the positions this kernel scores: its segment of the class list (k_k5_classify), or
-     * every position (wide ranks) */
+     * every position */
     const uint32_t* L = nullptr;
     uint32_t lcount = a.ndocs;
-    if (!WIDE && a.cls_list) {
+    if (a.cls_list) {
         const uint32_t lo = G(a.cls_off)[a.cls_nblk];
         L = a.cls_list + lo;
         lcount = G(a.cls_off)[2 * a.cls_nblk] - lo;
@@ -1392,12 +1395,51 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
     }
     if (presorted || n > (uint32_t)K5_MAX) {
         if (n > (uint32_t)K5_MAX && !presorted) { if (tid == 0) atomicOr(a.status, ST_BOUNDS); continue; }
-        for (uint32_t j = tid; j < n; j += NT) k5_emit(a, ob + j, ds, k5_rank(a, G(a.rec_slot)[rb + j]), G(a.rec_cnt)[rb + j]);
+        /* K5L_EB elements per thread in flight: the loads, then the idf gathers, then the
+         * stores (a per-element loop is one dependent chain of round trips) */
+        for (uint32_t j0 = 0; j0 < n; j0 += NT * K5L_EB) {
+            uint32_t rk[K5L_EB], cn[K5L_EB];
+            double f[K5L_EB];
+#pragma unroll
+            for (int e = 0; e < K5L_EB; ++e) {
+                const uint32_t j = j0 + NT * e + tid;
+                rk[e] = j < n ? G(a.rec_slot)[rb + j] : 0u;
+                cn[e] = j < n ? G(a.rec_cnt)[rb + j] : 0u;
+            }
+#pragma unroll
+            for (int e = 0; e < K5L_EB; ++e) {
+                const uint32_t j = j0 + NT * e + tid;
+                if (j < n) rk[e] = k5_rank(a, rk[e]);
+                f[e] = j < n ? G(a.idf_rank)[rk[e]] : 0.0;
+            }
+#pragma unroll
+            for (int e = 0; e < K5L_EB; ++e) {
+                const uint32_t j = j0 + NT * e + tid;
+                if (j < n) {
+                    G(a.out_term)[ob + j] = rk[e];
+                    G(a.out_cnt)[ob + j] = cn[e];
+                    G(a.out_score)[ob + j] = ((double)cn[e] / ds) * f[e];   /* TFIDF.c:202,243-244 */
+                }
+            }
+        }
         continue;
     }
-    for (uint32_t j = tid; j < n; j += NT) {
-        kbuf[0][j] = k5_rank(a, G(a.rec_slot)[rb + j]);
-        vbuf[0][j] = G(a.rec_cnt)[rb + j];
+    for (uint32_t j0 = 0; j0 < n; j0 += NT * K5L_EB) {   /* loads in flight together */
+        uint32_t sl[K5L_EB], cn[K5L_EB];
+#pragma unroll
+        for (int e = 0; e < K5L_EB; ++e) {
+            const uint32_t j = j0 + NT * e + tid;
+            sl[e] = j < n ? G(a.rec_slot)[rb + j] : 0u;
+            cn[e] = j < n ? G(a.rec_cnt)[rb + j] : 0u;
+        }
+#pragma unroll
+        for (int e = 0; e < K5L_EB; ++e) {
+            const uint32_t j = j0 + NT * e + tid;
+            if (j < n) {
+                kbuf[0][j] = k5_rank(a, sl[e]);
+                vbuf[0][j] = cn[e];
+            }
+        }
     }
     {
         /* bucket sort (ranks are distinct within a document): K5L_NB buckets by the rank's
@@ -1429,12 +1471,33 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
                 vbuf[1][q] = j;
             }
             __syncthreads();   /* bh[d] = bucket d's end = bucket d+1's start */
-            for (uint32_t p = tid; p < n; p += NT) {
-                const uint32_t k = kbuf[1][p], d = k >> hsh;
-                const uint32_t gs = d ? bh[d - 1] : 0u, ge = bh[d];
-                uint32_t less = 0;
-                for (uint32_t f = gs; f < ge; ++f) less += kbuf[1][f] < k ? 1u : 0u;
-                k5_emit(a, ob + gs + less, ds, k, vbuf[0][vbuf[1][p]]);
+            for (uint32_t p0 = 0; p0 < n; p0 += NT * K5L_EB) {
+                uint32_t kk[K5L_EB], ps[K5L_EB], cn[K5L_EB];
+                double f[K5L_EB];
+#pragma unroll
+                for (int e = 0; e < K5L_EB; ++e) {
+                    const uint32_t p = p0 + NT * e + tid;
+                    kk[e] = 0u; ps[e] = 0u; cn[e] = 0u;
+                    if (p < n) {
+                        const uint32_t k = kbuf[1][p], d = k >> hsh;
+                        const uint32_t gs = d ? bh[d - 1] : 0u, ge = bh[d];
+                        uint32_t less = 0;
+                        for (uint32_t g = gs; g < ge; ++g) less += kbuf[1][g] < k ? 1u : 0u;
+                        kk[e] = k;
+                        ps[e] = gs + less;
+                        cn[e] = vbuf[0][vbuf[1][p]];
+                    }
+                    f[e] = p < n ? G(a.idf_rank)[kk[e]] : 0.0;
+                }
+#pragma unroll
+                for (int e = 0; e < K5L_EB; ++e) {
+                    if (p0 + NT * e + tid < n) {
+                        const uint64_t o = ob + ps[e];
+                        G(a.out_term)[o] = kk[e];
+                        G(a.out_cnt)[o] = cn[e];
+                        G(a.out_score)[o] = ((double)cn[e] / ds) * f[e];   /* TFIDF.c:202,243-244 */
+                    }
+                }
             }
             __syncthreads();   /* the next document reuses the LDS buffers */
             continue;
@@ -1547,43 +1610,134 @@ __global__ __launch_bounds__(256) void k_k5_scatter(K5Args a) {
 }
 
 /* Documents of <= K5_SMALL_DOC pairs (c5: 1e6 documents of ~50 pairs), listed by
- * k_k5_classify: one wave per document over the list, 0.5 KB of LDS per wave and few
- * registers, so ~3x the documents of the wave kernel are in flight per CU — the path is a
- * chain of dependent round trips per document (metadata -> records -> idf), and latency
- * is hidden by the number of documents in flight.  Position of a pair = the number of
- * smaller ranks in its document (ranks are distinct within a document; presorted runs
- * keep their order).  TFIDF.c:202,243-245,273. */
+ * k_k5_classify.  One wave per document, each wave over a contiguous run of the small
+ * list: the run's metadata is loaded 64 documents at a time (lane j: document j of the
+ * batch) and read out with readlane, and the per-document chain (records -> idf -> output)
+ * is software-pipelined: while document k is positioned and written, the idf of k+1 and
+ * the records of k+2 are in flight, so a document costs about one memory round trip
+ * instead of five.  Position of a pair = the number of smaller ranks in its document
+ * (ranks are distinct within a document; presorted runs keep their order).
+ * TFIDF.c:202,243-245,273. */
 constexpr int K5S_WG = 4;   /* waves per workgroup */
-__global__ __launch_bounds__(256, 8) void k_score_small(K5Args a) {
+#ifndef K5S_OCC
+#define K5S_OCC 6           /* workgroups per CU it is compiled for */
+#endif
+struct K5SDoc {
+    uint64_t rb, ob;
+    uint32_t n;
+    bool presorted;
+    double ds;
+};
+__device__ __forceinline__ void k5s_batch(const K5Args& a, const uint32_t* L, uint32_t d, uint32_t d1, uint4& m,
+                                          uint64_t& ob) {
+    m = make_uint4(0, 0, 0, 0);
+    ob = 0;
+    if (d < d1) {
+        const uint32_t i = G(L)[d];
+        m = gload(a.meta + i);
+        ob = G(a.out_off)[i];
+    }
+}
+__global__ __launch_bounds__(256, K5S_OCC) void k_score_small(K5Args a) {
     __shared__ __attribute__((aligned(16))) uint32_t kb[K5S_WG][K5_SMALL_DOC + 4];
+    __shared__ uint4 bm[K5S_WG][64];      /* the current batch's metadata (the next one: registers) */
+    __shared__ uint64_t bo[K5S_WG][64];
+    constexpr int Q = K5_SMALL_DOC / 64;
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint32_t* buf = kb[w];
     const uint32_t nsmall = G(a.cls_off)[a.cls_nblk];   /* the small segment starts the class list */
-    const uint32_t stride = gridDim.x * K5S_WG;
-    constexpr int Q = K5_SMALL_DOC / 64;
-    for (uint32_t li = blockIdx.x * K5S_WG + w; li < nsmall; li += stride) {
-        const uint32_t i = G(a.cls_list)[li];
-        const uint4 m = gload(a.meta + i);
-        const uint32_t n = m.z & 0x3FFFFFFFu;
-        const bool presorted = ((m.z >> 30) & DF_PRESORTED) != 0;
-        const uint64_t rb = ((uint64_t)m.y << 32) | m.x;
-        const uint64_t ob = G(a.out_off)[i];
-        const double ds = (double)m.w;
-        if (n > K5_SMALL_DOC || rb + n > a.rec_total) { if (lane == 0) atomicOr(a.status, ST_BOUNDS); continue; }
-        uint32_t r[Q], c[Q], pos[Q];
+    const uint32_t nw = gridDim.x * K5S_WG, wid = blockIdx.x * K5S_WG + w;
+    const uint32_t per = (nsmall + nw - 1) / nw;
+    const uint32_t d0 = wid * per;
+    const uint32_t d1 = d0 + per < nsmall ? d0 + per : nsmall;
+    if (d0 >= d1) return;
+    const uint32_t cnt = d1 - d0;
+    const uint32_t* L = a.cls_list;
+    uint4 mnxt;
+    uint64_t onxt;
+    k5s_batch(a, L, d0 + lane, d1, mnxt, onxt);
+    bm[w][lane] = mnxt;
+    bo[w][lane] = onxt;
+    k5s_batch(a, L, d0 + 64 + lane, d1, mnxt, onxt);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t curb = 0;   /* batch in bm / bo */
+    auto doc_at = [&](uint32_t k) -> K5SDoc {
+        K5SDoc d;
+        if (k >= cnt) { d.rb = 0; d.ob = 0; d.n = 0; d.presorted = true; d.ds = 1.0; return d; }
+        const int l = (int)(k & 63u);
+        uint32_t mx, my, mz, mw, olo, ohi;
+        if ((k >> 6) == curb) {
+            const uint4 m = bm[w][l];
+            const uint64_t o = bo[w][l];
+            mx = __builtin_amdgcn_readfirstlane(m.x); my = __builtin_amdgcn_readfirstlane(m.y);
+            mz = __builtin_amdgcn_readfirstlane(m.z); mw = __builtin_amdgcn_readfirstlane(m.w);
+            olo = __builtin_amdgcn_readfirstlane((uint32_t)o);
+            ohi = __builtin_amdgcn_readfirstlane((uint32_t)(o >> 32));
+        } else {
+            mx = __builtin_amdgcn_readlane(mnxt.x, l); my = __builtin_amdgcn_readlane(mnxt.y, l);
+            mz = __builtin_amdgcn_readlane(mnxt.z, l); mw = __builtin_amdgcn_readlane(mnxt.w, l);
+            olo = __builtin_amdgcn_readlane((uint32_t)onxt, l);
+            ohi = __builtin_amdgcn_readlane((uint32_t)(onxt >> 32), l);
+        }
+        d.rb = ((uint64_t)my << 32) | mx;
+        d.ob = ((uint64_t)ohi << 32) | olo;
+        d.n = mz & 0x3FFFFFFFu;
+        d.presorted = ((mz >> 30) & DF_PRESORTED) != 0;
+        d.ds = (double)mw;
+        if (d.n > K5_SMALL_DOC || d.rb + d.n > a.rec_total) {
+            if (lane == 0) atomicOr(a.status, ST_BOUNDS);
+            d.n = 0;
+        }
+        return d;
+    };
+    auto load_rec = [&](const K5SDoc& d, uint32_t (&r)[Q], uint32_t (&c)[Q]) {
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const uint32_t j = 64u * q + lane;
-            const bool v = j < n;
-            r[q] = v ? k5_rank(a, G(a.rec_slot)[rb + j]) : 0xFFFFFFFFu;
-            c[q] = v ? G(a.rec_cnt)[rb + j] : 0u;
-            pos[q] = j;
+            const bool v = j < d.n;
+            r[q] = v ? G(a.rec_slot)[d.rb + j] : 0xFFFFFFFFu;
+            c[q] = v ? G(a.rec_cnt)[d.rb + j] : 0u;
         }
-        if (!presorted) {
+    };
+    auto load_idf = [&](const K5SDoc& d, uint32_t (&r)[Q], double (&f)[Q]) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const bool v = 64u * q + lane < d.n;
+            if (v) r[q] = k5_rank(a, r[q]);
+            f[q] = v ? G(a.idf_rank)[r[q]] : 0.0;
+        }
+    };
+    K5SDoc D0 = doc_at(0), D1 = doc_at(1);
+    uint32_t r0[Q], c0[Q], r1[Q], c1[Q];
+    double f0[Q];
+    load_rec(D0, r0, c0);
+    load_rec(D1, r1, c1);
+    load_idf(D0, r0, f0);
+    for (uint32_t k = 0; k < cnt; ++k) {
+        if (k && (k & 63u) == 0u) {   /* doc k starts batch curb + 1 */
+            bm[w][lane] = mnxt;
+            bo[w][lane] = onxt;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            ++curb;
+            k5s_batch(a, L, d0 + 64u * (curb + 1) + lane, d1, mnxt, onxt);
+        }
+        const K5SDoc D2 = doc_at(k + 2);
+        uint32_t r2[Q], c2[Q];
+        double f1[Q];
+        load_rec(D2, r2, c2);
+        load_idf(D1, r1, f1);
+        /* document k: positions, then the output */
+        const uint32_t n = D0.n;
+        uint32_t pos[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) pos[q] = 64u * q + lane;
+        if (!D0.presorted && n > 1u) {
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
                 const uint32_t j = 64u * q + lane;
-                if (j < n) buf[j] = r[q];
+                if (j < n) buf[j] = r0[q];
             }
             const uint32_t n4 = (n + 3u) & ~3u;
             if (lane < 4u && n + lane < n4) buf[n + lane] = 0xFFFFFFFFu;
@@ -1596,23 +1750,27 @@ __global__ __launch_bounds__(256, 8) void k_score_small(K5Args a) {
                 const uint4 k4 = k4p[i4];
 #pragma unroll
                 for (int q = 0; q < Q; ++q)
-                    pos[q] += (k4.x < r[q] ? 1u : 0u) + (k4.y < r[q] ? 1u : 0u) + (k4.z < r[q] ? 1u : 0u) +
-                              (k4.w < r[q] ? 1u : 0u);
+                    pos[q] += (k4.x < r0[q] ? 1u : 0u) + (k4.y < r0[q] ? 1u : 0u) + (k4.z < r0[q] ? 1u : 0u) +
+                              (k4.w < r0[q] ? 1u : 0u);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        double idf[Q];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) idf[q] = (64u * q + lane < n) ? G(a.idf_rank)[r[q]] : 0.0;
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             if (64u * q + lane < n) {
-                const uint64_t o = ob + pos[q];
-                G(a.out_term)[o] = r[q];
-                G(a.out_cnt)[o] = c[q];
-                G(a.out_score)[o] = ((double)c[q] / ds) * idf[q];   /* TFIDF.c:202,243-244 */
+                const uint64_t o = D0.ob + pos[q];
+                G(a.out_term)[o] = r0[q];
+                G(a.out_cnt)[o] = c0[q];
+                G(a.out_score)[o] = ((double)c0[q] / D0.ds) * f0[q];   /* TFIDF.c:202,243-244 */
             }
+        }
+        D0 = D1;
+        D1 = D2;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            r0[q] = r1[q]; c0[q] = c1[q]; f0[q] = f1[q];
+            r1[q] = r2[q]; c1[q] = c2[q];
         }
     }
 }
@@ -1628,8 +1786,31 @@ __global__ __launch_bounds__(256) void k_emit_split(K5Args a) {
         const double ds = (double)m.w;
         if (rb + n > a.rec_total) { if (threadIdx.x == 0) atomicOr(a.status, ST_BOUNDS); continue; }
         const uint32_t j1 = (tk.y + 1) * K5_PS_SPLIT < n ? (tk.y + 1) * K5_PS_SPLIT : n;
-        for (uint32_t j = tk.y * K5_PS_SPLIT + threadIdx.x; j < j1; j += 256)
-            k5_emit(a, ob + j, ds, k5_rank(a, G(a.rec_slot)[rb + j]), G(a.rec_cnt)[rb + j]);
+        for (uint32_t j0 = tk.y * K5_PS_SPLIT; j0 < j1; j0 += 256 * K5L_EB) {   /* K5L_EB in flight */
+            uint32_t rk[K5L_EB], cn[K5L_EB];
+            double f[K5L_EB];
+#pragma unroll
+            for (int e = 0; e < K5L_EB; ++e) {
+                const uint32_t j = j0 + 256u * e + threadIdx.x;
+                rk[e] = j < j1 ? G(a.rec_slot)[rb + j] : 0u;
+                cn[e] = j < j1 ? G(a.rec_cnt)[rb + j] : 0u;
+            }
+#pragma unroll
+            for (int e = 0; e < K5L_EB; ++e) {
+                const uint32_t j = j0 + 256u * e + threadIdx.x;
+                if (j < j1) rk[e] = k5_rank(a, rk[e]);
+                f[e] = j < j1 ? G(a.idf_rank)[rk[e]] : 0.0;
+            }
+#pragma unroll
+            for (int e = 0; e < K5L_EB; ++e) {
+                const uint32_t j = j0 + 256u * e + threadIdx.x;
+                if (j < j1) {
+                    G(a.out_term)[ob + j] = rk[e];
+                    G(a.out_cnt)[ob + j] = cn[e];
+                    G(a.out_score)[ob + j] = ((double)cn[e] / ds) * f[e];   /* TFIDF.c:202,243-244 */
+                }
+            }
+        }
     }
 }
 static void launch_score_large(const K5Args& a, uint32_t grid, hipStream_t s) {
@@ -1654,36 +1835,38 @@ int launch_score_order(const K5Args& a, Arena& ar, hipStream_t s, hipStream_t s2
     const uint32_t wg_need = (a.ndocs + NT / 64 - 1) / (NT / 64);
     const uint32_t wg = wg_need < (uint32_t)ncu * 4u ? wg_need : (uint32_t)ncu * 4u; /* 36 KB LDS: 4 per CU */
     const uint32_t grid = a.ndocs < 2048u ? a.ndocs : 2048u; /* persistent over the handed-off list */
-    if (a.rank_bits + K5_IDX_BITS > 32) {   /* skewed wide documents are handed off during the run */
-        K5Args b = a;
-        b.cls_list = nullptr;   /* the wide instance takes every position (and hands off on the fly) */
-        b.split_count = nullptr;
-        k_score_wave<true><<<wg, NT, 0, s>>>(b);
-        launch_score_large(b, grid, s);
-        return ok();
-    }
+    /* wide ranks (> 32 - K5_IDX_BITS bits): the wave kernel's instance that hands skewed
+     * documents to k_score_large during the run, scored after it by a second k_score_large
+     * over that list */
+    const bool wide = a.rank_bits + K5_IDX_BITS > 32;
+    K5Args hand = a;
+    hand.cls_list = nullptr;
     if (!a.cls_list || !a.cls_off) return -1;
     k_k5_classify<<<a.cls_nblk, 256, 0, s>>>(a);
     if (scan_excl_u32(a.cls_off, a.cls_off, 3ull * a.cls_nblk + 1, ar, s)) return -1;
     k_k5_scatter<<<a.cls_nblk, 256, 0, s>>>(a);
-    k_score_small<<<(unsigned)ncu * 8u, 256, 0, s>>>(a);
+    k_score_small<<<(unsigned)ncu * (unsigned)K5S_OCC, 256, 0, s>>>(a);
 #ifndef K5_SERIAL_LARGE
     if (s2 && ev_fork && ev_join) {
         /* the wave kernel first (its persistent grid takes the CUs), k_score_large on the
          * side stream fills them as the wave kernel's workgroups retire */
         if (hipEventRecord(ev_fork, s) != hipSuccess) return -1;
-        k_score_wave<false><<<wg, NT, 0, s>>>(a);
+        if (wide) k_score_wave<true><<<wg, NT, 0, s>>>(a);
+        else k_score_wave<false><<<wg, NT, 0, s>>>(a);
         if (hipStreamWaitEvent(s2, ev_fork, 0) != hipSuccess) return -1;
-        if (a.split_count) k_emit_split<<<(unsigned)ncu * 4u, 256, 0, s2>>>(a);
         launch_score_large(a, grid, s2);
+        if (a.split_count) k_emit_split<<<(unsigned)ncu * 4u, 256, 0, s2>>>(a);
         if (hipEventRecord(ev_join, s2) != hipSuccess) return -1;
         if (hipStreamWaitEvent(s, ev_join, 0) != hipSuccess) return -1;
+        if (wide) launch_score_large(hand, grid, s);
         return ok();
     }
 #endif
-    k_score_wave<false><<<wg, NT, 0, s>>>(a);
+    if (wide) k_score_wave<true><<<wg, NT, 0, s>>>(a);
+    else k_score_wave<false><<<wg, NT, 0, s>>>(a);
     if (a.split_count) k_emit_split<<<(unsigned)ncu * 4u, 256, 0, s>>>(a);
     launch_score_large(a, grid, s);
+    if (wide) launch_score_large(hand, grid, s);
     return ok();
 }
 

@@ -6,9 +6,9 @@ import csv, sys
 rows=list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r:int(r['Start_Timestamp']))
 idx=[i for i,r in enumerate(rows) if 'k_score_wave' in r['Kernel_Name']]
-i0=idx[-1]-3
+i0=idx[-1]-7
 t0=int(rows[i0]['Start_Timestamp'])
-for r in rows[i0:i0+12]:
+for r in rows[i0:i0+14]:
     s,e=int(r['Start_Timestamp']),int(r['End_Timestamp'])
     print("%8.1f us  dur %7.1f  q%s %s"%((s-t0)/1e3,(e-s)/1e3,r['Queue_Id'],r['Kernel_Name'][:50]))
 PY
