@@ -900,6 +900,9 @@ constexpr int K5_BATCH = 8;           /* gathers per lane in flight together */
 #ifndef K5_WPS
 #define K5_WPS 4                      /* waves per SIMD the wave kernel is compiled for */
 #endif
+#ifndef K5_WPS_WIDE
+#define K5_WPS_WIDE 4                 /* ... its wide-rank instance */
+#endif
 constexpr uint32_t K5_NB_BITS = 9;    /* bucket sort: 512 buckets by the rank's top bits */
 constexpr uint32_t K5_NB = 1u << K5_NB_BITS;
 constexpr uint32_t K5_GROUP_MAX = 48; /* larger buckets (skewed ranks): the radix path */
@@ -946,12 +949,16 @@ __device__ __forceinline__ bool k5_by_wave(const K5Args& a, uint32_t n, bool pre
 /* Skewed documents (a bucket of the bucket sort above K5_GROUP_MAX keys): LSD radix sort
  * by rank, 8-bit digits, of the packed keys in buf0 — a wave-private histogram, a DPP scan
  * of the 256 bins and a stable multisplit scatter (8 ballots) per round of 64 keys. */
-__device__ __noinline__ void k5_radix(const K5Args& a, uint32_t* buf0, uint32_t* buf1, uint32_t* h, uint32_t n,
-                                      uint64_t rb, uint64_t ob, double ds) {
+/* (the fields it uses are passed as values: a reference to the kernel's argument struct
+ * would put the struct on the stack, and every field the caller reads would become a
+ * scratch load — one in-order vmcnt wait behind its prefetch loads) */
+__device__ __noinline__ void k5_radix(uint32_t rank_bits, const uint32_t* rec_cnt, const double* idf_rank,
+                                      uint32_t* out_term, uint32_t* out_cnt, double* out_score, uint32_t* buf0,
+                                      uint32_t* buf1, uint32_t* h, uint32_t n, uint64_t rb, uint64_t ob, double ds) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t below = (1ull << lane) - 1ull;
     uint32_t cur = 0;
-    for (uint32_t sh = K5_IDX_BITS; sh < K5_IDX_BITS + a.rank_bits; sh += 8) {
+    for (uint32_t sh = K5_IDX_BITS; sh < K5_IDX_BITS + rank_bits; sh += 8) {
         const uint32_t* src = cur ? buf1 : buf0;
         uint32_t* dst = cur ? buf0 : buf1;
         h[4 * lane] = 0; h[4 * lane + 1] = 0; h[4 * lane + 2] = 0; h[4 * lane + 3] = 0;
@@ -1005,16 +1012,16 @@ __device__ __noinline__ void k5_radix(const K5Args& a, uint32_t* buf0, uint32_t*
         }
 #pragma unroll
         for (int q = 0; q < K5_BATCH; ++q) {
-            cnt[q] = G(a.rec_cnt)[rb + (key[q] & ((1u << K5_IDX_BITS) - 1u))];
-            idf[q] = G(a.idf_rank)[key[q] >> K5_IDX_BITS];
+            cnt[q] = G(rec_cnt)[rb + (key[q] & ((1u << K5_IDX_BITS) - 1u))];
+            idf[q] = G(idf_rank)[key[q] >> K5_IDX_BITS];
         }
 #pragma unroll
         for (int q = 0; q < K5_BATCH; ++q) {
             const uint32_t j = j0 + 64 * q + lane;
             if (j < n) {
-                G(a.out_term)[ob + j] = key[q] >> K5_IDX_BITS;
-                G(a.out_cnt)[ob + j] = cnt[q];
-                G(a.out_score)[ob + j] = ((double)cnt[q] / ds) * idf[q]; /* TFIDF.c:202,243-244 */
+                G(out_term)[ob + j] = key[q] >> K5_IDX_BITS;
+                G(out_cnt)[ob + j] = cnt[q];
+                G(out_score)[ob + j] = ((double)cnt[q] / ds) * idf[q]; /* TFIDF.c:202,243-244 */
             }
         }
     }
@@ -1048,7 +1055,7 @@ __device__ __forceinline__ void k5_prefetch(const K5Args& a, const uint4& m, uin
 /* WIDE: the instance launched when ranks exceed 32 - K5_IDX_BITS bits (its extra path
  * costs registers the common instance must not pay: c2 score 0.88 -> 1.16 ms with it) */
 template <bool WIDE>
-__global__ __launch_bounds__(NT, K5_WPS) void k_score_wave(K5Args a) {
+__global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(K5Args a) {
     __shared__ __attribute__((aligned(16))) uint32_t kb[NT / 64][2][K5_WAVE];
     __shared__ uint32_t hist[NT / 64][K5_NB];
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1221,7 +1228,7 @@ __global__ __launch_bounds__(NT, K5_WPS) void k_score_wave(K5Args a) {
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const bool wide = WIDE && a.rank_bits + K5_IDX_BITS > 32;
+        const bool wide = WIDE;   /* launched only for ranks over 32 - K5_IDX_BITS bits */
         if (gmax > K5_GROUP_MAX && wide) { /* skewed and too wide for packed keys: k_score_large */
             if (lane == 0) G(a.large_list)[atomicAdd(a.large_count, 1u)] = i;
             continue;
@@ -1284,7 +1291,9 @@ __global__ __launch_bounds__(NT, K5_WPS) void k_score_wave(K5Args a) {
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            k5_radix(a, buf0, buf1, h, n, rb, ob, ds);
+            if constexpr (!WIDE)   /* the wide instance runs only for wide ranks: handed off above */
+                k5_radix(a.rank_bits, a.rec_cnt, a.idf_rank, a.out_term, a.out_cnt, a.out_score, buf0, buf1, h, n,
+                         rb, ob, ds);
             continue;
         }
 #pragma unroll
@@ -1833,12 +1842,13 @@ int launch_score_order(const K5Args& a, Arena& ar, hipStream_t s, hipStream_t s2
             ncu = 256;
     }
     const uint32_t wg_need = (a.ndocs + NT / 64 - 1) / (NT / 64);
-    const uint32_t wg = wg_need < (uint32_t)ncu * 4u ? wg_need : (uint32_t)ncu * 4u; /* 36 KB LDS: 4 per CU */
+    const bool wide = a.rank_bits + K5_IDX_BITS > 32;
+    const uint32_t wg_cu = wide ? (uint32_t)K5_WPS_WIDE : 4u;   /* 40 KB LDS: 4 per CU; wide: its registers */
+    const uint32_t wg = wg_need < (uint32_t)ncu * wg_cu ? wg_need : (uint32_t)ncu * wg_cu;
     const uint32_t grid = a.ndocs < 2048u ? a.ndocs : 2048u; /* persistent over the handed-off list */
     /* wide ranks (> 32 - K5_IDX_BITS bits): the wave kernel's instance that hands skewed
      * documents to k_score_large during the run, scored after it by a second k_score_large
      * over that list */
-    const bool wide = a.rank_bits + K5_IDX_BITS > 32;
     K5Args hand = a;
     hand.cls_list = nullptr;
     if (!a.cls_list || !a.cls_off) return -1;
