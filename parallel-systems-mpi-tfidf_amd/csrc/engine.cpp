@@ -139,6 +139,7 @@ struct tfidf_ctx {
     /* last run */
     bool have_result = false;
     bool have_info = false;   /* run counters/timings valid (also after an ablation run) */
+    uint64_t run_nbytes = 0;  /* corpus bytes of the last run (its bounds, read once by the run) */
     tfidf_corpus corpus{};
     const uint8_t* dev_bytes = nullptr;
     const uint32_t* dev_ids = nullptr;
@@ -973,6 +974,7 @@ extern "C" int tfidf_run(tfidf_ctx* ctx, const tfidf_corpus* in) {
     if (rc == 1) return TFIDF_E_CAPACITY;
     if (rc) return rc;
     ctx->corpus = *in;
+    ctx->run_nbytes = c.hi - c.lo;
     ctx->dev_bytes = c.bytes;
     ctx->dev_ids = dev_ids;
     ctx->ndocs = N;
@@ -1064,20 +1066,7 @@ extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info) {
     if (!ctx || !info) return TFIDF_E_INVAL;
     if (!ctx->have_info) return TFIDF_E_STATE;
     memset(info, 0, sizeof(*info));
-    info->nbytes = ctx->corpus.ndocs ? 0 : 0;
-    {
-        uint64_t lo = 0, hi = 0;
-        if (ctx->corpus.ndocs) {
-            if (ctx->corpus.flags & TFIDF_CORPUS_DEVICE) {
-                (void)hipMemcpy(&lo, ctx->corpus.doc_off, 8, hipMemcpyDeviceToHost);
-                (void)hipMemcpy(&hi, ctx->corpus.doc_off + ctx->corpus.ndocs, 8, hipMemcpyDeviceToHost);
-            } else {
-                lo = ctx->corpus.doc_off[0];
-                hi = ctx->corpus.doc_off[ctx->corpus.ndocs];
-            }
-        }
-        info->nbytes = hi - lo;
-    }
+    info->nbytes = ctx->run_nbytes;   /* no device round trip: the run read the bounds */
     info->ntokens = ctx->ntokens;
     info->npairs = ctx->npairs;
     info->nterms = ctx->V;
