@@ -12,3 +12,7 @@ cat $OUT/bench_c2.json
 bash scripts/kstats.sh r02f_c2 > $OUT/kernel_stats_c2.txt 2>&1 || { echo "kstats failed"; exit 1; }
 head -8 $OUT/kernel_stats_c2.txt
 KSTATS=0 PMC=0 CFGS="c4 c5" bash scripts/measure_cfgs.sh r02_final || exit 1
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -20 $OUT/gpu_tests.log; exit 1; }
+tail -2 $OUT/gpu_tests.log
+timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; tail -5 $OUT/smoke.log; exit 1; }
+tail -1 $OUT/smoke.log
