@@ -418,3 +418,35 @@ def test_df_histogram_bin_overflow(engine):
     r = engine.fetch()
     assert np.all(r["df"] == N) and np.all(r["count"] == 1) and np.all(r["docsize"] == 1)
     assert np.all(r["score"] == 0.0)
+
+
+def _doc_with_terms(rng, n, vocab):
+    """a document holding exactly n distinct terms of `vocab`, each 1-3 times, shuffled"""
+    ids = rng.choice(len(vocab), size=n, replace=False)
+    toks = np.repeat(ids, rng.integers(1, 4, size=n))
+    rng.shuffle(toks)
+    return b" ".join(vocab[i] for i in toks)
+
+
+def test_score_document_classes_vs_oracle(engine):
+    """K5's document classes at their boundaries (finalize.hip k5_class): <= 128 pairs
+    (k_score_small), <= 64 / <= 1024 (wave kernel: bitonic, counting, bucket paths), > 1024
+    (k_score_large, both instances), and one > 4 MiB document (dense merge: a presorted run
+    over 4096 pairs, emitted by k_emit_split's chunk tasks), among many small documents."""
+    rng = np.random.default_rng(11)
+    vocab = [b"t%05d" % i for i in range(30000)]
+    sizes = [1, 2, 63, 64, 65, 127, 128, 129, 511, 512, 513, 1023, 1024, 1025, 2047, 2048, 2049, 4096, 4097, 9000]
+    docs = [_doc_with_terms(rng, n, vocab) for n in sizes]
+    docs += [_doc_with_terms(rng, int(n), vocab) for n in rng.integers(1, 200, size=300)]
+    big = []
+    total = 0
+    while total < (4 << 20) + 65536:   # > 4 MiB: the dense merge's presorted run
+        d = _doc_with_terms(rng, 20000, vocab)
+        big.append(d)
+        total += len(d) + 1
+    docs.append(b" ".join(big))
+    order = rng.permutation(len(docs))
+    docs = [docs[i] for i in order]
+    data, off = docs_to_arrays(docs)
+    res = check_vs_oracle(engine, data, off)
+    assert res["npairs"] > 20000
