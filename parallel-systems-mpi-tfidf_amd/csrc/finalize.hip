@@ -1858,7 +1858,7 @@ int launch_score_order(const K5Args& a, Arena& ar, hipStream_t s, hipStream_t s2
     k_score_small<<<(unsigned)ncu * (unsigned)K5S_OCC, 256, 0, s>>>(a);
     /* k_score_large after the wave kernel on the same stream: beside it on the side stream
      * (-DK5_CONCURRENT_LARGE) measured c2 score 0.74 vs 0.76 ms but c4 3.18-3.29 vs
-     * 3.04-3.11 and c5 0.83 vs 0.81, and on some boxes an occasional ~2x slower stage */
+     * 3.04-3.11 and c5 0.83 vs 0.81 */
 #ifdef K5_CONCURRENT_LARGE
     if (s2 && ev_fork && ev_join) {
         /* the wave kernel first (its persistent grid takes the CUs), k_score_large on the
