@@ -196,7 +196,7 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    k1_ms, tot_ms = [], []
+    k1_ms, tot_ms, stage_steps = [], [], []
     barrier()
     hip_device_sync()
     t0 = time.perf_counter()
@@ -205,6 +205,7 @@ def main():
         info = eng.info()
         k1_ms.append(info["ms_tokcount"])
         tot_ms.append(info["ms_total"])
+        stage_steps.append(info["stages"])
     hip_device_sync()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -268,6 +269,8 @@ def main():
             "tokens_per_s": round(T_all * args.steps / elapsed, 1),
             "device_ms_per_step": round(float(np.mean(tot_ms)), 4),
             "stage_ms": {k: round(v, 4) for k, v in info["stages"].items()},
+            "stage_ms_mean": {k: round(float(np.mean([st[k] for st in stage_steps])), 4) for k in info["stages"]},
+            "stage_ms_max": {k: round(float(np.max([st[k] for st in stage_steps])), 4) for k in info["stages"]},
             "k1_work": {"chunks": int(info["nchunks"]), "partial_records": int(info["partial_records"]),
                         "vocab_capacity": int(info["vocab_capacity"]), "terms": int(info["nterms"])},
             "roofline": {"bound": "hbm", "kernel": f"{kern} (K1)", "achieved": round(achieved, 2),
