@@ -39,7 +39,10 @@ struct DevBuf {
     int ensure(size_t bytes) {
         if (bytes <= cap && p) return 0;
         if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
-        size_t want = bytes < 256 ? 256 : bytes;
+        /* 1/8 headroom: sizes that vary a little from run to run (the record total after
+         * K1's overflow records) must not reallocate — hipFree synchronises the device and
+         * a 1 GB hipMalloc inside a stage left the GPU idle for ~0.7 ms */
+        size_t want = bytes < 256 ? 256 : bytes + (bytes >= (1u << 20) ? bytes / 8 : 0);
         if (hipMalloc(&p, want) != hipSuccess) { p = nullptr; return -1; }
         cap = want;
         return 0;
