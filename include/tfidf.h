@@ -105,7 +105,15 @@ int tfidf_comm_unique_id(uint8_t id[TFIDF_UNIQUE_ID_BYTES]);
  * of this context is collective: all ranks call it, each on its own shard (contiguous
  * ranges of the "docN@" order, ndocs_total = N of the whole corpus).  Capacity retries
  * are agreed between the ranks (all repeat or none does); a rank whose run fails makes
- * the others return TFIDF_E_PEER instead of waiting. */
+ * the others return TFIDF_E_PEER instead of waiting.
+ * Abort contract: a failure agreed before the exchange's collectives (a local error, a
+ * capacity retry) needs nothing from the caller.  A rank-local failure AFTER the agreement
+ * (inside the key all-gather / DF all-reduce sequence) aborts this rank's communicator; its
+ * peers may then be blocked inside a collective, and with one process per GPU only the
+ * caller can reach them: it must make every other rank call ncclCommAbort on its own
+ * communicator (e.g. by tfidf_close on those contexts after its out-of-band failure notice)
+ * — tfidf_group_* does exactly this for its clique.  A context whose communicator was
+ * aborted returns TFIDF_E_PEER / TFIDF_E_STATE from then on: close and reopen it. */
 int tfidf_comm_init(tfidf_ctx* ctx, const uint8_t id[TFIDF_UNIQUE_ID_BYTES], int rank, int nranks);
 
 /* ---- one process, several shards: the drop-in for `mpirun -np P ./TFIDF`
@@ -113,7 +121,11 @@ int tfidf_comm_init(tfidf_ctx* ctx, const uint8_t id[TFIDF_UNIQUE_ID_BYTES], int
  *      gather + sort).  Rank r runs on devices[r] (NULL: device r).  When every rank has
  *      its own GPU the ranks are one RCCL clique (ncclCommInitAll); when a device is
  *      listed more than once (or TFIDF_GROUP_LOCAL is set) they exchange through device
- *      copies in this process — same engine code, same results. */
+ *      copies in this process — same engine code, same results.  An error on one rank
+ *      inside the exchange aborts EVERY communicator of the clique, so no peer stays
+ *      blocked in a collective; the other ranks return TFIDF_E_PEER.  An RCCL group is
+ *      unusable after such an abort (close and reopen it); an in-process group starts its
+ *      next tfidf_group_run afresh. */
 #define TFIDF_GROUP_LOCAL 1u
 typedef struct tfidf_group tfidf_group;
 int tfidf_group_open(int nranks, const int* devices, uint32_t flags, tfidf_group** out);
@@ -152,6 +164,11 @@ typedef struct tfidf_run_info {
     double   ms_stage[16];    /* per-stage device times, see tfidf_stage_name() */
     uint32_t nstages;
     uint32_t flags;           /* TFIDF_RUN_* */
+    /* device (re)allocations made by this library in this process since it was loaded
+     * (hipMalloc of the engine's buffers, cumulative, all contexts): a caller timing
+     * steady-state runs reads them before and after and expects no change */
+    uint64_t device_allocs;
+    uint64_t device_alloc_bytes;
 } tfidf_run_info;
 #define TFIDF_RUN_K1_VS   2u  /* slot-keyed tokenize+count kernel (the default path; the general
                                  kernel of TFIDF_K1=general or an unaligned corpus leaves it clear) */
@@ -159,6 +176,8 @@ typedef struct tfidf_run_info {
                                  clear with TFIDF_RUN_K1_VS set: k_tokcount_vs (larger tables) */
 #define TFIDF_RUN_K1_SPLIT 8u /* ... run as k_tok_resolve + k_count_slots (TFIDF_K1=split) */
 int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info);
+/* The same device-allocation counters without a run (process-wide, cumulative). */
+int tfidf_alloc_stats(uint64_t* allocs, uint64_t* bytes);
 const char* tfidf_stage_name(int stage);
 /* Enables per-stage HIP event timing (adds a few event records per run). */
 int tfidf_set_timing(tfidf_ctx* ctx, int enable);

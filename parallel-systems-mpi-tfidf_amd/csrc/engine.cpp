@@ -21,6 +21,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -33,6 +34,23 @@ extern "C" void tfidf_synth_spec(syn_spec* s, uint64_t seed, uint32_t V, uint32_
 
 namespace {
 
+/* every device allocation of the engine goes through dev_malloc: the counters behind
+ * tfidf_run_info.device_allocs / device_alloc_bytes (a steady-state run makes none) */
+std::atomic<uint64_t> g_dev_allocs{0}, g_dev_alloc_bytes{0};
+
+}  // namespace
+
+hipError_t tfidf_dev_malloc(void** p, size_t bytes) {
+    const hipError_t e = hipMalloc(p, bytes);
+    if (e == hipSuccess) {
+        g_dev_allocs.fetch_add(1, std::memory_order_relaxed);
+        g_dev_alloc_bytes.fetch_add(bytes, std::memory_order_relaxed);
+    }
+    return e;
+}
+
+namespace {
+
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
@@ -41,17 +59,22 @@ struct DevBuf {
         if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
         /* 1/8 headroom: sizes that vary a little from run to run (the record total after
          * K1's overflow records) must not reallocate — hipFree synchronises the device and
-         * a 1 GB hipMalloc inside a stage left the GPU idle for ~0.7 ms */
-        size_t want = bytes < 256 ? 256 : bytes + (bytes >= (1u << 20) ? bytes / 8 : 0);
-        if (hipMalloc(&p, want) != hipSuccess) { p = nullptr; return -1; }
-        cap = want;
-        return 0;
+         * a 1 GB hipMalloc inside a stage left the GPU idle for ~0.7 ms.  Near the HBM
+         * capacity the headroom is dropped rather than failing a size that fits exactly. */
+        const size_t want = bytes < 256 ? 256 : bytes + (bytes >= (1u << 20) ? bytes / 8 : 0);
+        if (tfidf_dev_malloc(&p, want) == hipSuccess) { cap = want; return 0; }
+        (void)hipGetLastError();
+        p = nullptr;
+        if (want != bytes && tfidf_dev_malloc(&p, bytes) == hipSuccess) { cap = bytes; return 0; }
+        (void)hipGetLastError();
+        p = nullptr;
+        return -1;
     }
     /* grow preserving the first `keep` bytes */
     int grow_keep(size_t bytes, size_t keep, hipStream_t s) {
         if (bytes <= cap && p) return 0;
         void* q = nullptr;
-        if (hipMalloc(&q, bytes) != hipSuccess) return -1;
+        if (tfidf_dev_malloc(&q, bytes) != hipSuccess) return -1;
         if (p && keep) {
             if (hipMemcpyAsync(q, p, keep, hipMemcpyDeviceToDevice, s) != hipSuccess) return -1;
             if (hipStreamSynchronize(s) != hipSuccess) return -1;
@@ -81,6 +104,9 @@ struct tfidf_ctx {
                                cross-checks and A/B timing */
     bool stamps_on = false; /* env TFIDF_STAMPS=1 with the diagnostic library build */
     uint32_t ablate = 0;    /* env TFIDF_K1_ABLATE: K1 timing experiments, pipeline stops after K1 */
+    int xfail_rank = -1;    /* env TFIDF_TEST_XFAIL_RANK (tests): this rank fails inside the exchange of
+                               its first run, right after the key all-gather (the abort path of
+                               exchange_df) */
     DevBuf stamps;
     bool k1_vs = false;     /* last run used the slot-keyed kernel (default) */
     bool k1_st = false;     /* ... and of those the LDS-staged tokcount_st (else tokcount_vs) */
@@ -226,6 +252,8 @@ int tfidf_open(int device, tfidf_ctx** out) {
     ctx->stamps_on = ks && ks[0] == '1';
     const char* ka = getenv("TFIDF_K1_ABLATE");
     ctx->ablate = ka ? (uint32_t)strtoul(ka, nullptr, 0) : 0u;
+    const char* kx = getenv("TFIDF_TEST_XFAIL_RANK");
+    ctx->xfail_rank = kx ? atoi(kx) : -1;
     /* diagnostics: initial vocabulary capacity (power of two) and the load it may reach
      * before the run is repeated with a larger table (TFIDF_VLOAD percent, default 50) */
     const char* kv = getenv("TFIDF_VCAP");
@@ -377,6 +405,12 @@ static int exchange_collective(tfidf_ctx* ctx, uint32_t V, uint64_t maxv) {
     if (V) HIPCHK(hipMemcpyAsync(ctx->x_send.p, ctx->x_mine.p, (size_t)V * 16, hipMemcpyDeviceToDevice, s));
     int rc = xp->allgather(ctx->x_send.p, ctx->x_recv.p, maxv * 16, s);
     if (rc) return rc;
+    if (ctx->xfail_rank == xp->rank) {   /* tests: a rank-local failure after a collective (once) */
+        ctx->xfail_rank = -1;
+        HIPCHK(hipStreamSynchronize(s));
+        fprintf(stderr, "tfidf: rank %d: injected exchange failure (TFIDF_TEST_XFAIL_RANK)\n", xp->rank);
+        return TFIDF_E_HIP;
+    }
     HIPCHK(hipMemsetAsync(ctx->x_seq0.p, 0, ntot * 4, s));
     uint32_t vm = 0;
     XCHK(key_varying_bytes_u128(ctx->x_recv.as<uint4>(), ntot, &vm, ar, s));
@@ -939,6 +973,9 @@ static int run_prepare(tfidf_ctx* ctx, const tfidf_corpus* in, CorpusDev& c, con
         HIPCHK(hipStreamSynchronize(s));
     }
     if (hi > in->nbytes || lo > hi) return TFIDF_E_INVAL;
+    /* timing ablations stop after K1, before the exchange: single-rank only (with a transport
+     * this error goes through the agreement, so every rank stops) */
+    if (ctx->ablate && ctx->xp) return TFIDF_E_INVAL;
     c.nbytes = in->nbytes;
     c.ndocs = N;
     c.lo = lo;
@@ -1029,9 +1066,9 @@ extern "C" int tfidf_hbm_probe(tfidf_ctx* ctx, uint64_t nbytes, int iters, doubl
     hipStream_t s = ctx->stream;
     void *a = nullptr, *b = nullptr;
     uint32_t* sink = nullptr;
-    if (hipMalloc(&a, nbytes) != hipSuccess) return TFIDF_E_NOMEM;
-    if (hipMalloc(&b, nbytes) != hipSuccess) { (void)hipFree(a); return TFIDF_E_NOMEM; }
-    if (hipMalloc((void**)&sink, 256) != hipSuccess) { (void)hipFree(a); (void)hipFree(b); return TFIDF_E_NOMEM; }
+    if (tfidf_dev_malloc(&a, nbytes) != hipSuccess) return TFIDF_E_NOMEM;
+    if (tfidf_dev_malloc(&b, nbytes) != hipSuccess) { (void)hipFree(a); return TFIDF_E_NOMEM; }
+    if (tfidf_dev_malloc((void**)&sink, 256) != hipSuccess) { (void)hipFree(a); (void)hipFree(b); return TFIDF_E_NOMEM; }
     int ncu = 256, dev = 0;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     const unsigned grid = (unsigned)(ncu > 0 ? ncu : 256) * 16u;
@@ -1065,6 +1102,13 @@ extern "C" int tfidf_hbm_probe(tfidf_ctx* ctx, uint64_t nbytes, int iters, doubl
     return rc;
 }
 
+extern "C" int tfidf_alloc_stats(uint64_t* allocs, uint64_t* bytes) {
+    if (!allocs || !bytes) return TFIDF_E_INVAL;
+    *allocs = g_dev_allocs.load(std::memory_order_relaxed);
+    *bytes = g_dev_alloc_bytes.load(std::memory_order_relaxed);
+    return TFIDF_OK;
+}
+
 extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info) {
     if (!ctx || !info) return TFIDF_E_INVAL;
     if (!ctx->have_info) return TFIDF_E_STATE;
@@ -1084,6 +1128,8 @@ extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info) {
     info->nstages = S_NSTAGES;
     info->flags = (ctx->k1_vs ? TFIDF_RUN_K1_VS : 0u) | (ctx->k1_st ? TFIDF_RUN_K1_ST : 0u) |
                   (ctx->k1_split ? TFIDF_RUN_K1_SPLIT : 0u);
+    info->device_allocs = g_dev_allocs.load(std::memory_order_relaxed);
+    info->device_alloc_bytes = g_dev_alloc_bytes.load(std::memory_order_relaxed);
     return TFIDF_OK;
 }
 

@@ -23,6 +23,7 @@
 #include <string.h>
 
 #include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -35,33 +36,75 @@ namespace {
 
 /* ------------------------------------------------------------------ RCCL -- */
 
+/* The communicators of one tfidf_group clique (ncclCommInitAll in one process).  An error
+ * on one rank after the agreement aborts EVERY communicator of the clique: a peer already
+ * inside an all-gather / all-reduce (or the stream synchronisation after it) is released
+ * by its own communicator's abort, not by the failing rank's.  `mu` orders the enqueue of
+ * a collective against the abort (no collective is enqueued on an aborted communicator);
+ * the synchronisations run outside it, so an abort can happen while a peer waits. */
+struct Clique {
+    std::mutex mu;
+    std::vector<ncclComm_t> comms;
+    bool aborted = false;
+    ~Clique() {
+        for (ncclComm_t c : comms)
+            if (c) (void)ncclCommDestroy(c);
+    }
+    void abort_all() {
+        std::lock_guard<std::mutex> lk(mu);
+        if (aborted) return;
+        aborted = true;
+        for (ncclComm_t& c : comms)
+            if (c) { (void)ncclCommAbort(c); c = nullptr; }
+    }
+};
+
 struct RcclXport final : Xport {
-    ncclComm_t comm = nullptr;
+    ncclComm_t own = nullptr;              /* a single-rank-per-process communicator (tfidf_comm_init) */
+    std::shared_ptr<Clique> clique;        /* ... or this rank's communicator in a group clique */
     int device = 0;
     uint64_t* dwords = nullptr;   /* 2 (send) + 2 * nranks (recv) */
     ~RcclXport() override {
-        if (comm) (void)ncclCommDestroy(comm);
+        if (own) (void)ncclCommDestroy(own);
         if (dwords) (void)hipFree(dwords);
     }
+    /* enqueues f(comm) under the clique lock; TFIDF_E_PEER once the clique was aborted */
+    template <class F> int enqueue(F&& f) {
+        if (clique) {
+            std::lock_guard<std::mutex> lk(clique->mu);
+            if (clique->aborted || !clique->comms[rank]) return TFIDF_E_PEER;
+            return f(clique->comms[rank]) == ncclSuccess ? TFIDF_OK : TFIDF_E_RCCL;
+        }
+        if (!own) return TFIDF_E_STATE;
+        return f(own) == ncclSuccess ? TFIDF_OK : TFIDF_E_RCCL;
+    }
+    /* a synchronisation that an abort of the clique released reports TFIDF_E_PEER */
+    int sync(hipStream_t s) {
+        const hipError_t e = hipStreamSynchronize(s);
+        if (clique) {
+            std::lock_guard<std::mutex> lk(clique->mu);
+            if (clique->aborted) return TFIDF_E_PEER;
+        }
+        return e == hipSuccess ? TFIDF_OK : TFIDF_E_HIP;
+    }
     int words(const uint64_t mine[2], uint64_t* all, hipStream_t s) override {
-        if (!comm) return TFIDF_E_STATE;
-        if (!dwords && hipMalloc((void**)&dwords, 16 * (size_t)(nranks + 1)) != hipSuccess) return TFIDF_E_NOMEM;
+        if (!dwords && tfidf_dev_malloc((void**)&dwords, 16 * (size_t)(nranks + 1)) != hipSuccess) return TFIDF_E_NOMEM;
         if (hipMemcpyAsync(dwords, mine, 16, hipMemcpyHostToDevice, s) != hipSuccess) return TFIDF_E_HIP;
-        if (ncclAllGather(dwords, dwords + 2, 2, ncclUint64, comm, s) != ncclSuccess) return TFIDF_E_RCCL;
+        int rc = enqueue([&](ncclComm_t c) { return ncclAllGather(dwords, dwords + 2, 2, ncclUint64, c, s); });
+        if (rc) return rc;
         if (hipMemcpyAsync(all, dwords + 2, 16 * (size_t)nranks, hipMemcpyDeviceToHost, s) != hipSuccess)
             return TFIDF_E_HIP;
-        return hipStreamSynchronize(s) == hipSuccess ? TFIDF_OK : TFIDF_E_HIP;
+        return sync(s);
     }
     int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
-        if (!comm) return TFIDF_E_STATE;
-        return ncclAllGather(send, recv, bytes, ncclUint8, comm, s) == ncclSuccess ? TFIDF_OK : TFIDF_E_RCCL;
+        return enqueue([&](ncclComm_t c) { return ncclAllGather(send, recv, bytes, ncclUint8, c, s); });
     }
     int allreduce_sum_u32(uint32_t* buf, size_t n, hipStream_t s) override {
-        if (!comm) return TFIDF_E_STATE;
-        return ncclAllReduce(buf, buf, n, ncclUint32, ncclSum, comm, s) == ncclSuccess ? TFIDF_OK : TFIDF_E_RCCL;
+        return enqueue([&](ncclComm_t c) { return ncclAllReduce(buf, buf, n, ncclUint32, ncclSum, c, s); });
     }
     void abort() override {
-        if (comm) { (void)ncclCommAbort(comm); comm = nullptr; }
+        if (clique) clique->abort_all();
+        else if (own) { (void)ncclCommAbort(own); own = nullptr; }
     }
     const char* name() const override { return "rccl"; }
 };
@@ -96,6 +139,13 @@ struct Hub {
         std::lock_guard<std::mutex> lk(mu);
         poisoned = true;
         cv.notify_all();
+    }
+    /* before a new group run, when no rank is inside the hub: an abort of the previous run
+     * does not poison this one */
+    void reset() {
+        std::lock_guard<std::mutex> lk(mu);
+        poisoned = false;
+        arrived = 0;
     }
 };
 
@@ -142,7 +192,7 @@ struct LocalXport final : Xport {
             if (tmp) (void)hipFree(tmp);
             tmp = nullptr;
             tmp_cap = 0;
-            if (hipMalloc((void**)&tmp, need) != hipSuccess) { abort(); return TFIDF_E_NOMEM; }
+            if (tfidf_dev_malloc((void**)&tmp, need) != hipSuccess) { abort(); return TFIDF_E_NOMEM; }
             tmp_cap = need;
         }
         int rc = allgather(buf, tmp, n * 4, s);
@@ -158,7 +208,7 @@ struct LocalXport final : Xport {
 
 Xport* make_rccl_xport(void* nccl_comm, int rank, int nranks, int device) {
     RcclXport* x = new RcclXport();
-    x->comm = (ncclComm_t)nccl_comm;
+    x->own = (ncclComm_t)nccl_comm;
     x->rank = rank;
     x->nranks = nranks;
     x->device = device;
@@ -210,15 +260,19 @@ int tfidf_group_open(int nranks, const int* devices, uint32_t flags, tfidf_group
         }
     } else if (!rc) {
         /* one RCCL communicator per GPU of the clique (a 1-rank group gets one too, so the
-         * exchange path is the same at every size) */
-        std::vector<ncclComm_t> comms((size_t)nranks, nullptr);
-        if (ncclCommInitAll(comms.data(), nranks, dev.data()) != ncclSuccess) rc = TFIDF_E_RCCL;
+         * exchange path is the same at every size), owned by the clique so that an error on
+         * one rank aborts them all */
+        auto cl = std::make_shared<Clique>();
+        cl->comms.assign((size_t)nranks, nullptr);
+        if (ncclCommInitAll(cl->comms.data(), nranks, dev.data()) != ncclSuccess) rc = TFIDF_E_RCCL;
         for (int r = 0; r < nranks && !rc; ++r) {
-            rc = tfidf_ctx_attach_xport(g->ctx[r], make_rccl_xport(comms[r], r, nranks, dev[r]));
-            comms[r] = nullptr;
+            RcclXport* x = new RcclXport();
+            x->clique = cl;
+            x->rank = r;
+            x->nranks = nranks;
+            x->device = dev[r];
+            rc = tfidf_ctx_attach_xport(g->ctx[r], x);
         }
-        for (ncclComm_t c : comms)
-            if (c) (void)ncclCommDestroy(c);
     }
     if (rc) {
         tfidf_group_close(g);
@@ -237,6 +291,7 @@ tfidf_ctx* tfidf_group_ctx(tfidf_group* g, int rank) {
 int tfidf_group_run(tfidf_group* g, const tfidf_corpus* shards) {
     if (!g || !shards) return TFIDF_E_INVAL;
     std::vector<int> rc((size_t)g->n, TFIDF_OK);
+    if (g->hub) g->hub->reset();   /* in-process ranks: a new run starts unpoisoned */
     std::vector<std::thread> th;
     for (int r = 1; r < g->n; ++r) th.emplace_back([&, r] { rc[r] = tfidf_run(g->ctx[r], &shards[r]); });
     rc[0] = tfidf_run(g->ctx[0], &shards[0]);

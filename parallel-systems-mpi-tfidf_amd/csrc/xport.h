@@ -46,6 +46,9 @@ int tfidf_ctx_attach_xport(tfidf_ctx* ctx, Xport* xp);
 int tfidf_ctx_device(const tfidf_ctx* ctx);
 hipStream_t tfidf_ctx_stream(const tfidf_ctx* ctx);
 
+/* engine.cpp: hipMalloc counted in tfidf_run_info.device_allocs / device_alloc_bytes */
+hipError_t tfidf_dev_malloc(void** p, size_t bytes);
+
 /* group.cpp */
 Xport* make_rccl_xport(void* nccl_comm, int rank, int nranks, int device);   /* takes the comm */
 int launch_sum_rows_u32(const uint32_t* rows, uint32_t nrows, uint64_t n, uint32_t* out, hipStream_t s);

@@ -217,7 +217,10 @@ int main(int argc, char** argv) {
     const int visible = tfidf_device_count();
     if (visible <= 0) return fail(TFIDF_E_NODEV);
     if (device >= 0) ngpus = 1;                 /* --device D: one GPU, that one */
-    if (ngpus <= 0 || ngpus > visible) ngpus = visible;
+    /* default: ONE GPU.  Several GPUs (an RCCL clique over xGMI) only when asked for with
+     * --gpus N: the multi-GPU path is validated on the driver's 8-GPU node, not here */
+    if (ngpus <= 0) ngpus = 1;
+    if (ngpus > visible) ngpus = visible;
     if (nshards <= 0) nshards = ngpus;
     if (nshards == 1) return run_single(device >= 0 ? device : 0, indir, outpath, debug, stats);
     if (device > 0) return fail(TFIDF_E_INVAL);   /* several shards use devices 0..N-1 */

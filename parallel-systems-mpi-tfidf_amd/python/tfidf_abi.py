@@ -27,7 +27,7 @@ RUN_K1_SPLIT = 8  # ... run as k_tok_resolve + k_count_slots (TFIDF_K1=split)
 # exported symbols declared by include/tfidf.h
 EXPORTS = [
     "tfidf_open", "tfidf_close", "tfidf_strerror", "tfidf_abi_version", "tfidf_comm_unique_id",
-    "tfidf_comm_init", "tfidf_run", "tfidf_fetch", "tfidf_result_free", "tfidf_last_run_info",
+    "tfidf_comm_init", "tfidf_run", "tfidf_fetch", "tfidf_result_free", "tfidf_last_run_info", "tfidf_alloc_stats",
     "tfidf_stage_name", "tfidf_set_timing", "tfidf_write_output", "tfidf_print_jobs",
     "tfidf_ingest_dir", "tfidf_free", "tfidf_synth_host", "tfidf_synth_device",
     "tfidf_format", "tfidf_copy_text", "tfidf_write_output_gpu", "tfidf_format_f64",
@@ -64,6 +64,7 @@ class RunInfo(C.Structure):
         ("nterms_global", C.c_uint32), ("nchunks", C.c_uint64), ("partial_records", C.c_uint64),
         ("ndocs", C.c_uint32), ("vocab_capacity", C.c_uint32), ("ms_total", C.c_double),
         ("ms_tokcount", C.c_double), ("ms_stage", C.c_double * 16), ("nstages", C.c_uint32), ("flags", C.c_uint32),
+        ("device_allocs", C.c_uint64), ("device_alloc_bytes", C.c_uint64),
     ]
 
 
@@ -100,6 +101,7 @@ def lib() -> C.CDLL:
         L.tfidf_result_free.argtypes = [C.POINTER(Result)]
         L.tfidf_result_free.restype = None
         L.tfidf_last_run_info.argtypes = [C.c_void_p, C.POINTER(RunInfo)]
+        L.tfidf_alloc_stats.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.tfidf_stage_name.restype = C.c_char_p
         L.tfidf_set_timing.argtypes = [C.c_void_p, C.c_int]
         L.tfidf_comm_unique_id.argtypes = [C.c_void_p]
@@ -250,6 +252,12 @@ class Engine:
         if hip.hipMemcpy(off.ctypes.data, c.doc_off, off.nbytes, 2) != 0:
             raise RuntimeError("hipMemcpy D2H failed")
         return out, off
+
+    def alloc_counters(self):
+        """(device allocations, bytes) the library has made in this process so far."""
+        a, b = C.c_uint64(), C.c_uint64()
+        _chk(lib().tfidf_alloc_stats(C.byref(a), C.byref(b)), "tfidf_alloc_stats")
+        return int(a.value), int(b.value)
 
     def info(self) -> dict:
         r = RunInfo()

@@ -136,6 +136,25 @@ def test_group_error_releases_peers():
         g.run_host(_shards("c2", 0.001, 2))
 
 
+@pytest.mark.parametrize("failing", [0, 1, 2])
+def test_exchange_failure_after_allgather_aborts_peers(failing, monkeypatch):
+    """A rank-local failure INSIDE the exchange (after the key all-gather, past the
+    agreement: TFIDF_TEST_XFAIL_RANK) aborts the transport; the peers, already on their way
+    into the DF all-reduce, return TFIDF_E_PEER instead of waiting, the group reports the
+    failing rank's own error, and the next run of the group starts afresh (the in-process
+    hub is reset).  The same engine path (exchange_df -> Xport::abort) aborts every RCCL
+    communicator of a clique."""
+    shards = _shards("c2", 0.001, 3)
+    monkeypatch.setenv("TFIDF_TEST_XFAIL_RANK", str(failing))   # read by tfidf_open; fires once
+    with tfidf_abi.Group(3, devices=[0, 0, 0]) as g:
+        with pytest.raises(tfidf_abi.TfidfError) as ei:
+            g.run_host(shards)
+        assert ei.value.rc == -3   # TFIDF_E_HIP, the failing rank's own error (the others: E_PEER)
+        g.run_host(shards)         # the same group again: the hub's poison was reset
+        ora = _full("c2", 0.001)
+        assert b"".join(g.ranks[r].text() for r in range(3)) == ora["output_txt"]
+
+
 def test_rccl_single_rank_runs_the_exchange():
     """A 1-rank RCCL communicator: exchange_df runs (agreement, ncclAllGather of the keys,
     union, ncclAllReduce) and the results are unchanged."""
