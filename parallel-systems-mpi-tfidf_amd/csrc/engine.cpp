@@ -100,7 +100,7 @@ struct tfidf_ctx {
     int rank = 0, nranks = 1;
     bool timing = true;
     int k1_mode = 0;        /* 0 auto (fused LDS-staged tokcount_st), 1 round-1 kernel (TFIDF_K1=vs),
-                               2 general K1 (TFIDF_K1=general), 3 split K1a + K1b (TFIDF_K1=split):
+                               2 general K1 (TFIDF_K1=general), 4 round-2 kernel (TFIDF_K1=st):
                                cross-checks and A/B timing */
     bool stamps_on = false; /* env TFIDF_STAMPS=1 with the diagnostic library build */
     uint32_t ablate = 0;    /* env TFIDF_K1_ABLATE: K1 timing experiments, pipeline stops after K1 */
@@ -110,7 +110,9 @@ struct tfidf_ctx {
     DevBuf stamps;
     bool k1_vs = false;     /* last run used the slot-keyed kernel (default) */
     bool k1_st = false;     /* ... and of those the LDS-staged tokcount_st (else tokcount_vs) */
-    bool k1_split = false;  /* ... or the split k_tok_resolve + k_count_slots */
+    bool k1_lean = false;   /* ... or k_tokcount_lean (the default up to K1_ST_MAX_CAP slots) */
+    LeanParams* lp_host = nullptr;   /* pinned staging of k_tokcount_lean's parameter block */
+    DevBuf lp_dev;
     hipEvent_t ev[S_NSTAGES + 1];
     Arena arena;
     DevBuf arena_buf;
@@ -126,7 +128,6 @@ struct tfidf_ctx {
     DevBuf syn_bytes, syn_off, syn_ids, syn_ntok, syn_blkfirst, syn_blkbytes, syn_cdf;
     /* stage buffers */
     DevBuf chunk_start, chunk_doc;
-    DevBuf tokstream, chunk_meta, tok_dlist, tok_dtok;   /* split K1 */
     DevBuf vkeys, vrep;
     /* vocabulary table: K1 is measurably faster at low load (fewer displaced keys behind
      * the two slots it loads per token): 1M slots (16 MB) to start, x4 past 12 % load */
@@ -247,7 +248,7 @@ int tfidf_open(int device, tfidf_ctx** out) {
     const char* km = getenv("TFIDF_K1");
     if (km && !strcmp(km, "general")) ctx->k1_mode = 2;
     if (km && !strcmp(km, "vs")) ctx->k1_mode = 1;
-    if (km && !strcmp(km, "split")) ctx->k1_mode = 3;
+    if (km && !strcmp(km, "st")) ctx->k1_mode = 4;
     const char* ks = getenv("TFIDF_STAMPS");
     ctx->stamps_on = ks && ks[0] == '1';
     const char* ka = getenv("TFIDF_K1_ABLATE");
@@ -279,6 +280,8 @@ int tfidf_open(int device, tfidf_ctx** out) {
     if (arena_reset(ctx, 64ull << 20) != 0) { delete ctx; return TFIDF_E_NOMEM; }
     if (ctx->counters.ensure(256) != 0) { delete ctx; return TFIDF_E_NOMEM; }
     if (hipHostMalloc((void**)&ctx->hpin, 256, hipHostMallocDefault) != hipSuccess) { delete ctx; return TFIDF_E_NOMEM; }
+    if (hipHostMalloc((void**)&ctx->lp_host, sizeof(LeanParams), hipHostMallocDefault) != hipSuccess ||
+        ctx->lp_dev.ensure(sizeof(LeanParams)) != 0) { delete ctx; return TFIDF_E_NOMEM; }
     *out = ctx;
     return TFIDF_OK;
 }
@@ -294,8 +297,7 @@ void tfidf_close(tfidf_ctx* ctx) {
     ctx->arena2_buf.release();
     DevBuf* bufs[] = {&ctx->arena_buf, &ctx->in_bytes, &ctx->in_off, &ctx->in_ids, &ctx->syn_bytes, &ctx->syn_off,
                       &ctx->syn_ids, &ctx->syn_ntok, &ctx->syn_blkfirst, &ctx->syn_blkbytes, &ctx->syn_cdf,
-                      &ctx->chunk_start, &ctx->chunk_doc, &ctx->tokstream, &ctx->chunk_meta, &ctx->tok_dlist,
-                      &ctx->tok_dtok, &ctx->vkeys, &ctx->vrep, &ctx->rec_slot, &ctx->rec_cnt,
+                      &ctx->chunk_start, &ctx->chunk_doc, &ctx->vkeys, &ctx->vrep, &ctx->rec_slot, &ctx->rec_cnt,
                       &ctx->part_doc, &ctx->part_slot, &ctx->part_cnt, &ctx->doc_recoff, &ctx->doc_npairs,
                       &ctx->doc_size, &ctx->doc_flags, &ctx->counters, &ctx->dense, &ctx->vslot, &ctx->skey0,
                       &ctx->skey1, &ctx->seq0, &ctx->seq1, &ctx->rank_of_slot, &ctx->slot_of_rank, &ctx->rank16, &ctx->pkey0,
@@ -310,6 +312,8 @@ void tfidf_close(tfidf_ctx* ctx) {
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i <= S_NSTAGES; ++i) (void)hipEventDestroy(ctx->ev[i]);
     if (ctx->hpin) (void)hipHostFree(ctx->hpin);
+    if (ctx->lp_host) (void)hipHostFree(ctx->lp_host);
+    ctx->lp_dev.release();
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -509,7 +513,7 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     /* K1 variant: the slot-keyed kernel (tokcount_vs.hip) needs a 16-byte aligned corpus
      * base; TFIDF_K1=general selects the general kernel (cross-checks) */
     const bool aligned = (((uintptr_t)c.bytes & 15u) == 0);
-    ctx->k1_vs = aligned && (ctx->k1_mode <= 1 || ctx->k1_mode == 3);
+    ctx->k1_vs = aligned && (ctx->k1_mode <= 1 || ctx->k1_mode == 4);
     if (ctx->k1_vs && ctx->vcap > K1_VS_MAX_CAP) return TFIDF_E_CAPACITY;
     /* ---- K1 ---- */
     mark(ctx, S_TOKCOUNT);
@@ -543,25 +547,21 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
      * K1_ST_MAX_CAP slots (config 4: ~1e7 terms, nearly every token a new (doc, term) pair)
      * its bucketed LDS count table runs full and the round-1 kernel is 2.3x faster (c4:
      * 11.5 vs 26.2 ms) */
-    ctx->k1_split = ctx->k1_vs && ctx->k1_mode == 3;
-    ctx->k1_st = ctx->k1_vs && ctx->k1_mode == 0 && ctx->vcap <= K1_ST_MAX_CAP;
-    if (nchunks && ctx->k1_split) {
-        /* K1a's token stream: span/2 + N + 4 per chunk words bound the tokens (tokcount_split.hip) */
-        const uint64_t tw = tokcount_split_words(span, N, nchunks);
-        ENSURE(ctx->tokstream, tw * 4 + 256);
-        ENSURE(ctx->chunk_meta, (nchunks + 1) * 8);
-        ENSURE(ctx->tok_dlist, ((size_t)N + nchunks + 2) * 4);
-        ENSURE(ctx->tok_dtok, ((size_t)N + nchunks + 2) * 4);
-        K1Split sp{};
-        sp.tok = ctx->tokstream.as<uint32_t>();
-        sp.tok_words = tw;
-        sp.chunk_meta = ctx->chunk_meta.as<uint2>();
-        sp.dlist = ctx->tok_dlist.as<uint32_t>();
-        sp.dtok = ctx->tok_dtok.as<uint32_t>();
-        sp.shard_a = cnt + 16;
-        sp.shard_b = cnt + 24;
-        LCHK(launch_tokcount_split(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), nchunks, vd, o,
-                                   sp, s));
+    ctx->k1_lean = ctx->k1_vs && ctx->k1_mode == 0 && ctx->vcap <= K1_ST_MAX_CAP;
+    ctx->k1_st = ctx->k1_vs && ctx->k1_mode == 4 && ctx->vcap <= K1_ST_MAX_CAP;
+    if (nchunks && ctx->k1_lean) {
+        LeanParams& lp = *ctx->lp_host;
+        lp.c = c;
+        lp.v = vd;
+        lp.o = o;
+        lp.chunk_start = ctx->chunk_start.as<uint64_t>();
+        lp.chunk_doc = ctx->chunk_doc.as<uint32_t>();
+        lp.c0 = 0;
+        lp.c1 = nchunks;
+        /* pinned source: the copy is stream-ordered before the launch and the block is not
+         * rewritten before the next run's copy (which follows this kernel on the stream) */
+        HIPCHK(hipMemcpyAsync(ctx->lp_dev.p, &lp, sizeof(LeanParams), hipMemcpyHostToDevice, s));
+        LCHK(launch_tokcount_lean(ctx->lp_dev.as<LeanParams>(), lp, s));
     } else if (nchunks && ctx->k1_st)
         LCHK(launch_tokcount_st(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
     else if (nchunks && ctx->k1_vs)
@@ -1043,19 +1043,6 @@ extern "C" int tfidf_debug_k1_stamps(tfidf_ctx* ctx, uint64_t* out, int n) {
     return m;
 }
 
-/* Diagnostics of the split K1 (tests/debug scripts only): copies the first n words of the
- * last run's token stream (0), chunk metadata (1: 2 words per chunk), ordinal document list
- * (2) or ordinal first-token indices (3) to the host. */
-extern "C" int tfidf_debug_split(tfidf_ctx* ctx, int what, uint32_t* out, uint64_t n) {
-    if (!ctx || !out) return TFIDF_E_INVAL;
-    DevBuf* b = what == 0 ? &ctx->tokstream : what == 1 ? &ctx->chunk_meta : what == 2 ? &ctx->tok_dlist
-              : what == 3 ? &ctx->tok_dtok : nullptr;
-    if (!b || !b->p) return TFIDF_E_STATE;
-    if (n * 4 > b->cap) n = b->cap / 4;
-    HIPCHK(hipMemcpy(out, b->p, 4 * (size_t)n, hipMemcpyDeviceToHost));
-    return (int)n;
-}
-
 /* Measured HBM streaming peaks: `iters` timed passes of a read-only stream
  * over nbytes and of an nbytes copy (counted as 2 x nbytes), after one warm-up pass each;
  * the buffers are allocated for the call and released. */
@@ -1127,7 +1114,7 @@ extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info) {
     for (int i = 0; i < S_NSTAGES; ++i) info->ms_stage[i] = ctx->ms_stage[i];
     info->nstages = S_NSTAGES;
     info->flags = (ctx->k1_vs ? TFIDF_RUN_K1_VS : 0u) | (ctx->k1_st ? TFIDF_RUN_K1_ST : 0u) |
-                  (ctx->k1_split ? TFIDF_RUN_K1_SPLIT : 0u);
+                  (ctx->k1_lean ? TFIDF_RUN_K1_LEAN : 0u);
     info->device_allocs = g_dev_allocs.load(std::memory_order_relaxed);
     info->device_alloc_bytes = g_dev_alloc_bytes.load(std::memory_order_relaxed);
     return TFIDF_OK;

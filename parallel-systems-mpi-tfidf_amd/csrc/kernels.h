@@ -99,21 +99,21 @@ int launch_tokcount_vs(const CorpusDev& c, const uint64_t* chunk_start, const ui
                        uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s);
 #define K1_VS_MAX_CAP (1ull << 28)
 
-/* K1 split into K1a (tokenize + vocabulary resolve -> token stream) and K1b (LDS count of the
- * stream -> records), tokcount_split.hip: TFIDF_K1=split (measured slower than tokcount_st) */
-struct K1Split {
-    uint32_t* tok;                   /* token stream: (ordinal mod G) << sb | slot per token */
-    uint64_t tok_words;              /* its capacity (tokcount_split_words) */
-    uint2* chunk_meta;               /* per chunk: (tokens, documents with tokens) */
-    uint32_t* dlist;                 /* [chunk_doc[c] + c + k]: document of ordinal k */
-    uint32_t* dtok;                  /* ... and the chunk index of its first token */
-    unsigned long long* shard_a;     /* 8 sharded chunk counters of K1a (zeroed per run) */
-    unsigned long long* shard_b;     /* ... of K1b */
-};
-int launch_tokcount_split(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc, uint64_t nch,
-                          const VocabDev& v, const K1Out& o, const K1Split& sp, hipStream_t s);
-uint64_t tokcount_split_words(uint64_t span, uint64_t ndocs, uint64_t nch);
 #define K1_ST_MAX_CAP (1ull << 22)   /* tokcount_st up to this vocabulary capacity, tokcount_vs beyond */
+
+/* K1 lean (tokcount_lean.hip): the default tokenize+count kernel up to K1_ST_MAX_CAP.  Its
+ * rarely used pointers and sizes are read from this block in device memory where they are
+ * used (scalar loads), not held in registers; `h` is the same block on the host (the
+ * launcher reads the hot fields from it).  Requires c0 == 0, a 16-byte aligned corpus. */
+struct LeanParams {
+    CorpusDev c;
+    VocabDev v;
+    K1Out o;
+    const uint64_t* chunk_start;
+    const uint32_t* chunk_doc;
+    uint64_t c0, c1;
+};
+int launch_tokcount_lean(const LeanParams* dparams, const LeanParams& h, hipStream_t s);
 
 /* vocabulary finalisation */
 int launch_vocab_flags(const VocabDev& v, uint64_t cap, uint32_t* flags, hipStream_t s);

@@ -22,7 +22,7 @@ TFIDF_CORPUS_DEVICE = 1
 UNIQUE_ID_BYTES = 128
 RUN_K1_VS = 2   # tfidf_run_info.flags (include/tfidf.h): slot-keyed K1 ...
 RUN_K1_ST = 4   # ... run as k_tokcount_st (else k_tokcount_vs)
-RUN_K1_SPLIT = 8  # ... run as k_tok_resolve + k_count_slots (TFIDF_K1=split)
+RUN_K1_LEAN = 16  # ... run as k_tokcount_lean (default; TFIDF_K1=st: k_tokcount_st)
 
 # exported symbols declared by include/tfidf.h
 EXPORTS = [
