@@ -148,6 +148,71 @@ def cpu_baseline(cfg: str, ndocs_sample: int, threads: int, info: dict):
     return out
 
 
+def main_shards(args):
+    """K shards of one config on one GPU through tfidf_group (LocalXport): the exchange
+    stage (key all-gather by device copies, union sort, DF all-reduce) at K ranks."""
+    K = args.shards
+    g = tfidf_abi.Group(K, devices=[0] * K)
+    corpora, plans = [], []
+    for r in range(K):
+        p = tfidf_configs.plan(args.config, scale=args.scale, rank=r, nranks=K, weak=False)
+        plans.append(p)
+        corpora.append(g.ranks[r].synth_device(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"],
+                                               p["ndocs_total"]))
+        g.ranks[r].set_timing(True)
+    hip_device_sync()
+    tc = time.perf_counter()
+    g.run(corpora)
+    hip_device_sync()
+    cold_ms = (time.perf_counter() - tc) * 1e3
+    for _ in range(max(0, args.warmup - 1)):
+        g.run(corpora)
+    hip_device_sync()
+    a0 = g.ranks[0].alloc_counters()
+    steps = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        g.run(corpora)
+        steps.append([e.info() for e in g.ranks])
+    hip_device_sync()
+    elapsed = time.perf_counter() - t0
+    a1 = g.ranks[0].alloc_counters()
+    infos = steps[-1]
+    C_all = sum(i["nbytes"] for i in infos)
+    P_all = sum(i["npairs"] for i in infos)
+    stage_names = list(infos[0]["stages"].keys())
+    # per step: the slowest rank's time of each stage (the ranks meet in the exchange)
+    st_max = {k: float(np.mean([max(i["stages"][k] for i in st) for st in steps])) for k in stage_names}
+    line = {
+        "metric": "corpus GB/s (TF-IDF hot path, K shards on one GPU: multi-rank path incl. the DF exchange)",
+        "value": round(C_all * args.steps / elapsed / 1e9, 4),
+        "unit": "GB/s",
+        "n_gpus": 1,
+        "shards": K,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "data": "synthetic (device-generated Zipfian corpus), resident in HBM",
+        "config": {"workload": f"{args.config} x{args.scale}: {sum(len(p['doc_ids']) for p in plans)} docs in {K} "
+                               f"shards, V={plans[0]['V']}, {C_all / 1e9:.3f} GB, {P_all} pairs",
+                   "parallelism": f"{K} ranks on 1 GPU (in-process transport: the key all-gather and DF "
+                                  f"all-reduce are device copies; xGMI time excluded)"},
+        "stage_ms_max_over_ranks_mean": {k: round(v, 4) for k, v in st_max.items()},
+        "exchange_ms": round(st_max.get("exchange", 0.0), 4),
+        "exchange_frac_of_step": round(st_max.get("exchange", 0.0) / (elapsed / args.steps * 1e3), 4),
+        "nterms_global": int(infos[0]["nterms_global"]),
+        "nterms_per_rank": [int(i["nterms"]) for i in infos],
+        "device_allocs_in_timed_steps": a1[0] - a0[0],
+        "cold_run_ms": round(cold_ms, 3),
+        "note": "ranks run concurrently on one GPU (host thread each); a rank's stage times include waiting "
+                "for its peers at the exchange",
+    }
+    print(json.dumps(line), flush=True)
+    g.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -165,7 +230,13 @@ def main():
     ap.add_argument("--no-probe", action="store_true", help="skip the measured HBM read/copy peak probe")
     ap.add_argument("--no-emit", action="store_true", help="skip the (untimed) output-emission measurement")
     ap.add_argument("--vocab", type=int, default=0, help="diagnostics only: override the config's vocabulary size")
+    ap.add_argument("--shards", type=int, default=0,
+                    help="K >= 2: the config's corpus cut into K byte-balanced shards run by K contexts on ONE "
+                         "GPU (tfidf_group, in-process transport): measures the multi-rank path and the DF "
+                         "exchange (xGMI time excluded); not the headline line")
     args = ap.parse_args()
+    if args.shards >= 2:
+        return main_shards(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

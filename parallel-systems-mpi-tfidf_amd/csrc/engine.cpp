@@ -57,11 +57,13 @@ struct DevBuf {
     int ensure(size_t bytes) {
         if (bytes <= cap && p) return 0;
         if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
-        /* 1/8 headroom: sizes that vary a little from run to run (the record total after
-         * K1's overflow records) must not reallocate — hipFree synchronises the device and
-         * a 1 GB hipMalloc inside a stage left the GPU idle for ~0.7 ms.  Near the HBM
-         * capacity the headroom is dropped rather than failing a size that fits exactly. */
-        const size_t want = bytes < 256 ? 256 : bytes + (bytes >= (1u << 20) ? bytes / 8 : 0);
+        /* 1/8 headroom (at least 4 KiB): sizes that vary a little from run to run (the
+         * record totals after K1's overflow records, the partial-record sort buffers) must
+         * not reallocate in steady state — hipFree synchronises the device and a 1 GB
+         * hipMalloc inside a stage left the GPU idle for ~0.7 ms (the bench counts
+         * allocations in its timed steps).  Near the HBM capacity the headroom is dropped
+         * rather than failing a size that fits exactly. */
+        const size_t want = bytes < 256 ? 256 : bytes + (bytes / 8 > 4096 ? bytes / 8 : 4096);
         if (tfidf_dev_malloc(&p, want) == hipSuccess) { cap = want; return 0; }
         (void)hipGetLastError();
         p = nullptr;

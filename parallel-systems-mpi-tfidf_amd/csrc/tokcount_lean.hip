@@ -470,7 +470,11 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_lean(const LeanParam
     /* Pg without __restrict__ from here on: its fields are read where used, never hoisted */
     const LeanParams* P = Pg;
     asm volatile("" : "+s"(P));
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    /* the wave index as a scalar: the step loop, the document walk and every position
+     * derived from them are then wave-uniform SGPR arithmetic and scalar branches, not
+     * exec-masked VALU (threadIdx-derived values are divergent to the compiler) */
+    const uint32_t wid = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
 
     for (int j = 0; j < EPT; ++j) { S.TK[j * NT + tid] = 0u; S.TC[j * NT + tid] = 0u; }
     if (tid < 64) {
@@ -493,8 +497,9 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_lean(const LeanParam
     auto resolve = [&](const Round& r) -> uint32_t {
         const uint32_t len = (r.e >> 10) & 31u;
         const bool valid = r.e != 0u;
-        const bool hit0 = r.s4.x == r.k0 && r.s4.y == r.k1 && r.s4.z == r.k2 && r.s4.w == r.k3;
-        const bool hit1 = r.t4.x == r.k0 && r.t4.y == r.k1 && r.t4.z == r.k2 && r.t4.w == r.k3;
+        /* bitwise compares (xor / or3): no short-circuit branches on the exec mask */
+        const bool hit0 = ((r.s4.x ^ r.k0) | (r.s4.y ^ r.k1) | (r.s4.z ^ r.k2) | (r.s4.w ^ r.k3)) == 0u;
+        const bool hit1 = ((r.t4.x ^ r.k0) | (r.t4.y ^ r.k1) | (r.t4.z ^ r.k2) | (r.t4.w ^ r.k3)) == 0u;
         uint32_t slot = hit0 ? r.hv : ((r.hv + 1) & vmask);
         const bool rare = valid && (len == LEN_LONG || (!hit0 && !hit1));
         if (__ballot(rare) != 0ull) {

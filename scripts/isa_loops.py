@@ -1,30 +1,41 @@
 #!/usr/bin/env python3
-"""Loop census of one kernel in a hipcc -S listing: for every backward branch (loop
-latch) the line span, instruction count and counts of VALU / SALU / spill traffic inside.
+"""Per-loop census of one kernel in a `hipcc --cuda-device-only -S` listing: every basic
+block is attributed to its innermost loop (LLVM's "Loop: Header=... Depth=..." block
+comments); for each loop header: depth, instructions, VALU, SALU, spill traffic
+(v_readlane/v_writelane, scratch), LDS and VMEM instructions of the blocks directly in it.
     python3 scripts/isa_loops.py file.s kernel_symbol_prefix"""
 import re
 import sys
+from collections import defaultdict
 
 lines = open(sys.argv[1]).read().split("\n")
-start = next(i for i, l in enumerate(lines) if l.startswith(sys.argv[2]) and ":" in l and not l.startswith("\t"))
+start = next(i for i, l in enumerate(lines) if l.startswith(sys.argv[2]) and ":" in l)
 end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
-body = lines[start:end + 1]
-labels = {}
-for i, l in enumerate(body):
-    m = re.match(r"^(\.LBB\d+_\d+):", l)
+cur = ("<top>", 0)
+stats = defaultdict(lambda: defaultdict(int))
+for l in lines[start:end + 1]:
+    m = re.match(r"^(\.LBB\d+_\d+|; %bb\.\d+):.*?(?:Header=(BB\d+_\d+) Depth=(\d+))?\s*$", l)
     if m:
-        labels[m.group(1)] = i
-loops = []
-for i, l in enumerate(body):
-    m = re.search(r"s_cbranch_\w+\s+(\.LBB\d+_\d+)|s_branch\s+(\.LBB\d+_\d+)", l)
-    if m:
-        t = m.group(1) or m.group(2)
-        if t in labels and labels[t] < i:
-            loops.append((labels[t], i, t))
-def cnt(a, b):
-    ins = [x.strip() for x in body[a:b + 1] if re.match(r"^\s+[a-z_]", x)]
-    c = lambda p: sum(1 for x in ins if re.match(p, x))
-    return len(ins), c(r"v_"), c(r"s_"), c(r"v_readlane|v_writelane"), c(r"scratch_"), c(r"ds_"), c(r"global_|buffer_")
-print("%6s %6s %-12s %5s %5s %5s %5s %5s %5s %5s" % ("from", "to", "label", "ins", "valu", "salu", "rdln", "scr", "ds", "vmem"))
-for a, b, t in sorted(loops, key=lambda x: (x[1] - x[0])):
-    print("%6d %6d %-12s %5d %5d %5d %5d %5d %5d %5d" % ((a + start + 1, b + start + 1, t) + cnt(a, b)))
+        if m.group(2):
+            cur = (m.group(2), int(m.group(3)))
+        elif "Loop Header" in l or "Parent Loop" in l:
+            mm = re.search(r"Depth=(\d+)", l)
+            name = m.group(1).lstrip(".L")
+            cur = (name, int(mm.group(1)) if mm else 1)
+        else:
+            cur = ("<top>", 0)
+        continue
+    m = re.match(r"^\s+([a-z_][a-z0-9_]*)", l)
+    if not m:
+        continue
+    op = m.group(1)
+    s = stats[cur]
+    s["ins"] += 1
+    s["valu"] += op.startswith("v_")
+    s["salu"] += op.startswith("s_")
+    s["spill"] += op in ("v_readlane_b32", "v_writelane_b32") or op.startswith("scratch_")
+    s["ds"] += op.startswith("ds_")
+    s["vmem"] += op.startswith(("global_", "buffer_", "flat_"))
+print("%-14s %5s %6s %6s %6s %6s %5s %5s" % ("loop", "depth", "ins", "valu", "salu", "spill", "ds", "vmem"))
+for (h, d), s in sorted(stats.items(), key=lambda x: (-x[0][1], x[0][0])):
+    print("%-14s %5d %6d %6d %6d %6d %5d %5d" % (h, d, s["ins"], s["valu"], s["salu"], s["spill"], s["ds"], s["vmem"]))
