@@ -251,12 +251,10 @@ __device__ __forceinline__ void lean_flush(LShared& S, const LeanParams* P, uint
     if (tid < GCAP) { S.f.dcnt[tid] = 0; S.f.drun[tid] = 0; }
     lds_barrier();
     const uint32_t smask = (1u << sb) - 1u;
-    uint32_t ek[EPT], ec[EPT];
-#pragma unroll
+    /* two passes over the table in LDS (no per-thread copy of the 14 entries: registers) */
     for (int j = 0; j < EPT; ++j) {
-        ek[j] = S.TK[j * NT + tid];
-        ec[j] = S.TC[j * NT + tid];
-        if (ek[j]) wave_agg_add(&S.f.dcnt[0], (ek[j] & 0x7FFFFFFFu) >> sb);
+        const uint32_t k = S.TK[j * NT + tid];
+        if (k) wave_agg_add(&S.f.dcnt[0], (k & 0x7FFFFFFFu) >> sb);
     }
     lds_barrier();
     uint32_t packed = 0;
@@ -294,19 +292,19 @@ __device__ __forceinline__ void lean_flush(LShared& S, const LeanParams* P, uint
     }
     uint32_t* const rec_slot = P->o.rec_slot;
     uint32_t* const rec_cnt = P->o.rec_cnt;
-#pragma unroll
     for (int j = 0; j < EPT; ++j) {
-        const uint32_t key = ek[j];
+        const uint32_t key = S.TK[j * NT + tid];
         if (key) {
+            const uint32_t c = S.TC[j * NT + tid];
             const uint32_t rel = (key & 0x7FFFFFFFu) >> sb;
             const uint32_t k = wave_agg_add_rtn(&S.f.drun[0], rel);
             const uint32_t dof = S.f.doff[rel];
             if (S.f.dstate[rel] == 2) {
                 const uint64_t q = rb + (dof & 0xFFFFu) + k;
-                if (rec_ok) { rec_slot[q] = key & smask; rec_cnt[q] = ec[j]; }
+                if (rec_ok) { rec_slot[q] = key & smask; rec_cnt[q] = c; }
             } else {
                 const uint64_t q = pb + (dof >> 16) + k;
-                if (part_ok) { P->o.part_doc[q] = gd0 + rel; P->o.part_slot[q] = key & smask; P->o.part_cnt[q] = ec[j]; }
+                if (part_ok) { P->o.part_doc[q] = gd0 + rel; P->o.part_slot[q] = key & smask; P->o.part_cnt[q] = c; }
             }
             S.TK[j * NT + tid] = 0u;
             S.TC[j * NT + tid] = 0u;
@@ -322,14 +320,12 @@ __device__ __forceinline__ void lean_flush_few(LShared& S, const LeanParams* P, 
     const int tid = threadIdx.x;
     const int lane = tid & 63, w = tid >> 6;
     const uint32_t smask = (1u << sb) - 1u;
-    uint32_t ek[EPT], ec[EPT];
     uint32_t pk[FEW / 2] = {0, 0, 0, 0};
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
-        ek[j] = S.TK[j * NT + tid];
-        ec[j] = S.TC[j * NT + tid];
-        if (ek[j]) {
-            const uint32_t rel = (ek[j] & 0x7FFFFFFFu) >> sb;
+        const uint32_t k = S.TK[j * NT + tid];
+        if (k) {
+            const uint32_t rel = (k & 0x7FFFFFFFu) >> sb;
 #pragma unroll
             for (uint32_t q = 0; q < FEW / 2; ++q)
                 pk[q] += (rel >> 1) == q ? (1u << (16 * (rel & 1u))) : 0u;
@@ -403,8 +399,9 @@ __device__ __forceinline__ void lean_flush_few(LShared& S, const LeanParams* P, 
     uint32_t* const rec_cnt = P->o.rec_cnt;
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
-        const uint32_t key = ek[j];
+        const uint32_t key = S.TK[j * NT + tid];
         if (key) {
+            const uint32_t c = S.TC[j * NT + tid];
             const uint32_t rel = (key & 0x7FFFFFFFu) >> sb;
             uint32_t r = 0;
 #pragma unroll
@@ -416,8 +413,8 @@ __device__ __forceinline__ void lean_flush_few(LShared& S, const LeanParams* P, 
             const uint64_t fb = S.fbase[rel];
             if (fb != ~0ull) {
                 const uint64_t qq = fb + r;
-                if (S.f.dstate[rel] == 2) { rec_slot[qq] = key & smask; rec_cnt[qq] = ec[j]; }
-                else { P->o.part_doc[qq] = gd0 + rel; P->o.part_slot[qq] = key & smask; P->o.part_cnt[qq] = ec[j]; }
+                if (S.f.dstate[rel] == 2) { rec_slot[qq] = key & smask; rec_cnt[qq] = c; }
+                else { P->o.part_doc[qq] = gd0 + rel; P->o.part_slot[qq] = key & smask; P->o.part_cnt[qq] = c; }
             }
             S.TK[j * NT + tid] = 0u;
             S.TC[j * NT + tid] = 0u;
@@ -490,8 +487,13 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_lean(const LeanParam
     };
     Round pend{};
     bool pending = false;
+    /* the round being filled: lanes [0, carry) hold keys built from earlier steps of this
+     * group, so every issued round is full (a step holds ~132 tokens: 64 + 64 + 4 would
+     * leave one nearly empty round per step) */
+    Round fillr{};
+    uint32_t carry = 0;
     uint32_t gd0_cur = 0;
-    uint64_t gbase_cur = 0;        /* absolute position of stage byte 0 of the pending round's step */
+    uint64_t wbase_cur = 0;        /* absolute position of window byte 0 of step 0 of the group */
 
     /* vocabulary slot of a round (miss path: lock-free insert / long term) -> LDS key */
     auto resolve = [&](const Round& r) -> uint32_t {
@@ -507,15 +509,15 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_lean(const LeanParam
                 const LeanParams* Q = P;
                 asm volatile("" : "+s"(Q));
                 if (len == LEN_LONG) {
-                    const uint32_t rel = r.e >> 16;
-                    slot = lean_slow_slot(Q, gbase_cur + (r.e & 1023u), S.gdoc[rel + 1]);
+                    const uint32_t rel = (r.e >> 16) & 0xFFu, st = r.e >> 24;
+                    slot = lean_slow_slot(Q, wbase_cur + (uint64_t)st * WSTEP + (r.e & 1023u), S.gdoc[rel + 1]);
                 } else {
                     slot = vocab_insert_s(Q->v.keys, Q->v.rep, Q->v.mask, ((uint64_t)r.k1 << 32) | r.k0,
                                           ((uint64_t)r.k3 << 32) | r.k2, 0, Q->o.status);
                 }
             }
         }
-        return (!valid || slot == INVALID_SLOT) ? 0u : (0x80000000u | ((r.e >> 16) << sb) | slot);
+        return (!valid || slot == INVALID_SLOT) ? 0u : (0x80000000u | (((r.e >> 16) & 0xFFu) << sb) | slot);
     };
     /* the LDS count of a round: one ds_read_b128 of the home bucket; a match adds, a new key
      * claims a free slot with one CAS; the rest (full bucket, lost race, overflow) bkt_slow */
@@ -616,6 +618,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_lean(const LeanParam
                 const int32_t own_lo = (int32_t)(gs - b0), own_hi = (int32_t)(ge - b0);
                 const int32_t rlo = relpos(c_lo, b0), rhi = relpos(c_hi, b0);
                 const uint64_t wbase = b0 - 16;                  /* absolute position of window byte 0, step 0 */
+                wbase_cur = wbase;
                 /* the wave's first step: prefetched during the previous chunk when it aimed here */
                 if (b0 != pfb) {
                     const uint64_t a = wbase + (uint64_t)wid * WSTEP + lane16;
@@ -703,30 +706,49 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_lean(const LeanParam
                         const uint32_t cnt = (ntok - tb) < (uint32_t)TLW ? (ntok - tb) : (uint32_t)TLW;
                         /* ---- rounds of 64 tokens; round r+1's vocabulary loads are issued
                          * before round r is counted ---- */
-                        for (uint32_t t0 = 0; t0 < cnt; t0 += 64) {
-                            Round q;
-                            const uint32_t t = t0 + (uint32_t)lane;
-                            q.e = t < cnt ? tl[t] : 0u;
-                            const uint32_t pos = q.e & 1023u, len = (q.e >> 10) & 15u;
-                            const u32x4u raw = *reinterpret_cast<const u32x4u*>(stage + pos);
-                            const uint4 sl = S.sel[len];
-                            q.k0 = __builtin_amdgcn_perm(0x09090909u, raw.x, sl.x);
-                            q.k1 = __builtin_amdgcn_perm(0x09090909u, raw.y, sl.y);
-                            q.k2 = __builtin_amdgcn_perm(0x09090909u, raw.z, sl.z);
-                            q.k3 = __builtin_amdgcn_perm(0x09090909u, raw.w, sl.w);
-                            q.hv = (uint32_t)key_hash(((uint64_t)q.k1 << 32) | q.k0, ((uint64_t)q.k3 << 32) | q.k2) & vmask;
-                            q.s4 = gload(vkeys + q.hv);
-                            q.t4 = gload(vkeys + ((q.hv + 1) & vmask));
-                            if (pending) count(resolve(pend));
-                            pend = q;
-                            gbase_cur = wbase + (uint64_t)s * WSTEP;
-                            pending = true;
+                        for (uint32_t t0 = 0; t0 < cnt;) {
+                            /* lanes [carry, carry + take) take entries t0.. of this step */
+                            const uint32_t take = (64u - carry) < (cnt - t0) ? (64u - carry) : (cnt - t0);
+                            if ((uint32_t)lane >= carry && (uint32_t)lane < carry + take) {
+                                const uint32_t e = tl[t0 + (uint32_t)lane - carry];
+                                const uint32_t pos = e & 1023u, len = (e >> 10) & 15u;
+                                const u32x4u raw = *reinterpret_cast<const u32x4u*>(stage + pos);
+                                const uint4 sl = S.sel[len];
+                                fillr.e = e | (s << 24);
+                                fillr.k0 = __builtin_amdgcn_perm(0x09090909u, raw.x, sl.x);
+                                fillr.k1 = __builtin_amdgcn_perm(0x09090909u, raw.y, sl.y);
+                                fillr.k2 = __builtin_amdgcn_perm(0x09090909u, raw.z, sl.z);
+                                fillr.k3 = __builtin_amdgcn_perm(0x09090909u, raw.w, sl.w);
+                            }
+                            carry += take;
+                            t0 += take;
+                            if (carry == 64u) {   /* a full round: its loads now, the pending round counted */
+                                Round q = fillr;
+                                q.hv = (uint32_t)key_hash(((uint64_t)q.k1 << 32) | q.k0, ((uint64_t)q.k3 << 32) | q.k2) & vmask;
+                                q.s4 = gload(vkeys + q.hv);
+                                q.t4 = gload(vkeys + ((q.hv + 1) & vmask));
+                                if (pending) count(resolve(pend));
+                                pend = q;
+                                pending = true;
+                                carry = 0;
+                            }
                         }
                         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                         __builtin_amdgcn_wave_barrier();
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                     }
                 }
+            }
+            if (carry) {   /* the group's last, partial round (lanes >= carry hold no token) */
+                Round q = fillr;
+                if ((uint32_t)lane >= carry) q.e = 0u;
+                q.hv = (uint32_t)key_hash(((uint64_t)q.k1 << 32) | q.k0, ((uint64_t)q.k3 << 32) | q.k2) & vmask;
+                q.s4 = gload(vkeys + q.hv);
+                q.t4 = gload(vkeys + ((q.hv + 1) & vmask));
+                if (pending) count(resolve(pend));
+                pend = q;
+                pending = true;
+                carry = 0;
             }
             if (pending) { count(resolve(pend)); pending = false; }
             if (ahead) {   /* the next chunk's document offsets, in flight during this flush */
