@@ -120,8 +120,11 @@ __device__ __forceinline__ int32_t relpos(uint64_t x, uint64_t base) {
 }
 
 /* ---- the bucketed LDS count table (as tokcount_st.hip) ---- */
+/* bucket of an LDS key (rel << sb | slot, bit 31 set): the slot bits are already a hash;
+ * the document bits are folded into the low 16, which a 24-bit multiply (full rate, unlike
+ * v_mul_lo_u32 / v_mul_hi_u32) scales to [0, NB) */
 __device__ __forceinline__ uint32_t bkt_hash(uint32_t key) {
-    return (uint32_t)(((uint64_t)(key * 0x9E3779B1u) * (uint64_t)NB) >> 32);   /* [0, NB) */
+    return (uint32_t)__umul24((key ^ (key >> 15)) & 0xFFFFu, NB) >> 16;   /* [0, NB) */
 }
 __device__ __forceinline__ uint32_t bkt_next(uint32_t b) { return b + 1 == NB ? 0u : b + 1; }
 __device__ __forceinline__ uint4 bkt_read(LShared& S, uint32_t b) { return reinterpret_cast<const uint4*>(S.TK)[b]; }
@@ -576,21 +579,23 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_lean(const LeanParam
     uint32_t chunk = runi(S.cur_chunk), nxt = runi(S.nxt_chunk);
     uint64_t cs = 0, ce = 0;
     uint32_t dfirst = 0, dlast = 0;
+    /* (loads through P are vector loads — the block is not provably read-only — so every
+     * value read from it is made wave-uniform explicitly: scalar registers and branches) */
     if (chunk < nchunk) {
-        cs = P->chunk_start[chunk];
-        ce = P->chunk_start[chunk + 1];
-        dfirst = P->chunk_doc[chunk];
-        dlast = P->chunk_doc[chunk + 1];
+        cs = uni64(P->chunk_start[chunk]);
+        ce = uni64(P->chunk_start[chunk + 1]);
+        dfirst = runi(P->chunk_doc[chunk]);
+        dlast = runi(P->chunk_doc[chunk + 1]);
     }
     while (chunk < nchunk) {
         if (tid == 0) pend_v = atomicAdd(&P->o.chunk_shard[shard], 1ull);
         uint64_t ncs = 0, nce = 0;
         uint32_t ndf = 0, ndl = 0;
         if (nxt < nchunk) {
-            ncs = P->chunk_start[nxt];
-            nce = P->chunk_start[nxt + 1];
-            ndf = P->chunk_doc[nxt];
-            ndl = P->chunk_doc[nxt + 1];
+            ncs = uni64(P->chunk_start[nxt]);
+            nce = uni64(P->chunk_start[nxt + 1]);
+            ndf = runi(P->chunk_doc[nxt]);
+            ndl = runi(P->chunk_doc[nxt + 1]);
         }
         if (cs < ce)
         for (uint32_t gd0 = dfirst; gd0 <= dlast; gd0 += gcap) {
