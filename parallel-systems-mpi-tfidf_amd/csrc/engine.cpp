@@ -149,6 +149,7 @@ struct tfidf_ctx {
      * of pageable or synchronous copies (two round trips per run saved) */
     uint64_t* hpin = nullptr;
     DevBuf dense, vslot, skey0, skey1, seq0, seq1, rank_of_slot, slot_of_rank, rank16;
+    DevBuf hot_slot;        /* k_tokcount_lean's hot term ids -> vocabulary slots */
     DevBuf pkey0, pkey1, pseq0, pseq1, phead;
     DevBuf big_list, big_idx, dense_cnt, kcnt, tile_cnt;   /* dense merge of long documents */
     DevBuf df_local, df_global, present, idf_vals;
@@ -302,7 +303,7 @@ void tfidf_close(tfidf_ctx* ctx) {
                       &ctx->chunk_start, &ctx->chunk_doc, &ctx->vkeys, &ctx->vrep, &ctx->rec_slot, &ctx->rec_cnt,
                       &ctx->part_doc, &ctx->part_slot, &ctx->part_cnt, &ctx->doc_recoff, &ctx->doc_npairs,
                       &ctx->doc_size, &ctx->doc_flags, &ctx->counters, &ctx->dense, &ctx->vslot, &ctx->skey0,
-                      &ctx->skey1, &ctx->seq0, &ctx->seq1, &ctx->rank_of_slot, &ctx->slot_of_rank, &ctx->rank16, &ctx->pkey0,
+                      &ctx->skey1, &ctx->seq0, &ctx->seq1, &ctx->rank_of_slot, &ctx->slot_of_rank, &ctx->rank16, &ctx->hot_slot, &ctx->pkey0,
                       &ctx->pkey1, &ctx->pseq0, &ctx->pseq1, &ctx->phead, &ctx->df_local, &ctx->df_global,
                       &ctx->present, &ctx->idf_vals, &ctx->dkey0, &ctx->dkey1, &ctx->dseq0, &ctx->dseq1,
                       &ctx->npairs_ord, &ctx->out_off, &ctx->doc_meta, &ctx->t_key, &ctx->t_len, &ctx->doc_tbytes,
@@ -540,6 +541,9 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     o.status = (uint32_t*)(cnt + 3);
     o.stamps = nullptr;
     o.ablate = ctx->ablate;
+    ENSURE(ctx->hot_slot, (size_t)HOT_SLOTS * 4);
+    o.hot_slot = ctx->hot_slot.as<uint32_t>();
+    o.hot_ctr = (uint32_t*)(cnt + 9);   /* zeroed with the run's counters */
     if (ctx->stamps_on) {
         ENSURE(ctx->stamps, 8 * K1_STAMP_WORDS);
         HIPCHK(hipMemsetAsync(ctx->stamps.p, 0, 8 * K1_STAMP_WORDS, s));
@@ -578,6 +582,8 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
         ctx->npairs = 0;
         return 2;
     }
+    /* the lean K1's hot-term marks leave the keys before anything else reads them */
+    if (nchunks && ctx->k1_lean) LCHK(launch_hot_unmark(vd.keys, o.hot_slot, o.hot_ctr, s));
     /* the vocabulary's used-slot flags and count are enqueued before the host reads K1's
      * counters: one host round trip for both */
     const uint64_t cap = ctx->vcap;
@@ -651,7 +657,8 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     ENSURE(ctx->skey1, (size_t)V * 16 + 16);
     ENSURE(ctx->seq0, (size_t)V * 4 + 4);
     ENSURE(ctx->seq1, (size_t)V * 4 + 4);
-    ENSURE(ctx->rank_of_slot, cap * 4);
+    /* rank maps: one entry per slot, plus one per hot term id (slot cap + id) */
+    ENSURE(ctx->rank_of_slot, (cap + HOT_SLOTS) * 4);
     ENSURE(ctx->slot_of_rank, (size_t)V * 4 + 4);
     LCHK(launch_vocab_compact(vd, cap, ctx->dense.as<uint32_t>(), c, ctx->vslot.as<uint32_t>(), ctx->skey0.as<uint4>(),
                               ctx->seq0.as<uint32_t>(), s));
@@ -671,9 +678,12 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     if (st & ST_HAS_LONG)   /* terms of >= 16 bytes exist: order the ones tied on 16 bytes */
         LCHK(launch_vocab_long_fixup(ctx->sorted_skey, ctx->sorted_dense, ctx->vslot.as<uint32_t>(), vd, c, V, ar, s));
     uint16_t* r16 = nullptr;
-    if (V <= 65536u) { ENSURE(ctx->rank16, cap * 2); r16 = ctx->rank16.as<uint16_t>(); }
+    if (V <= 65536u) { ENSURE(ctx->rank16, (cap + HOT_SLOTS) * 2); r16 = ctx->rank16.as<uint16_t>(); }
     LCHK(launch_vocab_rank(ctx->sorted_dense, ctx->vslot.as<uint32_t>(), V, ctx->rank_of_slot.as<uint32_t>(),
                            ctx->slot_of_rank.as<uint32_t>(), r16, s));
+    if (nchunks && ctx->k1_lean)
+        LCHK(launch_hot_ranks(ctx->rank_of_slot.as<uint32_t>(), r16, cap, ctx->hot_slot.as<uint32_t>(),
+                              (const uint32_t*)(cnt + 9), s));
     /* ---- partial documents ---- */
     mark(ctx, S_MERGE);
     uint64_t R_total = R_main;
@@ -770,7 +780,7 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     /* also rewrites every record's slot as its term rank (K5 then needs no rank gather) */
     LCHK(launch_df_hist(ctx->rec_slot.as<uint32_t>(), R_main, merged_count, R_total,
                         ctx->rank_of_slot.as<uint32_t>(),
-                        V <= 65536u ? ctx->rank16.as<uint16_t>() : nullptr, V, cap,
+                        V <= 65536u ? ctx->rank16.as<uint16_t>() : nullptr, V, cap + HOT_SLOTS,
                         (uint32_t*)(cnt + 3), ctx->df_local.as<uint32_t>(), ar, s));
     ctx->run_V = V;
     ctx->run_cap = cap;
@@ -894,7 +904,7 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
     a.nterms = V;
     a.rank_bits = V > 1 ? 32u - (uint32_t)__builtin_clz(V - 1) : 1u;
     a.rec_total = R_total;
-    a.slot_cap = cap;
+    a.slot_cap = cap + HOT_SLOTS;
     a.status = (uint32_t*)(cnt + 3);
     a.out_term = ctx->out_term.as<uint32_t>();
     a.out_cnt = ctx->out_cnt.as<uint32_t>();

@@ -76,6 +76,8 @@ struct K1Out {
                                     1 no vocabulary lookup, 2 no LDS counting, 4 no token walk */
     unsigned long long* stamps;  /* diagnostic build only: K1_NSTAMP phase cycle sums, WG count,
                                     then K1_NCOUNT event counters */
+    uint32_t* hot_slot;          /* k_tokcount_lean: vocabulary slot of hot term id (HOT_MAX) */
+    uint32_t* hot_ctr;           /* ... hot ids handed out (zeroed per run; may exceed HOT_MAX) */
 };
 #define K1_NSTAMP 17
 #define K1_NCOUNT 4   /* segments, flushes, tokens taking the full probe, probe iterations */
@@ -114,6 +116,14 @@ struct LeanParams {
     uint64_t c0, c1;
 };
 int launch_tokcount_lean(const LeanParams* dparams, const LeanParams& h, hipStream_t s);
+/* after k_tokcount_lean: clear the hot marks from the vocabulary keys (before any other
+ * stage reads them) */
+int launch_hot_unmark(uint4* keys, const uint32_t* hot_slot, const uint32_t* hot_ctr, hipStream_t s);
+/* after the vocabulary ranks: rank_of_slot[cap + id] (and rank16) = the rank of hot term id
+ * (k_tokcount_lean writes a dense-counted pair's record with slot cap + id) */
+int launch_hot_ranks(uint32_t* rank_of_slot, uint16_t* rank16, uint64_t cap, const uint32_t* hot_slot,
+                     const uint32_t* hot_ctr, hipStream_t s);
+#define HOT_SLOTS 1024u   /* = HOT_MAX (dev_vocab.h): slots cap .. cap + HOT_SLOTS of the rank maps */
 
 /* vocabulary finalisation */
 int launch_vocab_flags(const VocabDev& v, uint64_t cap, uint32_t* flags, hipStream_t s);

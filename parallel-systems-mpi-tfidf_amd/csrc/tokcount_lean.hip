@@ -49,7 +49,9 @@ constexpr int NT = 256;                   /* threads per workgroup */
 constexpr int WG_PER_CU = 4;              /* 16 waves per CU */
 constexpr int NWAVE = NT / 64;
 constexpr uint32_t WSTEP = 992;           /* bytes a wave step owns (lanes 1..62) */
-constexpr int TB = 3584;                  /* LDS table entries (u32 key + u32 count): 14 per thread */
+constexpr int TB = 2048;                  /* LDS table entries (u32 key + u32 count): 8 per thread */
+constexpr uint32_t DD = 4;                /* documents of a group with dense hot-term counters */
+constexpr uint32_t HW = HOT_MAX / 2;      /* words per document: two u16 counters each */
 constexpr int EPT = TB / NT;
 constexpr uint32_t FILL_LIMIT = TB - NT * 2 - 64; /* claims after which overflow mode starts */
 constexpr int GCAP = 256;                 /* documents per group at most */
@@ -62,6 +64,7 @@ constexpr int32_t FAR = 0x3FFFFFFF;       /* "no document start" in group-relati
 struct LShared {
     uint32_t TK[TB];                      /* key32 = 1 << 31 | doc-in-group << sb | slot (0: empty) */
     uint32_t TC[TB];                      /* its count */
+    uint32_t dense[DD * HW];              /* hot terms of the group's first DD documents: u16 counts */
     uint64_t gdoc[GCAP + 1];              /* doc_off of the group's documents */
     uint32_t dsz[GCAP];                   /* docSize accumulators */
     union {
@@ -80,6 +83,7 @@ struct LShared {
     uint64_t fbase[8];
     uint8_t dpart[GCAP];                  /* document has overflow records */
     uint32_t fill;
+    uint32_t hot_closed;                  /* this workgroup saw the hot ids run out */
     uint32_t cur_chunk, nxt_chunk;
     uint32_t wsum[NWAVE];
     unsigned long long rec_base, part_base;
@@ -158,7 +162,8 @@ __device__ __forceinline__ uint32_t claim_chunk(unsigned long long* ctr, uint32_
 
 /* term slot of a token whose term is >= 16 bytes (or runs past the 32-byte window): the
  * token is re-read from HBM (rare for text) */
-__device__ __forceinline__ uint32_t lean_slow_slot(const LeanParams* P, uint64_t p0, uint64_t dend) {
+__device__ __forceinline__ uint32_t lean_slow_slot(const LeanParams* P, uint64_t p0, uint64_t dend, uint32_t* hot_closed,
+                                                  uint32_t* hid) {
     const uint8_t* __restrict__ bytes = P->c.bytes;
     uint64_t p = p0;
     while (p < dend && !is_ws(bytes[p])) ++p;
@@ -172,13 +177,15 @@ __device__ __forceinline__ uint32_t lean_slow_slot(const LeanParams* P, uint64_t
             if (k < 8) lo |= b << (8 * k); else hi |= b << (8 * (k - 8));
         }
         make_short_key(lo, hi, (uint32_t)n, &klo, &khi);
-        return vocab_insert_s(P->v.keys, P->v.rep, P->v.mask, klo, khi, 0, P->o.status);
+        return vocab_insert_hot(P->v.keys, P->v.rep, P->v.mask, klo, khi, 0, P->o.status, P->o.hot_slot, P->o.hot_ctr,
+                                hot_closed, hid);
     }
     make_long_key(bytes + p0, n, &klo, &khi);
     /* rep = (length << 40) | offset holds 24 length bits (TFIDF_E_CAPACITY beyond) */
     if (n >= 0xFFFFFFull) atomicOr(P->o.status, ST_TERM_LONG);
     const uint64_t rep = ((n < 0xFFFFFFull ? n : 0xFFFFFFull) << 40) | p0;
-    return vocab_insert_s(P->v.keys, P->v.rep, P->v.mask, klo, khi, rep, P->o.status);
+    return vocab_insert_hot(P->v.keys, P->v.rep, P->v.mask, klo, khi, rep, P->o.status, P->o.hot_slot, P->o.hot_ctr,
+                            hot_closed, hid);
 }
 
 __device__ __forceinline__ void overflow_record(const LeanParams* P, uint32_t doc, uint32_t slot) {
@@ -246,18 +253,31 @@ __device__ __forceinline__ uint32_t wave_agg_add_rtn(uint32_t* ctr, uint32_t idx
     return k;
 }
 
-/* Emits every table entry of the group as records and clears the table (any number of
- * documents): per-document counts, a block scan, then every entry straight to its slot. */
+/* The hot-term counters a thread owns in the flush: words w = tid + NT * k (k < 8) of
+ * S.dense, i.e. document k / 2, term ids 2 (tid + NT (k & 1)) and that + 1. */
+constexpr int DPT = (int)(DD * HW) / NT;
+static_assert(DPT == 8 && (DD * HW) % NT == 0, "dense words per thread");
+__device__ __forceinline__ uint32_t nz16(uint32_t w) { return ((w & 0xFFFFu) != 0u ? 1u : 0u) + ((w >> 16) != 0u ? 1u : 0u); }
+
+/* Emits every table entry and every non-zero hot counter of the group as records and
+ * clears both (any number of documents): per-document counts, a block scan, then every
+ * entry straight to its slot.  A hot term's record carries slot cap + id (its rank comes
+ * from rank_of_slot[cap + id], see launch_hot_ranks). */
 __device__ __forceinline__ void lean_flush(LShared& S, const LeanParams* P, uint32_t gd0, uint32_t ng, uint64_t cs,
-                                        uint64_t ce, uint32_t sb) {
+                                           uint64_t ce, uint32_t sb, uint32_t cap) {
     const int tid = threadIdx.x;
     if (tid < GCAP) { S.f.dcnt[tid] = 0; S.f.drun[tid] = 0; }
     lds_barrier();
     const uint32_t smask = (1u << sb) - 1u;
-    /* two passes over the table in LDS (no per-thread copy of the 14 entries: registers) */
+    /* two passes over the table in LDS (no per-thread copy of the entries: registers) */
     for (int j = 0; j < EPT; ++j) {
         const uint32_t k = S.TK[j * NT + tid];
         if (k) wave_agg_add(&S.f.dcnt[0], (k & 0x7FFFFFFFu) >> sb);
+    }
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+        const uint32_t n = nz16(S.dense[tid + NT * k]);
+        if (n) atomicAdd(&S.f.dcnt[k >> 1], n);
     }
     lds_barrier();
     uint32_t packed = 0;
@@ -295,22 +315,35 @@ __device__ __forceinline__ void lean_flush(LShared& S, const LeanParams* P, uint
     }
     uint32_t* const rec_slot = P->o.rec_slot;
     uint32_t* const rec_cnt = P->o.rec_cnt;
+    auto emit = [&](uint32_t rel, uint32_t k, uint32_t slot, uint32_t c) {
+        const uint32_t dof = S.f.doff[rel];
+        if (S.f.dstate[rel] == 2) {
+            const uint64_t q = rb + (dof & 0xFFFFu) + k;
+            if (rec_ok) { rec_slot[q] = slot; rec_cnt[q] = c; }
+        } else {
+            const uint64_t q = pb + (dof >> 16) + k;
+            if (part_ok) { P->o.part_doc[q] = gd0 + rel; P->o.part_slot[q] = slot; P->o.part_cnt[q] = c; }
+        }
+    };
     for (int j = 0; j < EPT; ++j) {
         const uint32_t key = S.TK[j * NT + tid];
         if (key) {
             const uint32_t c = S.TC[j * NT + tid];
             const uint32_t rel = (key & 0x7FFFFFFFu) >> sb;
-            const uint32_t k = wave_agg_add_rtn(&S.f.drun[0], rel);
-            const uint32_t dof = S.f.doff[rel];
-            if (S.f.dstate[rel] == 2) {
-                const uint64_t q = rb + (dof & 0xFFFFu) + k;
-                if (rec_ok) { rec_slot[q] = key & smask; rec_cnt[q] = c; }
-            } else {
-                const uint64_t q = pb + (dof >> 16) + k;
-                if (part_ok) { P->o.part_doc[q] = gd0 + rel; P->o.part_slot[q] = key & smask; P->o.part_cnt[q] = c; }
-            }
+            emit(rel, wave_agg_add_rtn(&S.f.drun[0], rel), key & smask, c);
             S.TK[j * NT + tid] = 0u;
             S.TC[j * NT + tid] = 0u;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+        const uint32_t w = S.dense[tid + NT * k];
+        if (w) {
+            const uint32_t rel = (uint32_t)k >> 1, id = 2u * ((uint32_t)tid + NT * ((uint32_t)k & 1u));
+            uint32_t r = atomicAdd(&S.f.drun[rel], nz16(w));
+            if (w & 0xFFFFu) emit(rel, r++, cap + id, w & 0xFFFFu);
+            if (w >> 16) emit(rel, r, cap + id + 1u, w >> 16);
+            S.dense[tid + NT * k] = 0u;
         }
     }
 }
@@ -319,7 +352,7 @@ __device__ __forceinline__ void lean_flush(LShared& S, const LeanParams* P, uint
  * per-document counters per thread, one block scan, no LDS atomics.  Same output. */
 constexpr uint32_t FEW = 8;
 __device__ __forceinline__ void lean_flush_few(LShared& S, const LeanParams* P, uint32_t gd0, uint32_t ng, uint64_t cs,
-                                            uint64_t ce, uint32_t sb) {
+                                               uint64_t ce, uint32_t sb, uint32_t cap) {
     const int tid = threadIdx.x;
     const int lane = tid & 63, w = tid >> 6;
     const uint32_t smask = (1u << sb) - 1u;
@@ -334,6 +367,9 @@ __device__ __forceinline__ void lean_flush_few(LShared& S, const LeanParams* P, 
                 pk[q] += (rel >> 1) == q ? (1u << (16 * (rel & 1u))) : 0u;
         }
     }
+    /* dense words: document k / 2 of each pair k -> field (k / 2) & 1 of pk[k / 4] */
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) pk[k >> 2] += nz16(S.dense[tid + NT * k]) << (16 * ((k >> 1) & 1));
     uint32_t inc[FEW / 2];
 #pragma unroll
     for (uint32_t q = 0; q < FEW / 2; ++q) {
@@ -400,27 +436,40 @@ __device__ __forceinline__ void lean_flush_few(LShared& S, const LeanParams* P, 
     lds_barrier();
     uint32_t* const rec_slot = P->o.rec_slot;
     uint32_t* const rec_cnt = P->o.rec_cnt;
+    auto emit = [&](uint32_t rel, uint32_t slot, uint32_t c) {
+        uint32_t r = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < FEW / 2; ++q)
+            if ((rel >> 1) == q) {
+                r = (rank[q] >> (16 * (rel & 1u))) & 0xFFFFu;
+                rank[q] += 1u << (16 * (rel & 1u));
+            }
+        const uint64_t fb = S.fbase[rel];
+        if (fb != ~0ull) {
+            const uint64_t qq = fb + r;
+            if (S.f.dstate[rel] == 2) { rec_slot[qq] = slot; rec_cnt[qq] = c; }
+            else { P->o.part_doc[qq] = gd0 + rel; P->o.part_slot[qq] = slot; P->o.part_cnt[qq] = c; }
+        }
+    };
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
         const uint32_t key = S.TK[j * NT + tid];
         if (key) {
-            const uint32_t c = S.TC[j * NT + tid];
-            const uint32_t rel = (key & 0x7FFFFFFFu) >> sb;
-            uint32_t r = 0;
-#pragma unroll
-            for (uint32_t q = 0; q < FEW / 2; ++q)
-                if ((rel >> 1) == q) {
-                    r = (rank[q] >> (16 * (rel & 1u))) & 0xFFFFu;
-                    rank[q] += 1u << (16 * (rel & 1u));
-                }
-            const uint64_t fb = S.fbase[rel];
-            if (fb != ~0ull) {
-                const uint64_t qq = fb + r;
-                if (S.f.dstate[rel] == 2) { rec_slot[qq] = key & smask; rec_cnt[qq] = c; }
-                else { P->o.part_doc[qq] = gd0 + rel; P->o.part_slot[qq] = key & smask; P->o.part_cnt[qq] = c; }
-            }
+            emit((key & 0x7FFFFFFFu) >> sb, key & smask, S.TC[j * NT + tid]);
             S.TK[j * NT + tid] = 0u;
             S.TC[j * NT + tid] = 0u;
+        }
+    }
+    /* dense words after the table entries: the ranks per document continue (the scan
+     * counted them in the same order) */
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+        const uint32_t wd = S.dense[tid + NT * k];
+        if (wd) {
+            const uint32_t rel = (uint32_t)k >> 1, id = 2u * ((uint32_t)tid + NT * ((uint32_t)k & 1u));
+            if (wd & 0xFFFFu) emit(rel, cap + id, wd & 0xFFFFu);
+            if (wd >> 16) emit(rel, cap + id + 1u, wd >> 16);
+            S.dense[tid + NT * k] = 0u;
         }
     }
 }
@@ -477,6 +526,8 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_lean(const LeanParam
     const uint32_t wid = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
 
     for (int j = 0; j < EPT; ++j) { S.TK[j * NT + tid] = 0u; S.TC[j * NT + tid] = 0u; }
+    for (uint32_t j = (uint32_t)tid; j < DD * HW; j += NT) S.dense[j] = 0u;
+    if (tid == 0) S.hot_closed = 0u;
     if (tid < 64) {
         const uint32_t n = (uint32_t)tid >> 2, k = (uint32_t)tid & 3u;
         (&S.sel[n].x)[k] = perm_sel(n, k);
@@ -499,28 +550,39 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_lean(const LeanParam
     uint64_t wbase_cur = 0;        /* absolute position of window byte 0 of step 0 of the group */
 
     /* vocabulary slot of a round (miss path: lock-free insert / long term) -> LDS key */
+    /* vocabulary slot of a round (miss path: lock-free insert / long term); a hot term of
+     * one of the group's first DD documents is counted right here in its dense counter (one
+     * non-returning LDS add), everything else returns its LDS table key (0: nothing left) */
     auto resolve = [&](const Round& r) -> uint32_t {
         const uint32_t len = (r.e >> 10) & 31u;
+        const uint32_t rel = (r.e >> 16) & 0xFFu;
         const bool valid = r.e != 0u;
-        /* bitwise compares (xor / or3): no short-circuit branches on the exec mask */
-        const bool hit0 = ((r.s4.x ^ r.k0) | (r.s4.y ^ r.k1) | (r.s4.z ^ r.k2) | (r.s4.w ^ r.k3)) == 0u;
-        const bool hit1 = ((r.t4.x ^ r.k0) | (r.t4.y ^ r.k1) | (r.t4.z ^ r.k2) | (r.t4.w ^ r.k3)) == 0u;
+        /* bitwise compares (xor / or3): no short-circuit branches on the exec mask; a slot's
+         * hot mark (bytes 14-15) is not part of the term */
+        const bool hit0 = ((r.s4.x ^ r.k0) | (r.s4.y ^ r.k1) | (r.s4.z ^ r.k2) | (unhot_w(r.s4.w) ^ r.k3)) == 0u;
+        const bool hit1 = ((r.t4.x ^ r.k0) | (r.t4.y ^ r.k1) | (r.t4.z ^ r.k2) | (unhot_w(r.t4.w) ^ r.k3)) == 0u;
         uint32_t slot = hit0 ? r.hv : ((r.hv + 1) & vmask);
+        uint32_t hid = hot_id_w(hit0 ? r.s4.w : r.t4.w);
         const bool rare = valid && (len == LEN_LONG || (!hit0 && !hit1));
         if (__ballot(rare) != 0ull) {
             if (rare) {
                 const LeanParams* Q = P;
                 asm volatile("" : "+s"(Q));
                 if (len == LEN_LONG) {
-                    const uint32_t rel = (r.e >> 16) & 0xFFu, st = r.e >> 24;
-                    slot = lean_slow_slot(Q, wbase_cur + (uint64_t)st * WSTEP + (r.e & 1023u), S.gdoc[rel + 1]);
+                    const uint32_t st = r.e >> 24;
+                    slot = lean_slow_slot(Q, wbase_cur + (uint64_t)st * WSTEP + (r.e & 1023u), S.gdoc[rel + 1],
+                                          &S.hot_closed, &hid);
                 } else {
-                    slot = vocab_insert_s(Q->v.keys, Q->v.rep, Q->v.mask, ((uint64_t)r.k1 << 32) | r.k0,
-                                          ((uint64_t)r.k3 << 32) | r.k2, 0, Q->o.status);
+                    slot = vocab_insert_hot(Q->v.keys, Q->v.rep, Q->v.mask, ((uint64_t)r.k1 << 32) | r.k0,
+                                            ((uint64_t)r.k3 << 32) | r.k2, 0, Q->o.status, Q->o.hot_slot,
+                                            Q->o.hot_ctr, &S.hot_closed, &hid);
                 }
             }
         }
-        return (!valid || slot == INVALID_SLOT) ? 0u : (0x80000000u | (((r.e >> 16) & 0xFFu) << sb) | slot);
+        const bool ok = valid && slot != INVALID_SLOT;
+        const bool dense = ok && hid != HOT_NONE && rel < DD;
+        if (dense) atomicAdd(&S.dense[rel * HW + (hid >> 1)], 1u << (16u * (hid & 1u)));
+        return (ok && !dense) ? (0x80000000u | (rel << sb) | slot) : 0u;
     };
     /* the LDS count of a round: one ds_read_b128 of the home bucket; a match adds, a new key
      * claims a free slot with one CAS; the rest (full bucket, lost race, overflow) bkt_slow */
@@ -762,8 +824,8 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_lean(const LeanParam
                 dpre_ok = true;
             }
             lds_barrier();   /* every wave's walk is done (the walk state aliases the flush's) */
-            if (ng <= FEW) lean_flush_few(S, P, gd0, ng, cs, ce, sb);
-            else lean_flush(S, P, gd0, ng, cs, ce, sb);
+            if (ng <= FEW) lean_flush_few(S, P, gd0, ng, cs, ce, sb, vmask + 1u);
+            else lean_flush(S, P, gd0, ng, cs, ce, sb, vmask + 1u);
             if ((uint32_t)tid < ng) {
                 const uint32_t n = S.dsz[tid];
                 if (n) {
@@ -813,5 +875,35 @@ int launch_tokcount_lean(const LeanParams* dparams, const LeanParams& h, hipStre
     const uint64_t last_blk = h.c.nbytes ? ((h.c.nbytes - 1) & ~(uint64_t)15) : 0;
     k_tokcount_lean<<<(unsigned)grid, NT, 0, s>>>(dparams, h.c.bytes, h.v.keys, (uint32_t)h.v.mask, sb, gcap,
                                                   (uint32_t)n, h.c.lo, h.c.hi, last_blk);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+/* ---- hot terms after K1 (dev_vocab.h) ---- */
+__global__ void k_hot_unmark(uint4* __restrict__ keys, const uint32_t* __restrict__ hot_slot,
+                             const uint32_t* __restrict__ hot_ctr) {
+    const uint32_t n = min(*hot_ctr, HOT_MAX);
+    for (uint32_t id = threadIdx.x; id < n; id += blockDim.x) {
+        const uint32_t sl = hot_slot[id];
+        keys[sl].w = unhot_w(keys[sl].w);
+    }
+}
+int launch_hot_unmark(uint4* keys, const uint32_t* hot_slot, const uint32_t* hot_ctr, hipStream_t s) {
+    k_hot_unmark<<<1, 1024, 0, s>>>(keys, hot_slot, hot_ctr);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+__global__ void k_hot_ranks(uint32_t* __restrict__ rank_of_slot, uint16_t* __restrict__ rank16, uint64_t cap,
+                            const uint32_t* __restrict__ hot_slot, const uint32_t* __restrict__ hot_ctr) {
+    const uint32_t n = min(*hot_ctr, HOT_MAX);
+    for (uint32_t id = threadIdx.x; id < HOT_MAX; id += blockDim.x) {
+        const uint32_t r = id < n ? rank_of_slot[hot_slot[id]] : 0u;
+        rank_of_slot[cap + id] = r;
+        if (rank16) rank16[cap + id] = (uint16_t)(id < n ? rank16[hot_slot[id]] : 0u);
+    }
+}
+int launch_hot_ranks(uint32_t* rank_of_slot, uint16_t* rank16, uint64_t cap, const uint32_t* hot_slot,
+                     const uint32_t* hot_ctr, hipStream_t s) {
+    static_assert(HOT_SLOTS == HOT_MAX, "rank maps sized for every hot id");
+    k_hot_ranks<<<1, 1024, 0, s>>>(rank_of_slot, rank16, cap, hot_slot, hot_ctr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
