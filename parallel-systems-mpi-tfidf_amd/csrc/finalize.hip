@@ -317,7 +317,8 @@ __global__ void k_part_merge(const uint64_t* __restrict__ keys, const uint32_t* 
     const uint64_t up = __shfl_up(u, 1);
     if (val && (lane == 0 || up != u)) atomicAdd(&rec_cnt[u], v);
     if (!head) return;
-    rec_slot[u] = slot_of_rank[(uint32_t)k];
+    rec_slot[u] = (uint32_t)k;   /* the term RANK: merged records are ranked already (DF skips their gather) */
+    (void)slot_of_rank;
     uint32_t d = (uint32_t)(k >> 32);
     if (i == 0 || (uint32_t)(kp >> 32) != d) {
         doc_recoff[d] = u;
@@ -542,7 +543,7 @@ __global__ void k_dense_write(const uint32_t* __restrict__ dense, uint32_t V, ui
     const uint64_t base = rec_base + *merged_count + tile_off[(uint64_t)b * nt + t];
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-        if (v[k]) { rec_slot[base + o] = slot_of_rank[r0 + k]; rec_cnt[base + o] = v[k]; ++o; }
+        if (v[k]) { rec_slot[base + o] = r0 + k; rec_cnt[base + o] = v[k]; ++o; }   /* ranks (see k_part_merge) */
     if (t == 0 && threadIdx.x == 0) {
         const uint32_t d = big_list[b];
         const uint64_t first = tile_off[(uint64_t)b * nt], last = tile_off[(uint64_t)(b + 1) * nt];
@@ -590,7 +591,8 @@ __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ r
                                                         const uint32_t* __restrict__ nrec_extra,
                                                         const uint32_t* __restrict__ rank_of_slot,
                                                         const uint16_t* __restrict__ rank16, uint32_t V,
-                                                        uint64_t slot_cap, uint32_t* __restrict__ status,
+                                                        uint64_t slot_cap, uint64_t ranked_from,
+                                                        uint32_t* __restrict__ status,
                                                         uint32_t* __restrict__ part /* [grid][V/2 words] */) {
     extern __shared__ __attribute__((aligned(16))) uint32_t bins[]; /* V/2 words of two u16 counters */
     const uint32_t W = (V + 1) / 2;
@@ -608,23 +610,21 @@ __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ r
         }
 #pragma unroll
         for (int q = 0; q < DFH_B; ++q) {
-            if (sl[q] != 0xFFFFFFFFu && sl[q] >= slot_cap) { atomicOr(status, ST_BOUNDS); sl[q] = 0xFFFFFFFFu; }
-#if defined(DF_ABL) && (DF_ABL & 1)
-            r[q] = sl[q] != 0xFFFFFFFFu ? (sl[q] & 0x7FFFu) : 0u; /* timing only */
-#else
+            const bool ranked = i + (uint64_t)q * DFH_NT >= ranked_from;   /* merged records hold ranks */
+            if (sl[q] != 0xFFFFFFFFu && sl[q] >= (ranked ? (uint64_t)V : slot_cap)) {
+                atomicOr(status, ST_BOUNDS);
+                sl[q] = 0xFFFFFFFFu;
+            }
             /* V <= 65536: the 2-byte map (half the footprint of the 4-byte one: more of
              * these random gathers hit L2) */
-            r[q] = sl[q] == 0xFFFFFFFFu ? 0u : rank16 ? (uint32_t)rank16[sl[q]] : rank_of_slot[sl[q]];
-#endif
+            r[q] = sl[q] == 0xFFFFFFFFu ? 0u : ranked ? sl[q] : rank16 ? (uint32_t)rank16[sl[q]] : rank_of_slot[sl[q]];
         }
 #pragma unroll
         for (int q = 0; q < DFH_B; ++q) {
             if (sl[q] == 0xFFFFFFFFu) continue;
             atomicAdd(&bins[r[q] >> 1], 1u << (16 * (r[q] & 1)));
             /* records carry term ranks from here on: K5 reads them without a gather */
-#if !(defined(DF_ABL) && (DF_ABL & 2))
-            __builtin_nontemporal_store(r[q], &rec_slot[i + (uint64_t)q * DFH_NT]);
-#endif
+            if (i + (uint64_t)q * DFH_NT < ranked_from) __builtin_nontemporal_store(r[q], &rec_slot[i + (uint64_t)q * DFH_NT]);
         }
     }
     __syncthreads();
@@ -653,8 +653,8 @@ __global__ void k_df_colsum(const uint32_t* __restrict__ part, uint32_t nparts, 
  * instead of one dependent gather per iteration */
 constexpr int DFA_B = 8;
 __global__ void k_df_hist_atomic(uint32_t* __restrict__ rec_slot, uint64_t nrec, const uint32_t* __restrict__ nrec_extra,
-                                 const uint32_t* __restrict__ rank_of_slot, uint64_t slot_cap,
-                                 uint32_t* __restrict__ status, uint32_t* __restrict__ df) {
+                                 const uint32_t* __restrict__ rank_of_slot, uint64_t slot_cap, uint64_t ranked_from,
+                                 uint32_t V, uint32_t* __restrict__ status, uint32_t* __restrict__ df) {
     if (nrec_extra) nrec += *nrec_extra;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < nrec; i0 += stride * DFA_B) {
@@ -665,14 +665,17 @@ __global__ void k_df_hist_atomic(uint32_t* __restrict__ rec_slot, uint64_t nrec,
             sl[k] = i < nrec ? rec_slot[i] : 0xFFFFFFFFu;
         }
 #pragma unroll
-        for (int k = 0; k < DFA_B; ++k) r[k] = sl[k] < slot_cap ? rank_of_slot[sl[k]] : 0u;
+        for (int k = 0; k < DFA_B; ++k) {
+            const bool ranked = i0 + (uint64_t)k * stride >= ranked_from;
+            r[k] = ranked ? sl[k] : sl[k] < slot_cap ? rank_of_slot[sl[k]] : 0xFFFFFFFFu;
+        }
 #pragma unroll
         for (int k = 0; k < DFA_B; ++k) {
             const uint64_t i = i0 + (uint64_t)k * stride;
             if (i >= nrec) continue;
-            if (sl[k] >= slot_cap) { atomicOr(status, ST_BOUNDS); continue; }
+            if (r[k] >= V) { atomicOr(status, ST_BOUNDS); continue; }
             atomicAdd(&df[r[k]], 1u);
-            rec_slot[i] = r[k];
+            if (i < ranked_from) rec_slot[i] = r[k];
         }
     }
 }
@@ -692,8 +695,8 @@ constexpr uint32_t DFS_MAXSL = 4096;       /* slice histogram: 16 KB of LDS (V <
 __global__ __launch_bounds__(DFS_NT) void k_dfs_count(uint32_t* __restrict__ rec_slot, uint64_t nrec,
                                                       const uint32_t* __restrict__ nrec_extra,
                                                       const uint32_t* __restrict__ rank_of_slot, uint64_t slot_cap,
-                                                      uint32_t V, uint32_t nsl, uint32_t* __restrict__ status,
-                                                      uint32_t* __restrict__ cnt) {
+                                                      uint64_t ranked_from, uint32_t V, uint32_t nsl,
+                                                      uint32_t* __restrict__ status, uint32_t* __restrict__ cnt) {
     __shared__ uint32_t h[DFS_MAXSL];
     if (nrec_extra) nrec += *nrec_extra;
     for (uint32_t k = threadIdx.x; k < nsl; k += DFS_NT) h[k] = 0;
@@ -708,7 +711,7 @@ __global__ __launch_bounds__(DFS_NT) void k_dfs_count(uint32_t* __restrict__ rec
 #pragma unroll
     for (uint32_t e = 0; e < DFS_PER; ++e) {
         const uint64_t i = t0 + (uint64_t)e * DFS_NT;
-        if (i >= nrec) continue;
+        if (i >= nrec || i >= ranked_from) continue;   /* merged records hold ranks already */
         sl[e] = sl[e] < slot_cap ? rank_of_slot[sl[e]] : 0xFFFFFFFFu;
     }
 #pragma unroll
@@ -716,7 +719,7 @@ __global__ __launch_bounds__(DFS_NT) void k_dfs_count(uint32_t* __restrict__ rec
         const uint64_t i = t0 + (uint64_t)e * DFS_NT;
         if (i >= nrec) continue;
         if (sl[e] >= V) { atomicOr(status, ST_BOUNDS); continue; }   /* never expected */
-        rec_slot[i] = sl[e];   /* records carry term ranks from here on */
+        if (i < ranked_from) rec_slot[i] = sl[e];   /* records carry term ranks from here on */
         atomicAdd(&h[sl[e] / DFS_SLICE], 1u);
     }
     __syncthreads();
@@ -773,6 +776,8 @@ __global__ __launch_bounds__(DFS_NT) void k_dfs_slice(const uint32_t* __restrict
 int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra, uint64_t nrec_max,
                    const uint32_t* rank_of_slot, const uint16_t* rank16, uint32_t V, uint64_t slot_cap,
                    uint32_t* status, uint32_t* df, Arena& ar, hipStream_t s) {
+    /* records [0, nrec) hold vocabulary slots (K1), the merged ones after them term ranks */
+    const uint64_t ranked_from = nrec;
     if (V == 0) return 0;
     if (nrec_max < nrec) nrec_max = nrec;
     if (nrec_max == 0) return hipMemsetAsync(df, 0, (size_t)V * 4, s) == hipSuccess ? 0 : -1;
@@ -783,8 +788,8 @@ int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra
         uint32_t* part = (uint32_t*)ar.get((size_t)nparts * W * 4);
         if (!part) return -2;
         if (hipMemsetAsync(df, 0, (size_t)V * 4, s) != hipSuccess) return -1;
-        k_df_hist_lds<<<nparts, DFH_NT, (size_t)W * 4, s>>>(rec_slot, nrec, nrec_extra, rank_of_slot, rank16, V, slot_cap, status,
-                                                             part);
+        k_df_hist_lds<<<nparts, DFH_NT, (size_t)W * 4, s>>>(rec_slot, nrec, nrec_extra, rank_of_slot, rank16, V, slot_cap,
+                                                             ranked_from, status, part);
         k_df_colsum<<<dim3(grid_for(V), (nparts + DFC_G - 1) / DFC_G), NT, 0, s>>>(part, nparts, V, df);
         ar.release(m);
         return ok();
@@ -799,8 +804,8 @@ int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra
             uint32_t* part = (uint32_t*)ar.get((size_t)nrec_max * 4);
             if (!cnt || !part) return -2;   /* arena too small: the run is retried with a larger one */
             {
-                k_dfs_count<<<(uint32_t)ntiles, DFS_NT, 0, s>>>(rec_slot, nrec, nrec_extra, rank_of_slot, slot_cap, V,
-                                                               nsl, status, cnt);
+                k_dfs_count<<<(uint32_t)ntiles, DFS_NT, 0, s>>>(rec_slot, nrec, nrec_extra, rank_of_slot, slot_cap,
+                                                               ranked_from, V, nsl, status, cnt);
                 if (ok()) return -1;
                 if (scan_excl_u32(cnt, cnt, ntiles * nsl, ar, s)) return -1;
                 k_dfs_scatter<<<(uint32_t)ntiles, DFS_NT, 0, s>>>(rec_slot, nrec, nrec_extra, V, nsl, cnt, part);
@@ -814,7 +819,8 @@ int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra
     }
 #endif
     if (hipMemsetAsync(df, 0, (size_t)V * 4, s) != hipSuccess) return -1;
-    k_df_hist_atomic<<<4096, NT, 0, s>>>(rec_slot, nrec, nrec_extra, rank_of_slot, slot_cap, status, df);
+    k_df_hist_atomic<<<4096, NT, 0, s>>>(rec_slot, nrec, nrec_extra, rank_of_slot, slot_cap, ranked_from, V, status,
+                                         df);
     return ok();
 }
 

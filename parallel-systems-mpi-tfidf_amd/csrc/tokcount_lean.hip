@@ -162,8 +162,8 @@ __device__ __forceinline__ uint32_t claim_chunk(unsigned long long* ctr, uint32_
 
 /* term slot of a token whose term is >= 16 bytes (or runs past the 32-byte window): the
  * token is re-read from HBM (rare for text) */
-__device__ __forceinline__ uint32_t lean_slow_slot(const LeanParams* P, uint64_t p0, uint64_t dend, uint32_t* hot_closed,
-                                                  uint32_t* hid) {
+__device__ __forceinline__ uint32_t lean_slow_slot_in(const LeanParams* P, uint64_t p0, uint64_t dend,
+                                                     uint32_t* hot_closed, uint32_t* hid) {
     const uint8_t* __restrict__ bytes = P->c.bytes;
     uint64_t p = p0;
     while (p < dend && !is_ws(bytes[p])) ++p;
@@ -199,11 +199,28 @@ __device__ __forceinline__ void overflow_record(const LeanParams* P, uint32_t do
     else atomicOr(P->o.status, ST_PART_FULL);
 }
 
+/* The miss paths, out of line (their registers are not the rounds' problem); the hot id
+ * comes back packed with the slot (slot | id << 32), not through memory: a pointer to a
+ * round variable would put it in scratch, and every scratch access waits on vmcnt. */
+__device__ __noinline__ uint64_t lean_slow_slot(const LeanParams* P, uint64_t p0, uint64_t dend, uint32_t* hot_closed) {
+    uint32_t hid = HOT_NONE;
+    const uint32_t sl = lean_slow_slot_in(P, p0, dend, hot_closed, &hid);
+    return ((uint64_t)hid << 32) | sl;
+}
+__device__ __noinline__ uint64_t lean_insert(const LeanParams* P, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3,
+                                             uint32_t* hot_closed) {
+    uint32_t hid = HOT_NONE;
+    const uint32_t sl = vocab_insert_hot(P->v.keys, P->v.rep, P->v.mask, ((uint64_t)k1 << 32) | k0,
+                                         ((uint64_t)k3 << 32) | k2, 0, P->o.status, P->o.hot_slot, P->o.hot_ctr,
+                                         hot_closed, &hid);
+    return ((uint64_t)hid << 32) | sl;
+}
+
 /* Counts `key` the slow way, from bucket b on (home bucket full, a lost claim, or overflow
  * mode).  Returns 1 when this call claimed a slot.  A key not in the table in overflow
  * mode, or after PMAX buckets, becomes a partial record of count 1. */
 constexpr int PMAX = 16;
-__device__ uint32_t bkt_slow(LShared& S, const LeanParams* P, uint32_t key, uint32_t b, bool over, uint32_t gd0,
+__device__ __noinline__ uint32_t bkt_slow(LShared& S, const LeanParams* P, uint32_t key, uint32_t b, bool over, uint32_t gd0,
                              uint32_t sb) {
     for (int probe = 0, tries = 0; probe < PMAX && tries < 64; ++tries) {
         const uint4 kk = bkt_read(S, b);
@@ -487,8 +504,7 @@ __device__ __forceinline__ uint32_t perm_sel(uint32_t n, uint32_t k) {
 
 /* the document-start masks of a step whose window [sbo - 16, sbo + 1008) holds a document
  * start (wave-uniform loop over the group's documents from wr on) */
-__device__ __forceinline__ uint32_t doc_starts(LShared& S, uint32_t wr, uint32_t ng, uint64_t b0, int32_t sbo,
-                                            int32_t gp, uint32_t* dsn_out, uint32_t* base_out, uint32_t* wemp_out) {
+__device__ __noinline__ uint4 doc_starts(LShared& S, uint32_t wr, uint32_t ng, uint64_t b0, int32_t sbo, int32_t gp) {
     uint32_t ds = 0, dsn = 0, base = wr, wemp = 0;
     int32_t sprev = -0x40000000;
     for (uint32_t k = wr; k <= ng; ++k) {
@@ -502,10 +518,7 @@ __device__ __forceinline__ uint32_t doc_starts(LShared& S, uint32_t wr, uint32_t
             dsn |= k > wr ? 1u << (uint32_t)(sk - gp) : 0u;
         }
     }
-    *dsn_out = dsn;
-    *base_out = base;
-    *wemp_out = wemp;
-    return ds;
+    return make_uint4(ds, dsn, base, wemp);   /* by value: no scratch for out-parameters */
 }
 
 }  // namespace
@@ -568,15 +581,12 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_lean(const LeanParam
             if (rare) {
                 const LeanParams* Q = P;
                 asm volatile("" : "+s"(Q));
-                if (len == LEN_LONG) {
-                    const uint32_t st = r.e >> 24;
-                    slot = lean_slow_slot(Q, wbase_cur + (uint64_t)st * WSTEP + (r.e & 1023u), S.gdoc[rel + 1],
-                                          &S.hot_closed, &hid);
-                } else {
-                    slot = vocab_insert_hot(Q->v.keys, Q->v.rep, Q->v.mask, ((uint64_t)r.k1 << 32) | r.k0,
-                                            ((uint64_t)r.k3 << 32) | r.k2, 0, Q->o.status, Q->o.hot_slot,
-                                            Q->o.hot_ctr, &S.hot_closed, &hid);
-                }
+                const uint64_t sh = len == LEN_LONG
+                    ? lean_slow_slot(Q, wbase_cur + (uint64_t)(r.e >> 24) * WSTEP + (r.e & 1023u), S.gdoc[rel + 1],
+                                     &S.hot_closed)
+                    : lean_insert(Q, r.k0, r.k1, r.k2, r.k3, &S.hot_closed);
+                slot = (uint32_t)sh;
+                hid = (uint32_t)(sh >> 32);
             }
         }
         const bool ok = valid && slot != INVALID_SLOT;
@@ -699,20 +709,28 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_lean(const LeanParam
                     const int32_t sbo = (int32_t)(s * WSTEP);    /* first owned byte, group-relative */
                     const int32_t gp = sbo - 16 + (int32_t)lane16; /* this lane's first byte */
                     const uint4 cur = pf0;
+                    /* The wave's next step (or after its last one the next chunk's first) is
+                     * loaded after this step's first round of vocabulary gathers, not now:
+                     * vmcnt completes in issue order, so a corpus load issued here would hold up
+                     * the wait for those gathers with the HBM latency.  Issued behind them it
+                     * has a round's time before the next wait that covers it. */
+                    uint64_t pfa;
                     {
-                        /* the wave's next step, or after its last one the next chunk's first */
                         const bool redirect = ahead && s + NWAVE >= nsteps;
-                        uint64_t a;
                         if (redirect) {
                             const uint64_t nb0 = ncs & ~(uint64_t)15;
-                            a = nb0 - 16 + (uint64_t)wid * WSTEP;
+                            pfa = nb0 - 16 + (uint64_t)wid * WSTEP;
                             pfb = nb0;
                         } else {
-                            a = wbase + (uint64_t)(s + NWAVE) * WSTEP;
+                            pfa = wbase + (uint64_t)(s + NWAVE) * WSTEP;
                         }
-                        a += lane16;
-                        pf0 = ld16(bytes + (a < last_blk ? a : last_blk));
                     }
+                    bool pf_due = true;
+                    auto prefetch = [&]() {
+                        const uint64_t a = pfa + lane16;
+                        pf0 = ld16(bytes + (a < last_blk ? a : last_blk));
+                        pf_due = false;
+                    };
                     reinterpret_cast<uint4*>(stage)[lane] = cur;
                     /* ---- classify (bytes outside the shard read as whitespace) ---- */
                     uint32_t ws = ws_mask16_swar(cur);
@@ -724,7 +742,13 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_lean(const LeanParam
                     }
                     uint32_t ds = 0, dsn = 0, base = wr, wemp = 0;
                     const bool hasdoc = wnext < sbo + (int32_t)WSTEP + 16 || wcur + 16 >= sbo;
-                    if (hasdoc) ds = doc_starts(S, wr, ng, b0, sbo, gp, &dsn, &base, &wemp);
+                    if (hasdoc) {
+                        const uint4 d4 = doc_starts(S, wr, ng, b0, sbo, gp);
+                        ds = d4.x;
+                        dsn = d4.y;
+                        base = d4.z;
+                        wemp = d4.w;
+                    }
                     const uint32_t prev = (lane_prev(ws) >> 15) & 1u;
                     uint32_t own = (lane >= 1 && lane <= 62) ? 0xFFFFu : 0u;
                     if (!(sbo >= own_lo && sbo + (int32_t)WSTEP <= own_hi) && own) {
@@ -743,7 +767,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_lean(const LeanParam
                     const uint32_t nmine = (uint32_t)__popc(starts);
                     const uint32_t incl = wave_incl_scan(nmine);
                     const uint32_t ntok = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-                    if (ntok == 0) continue;
+                    if (ntok == 0) { prefetch(); continue; }
                     tokens_wg += ntok;
                     if (!hasdoc && lane == 0) atomicAdd(&S.dsz[wr], ntok);
                     for (uint32_t tb = 0; tb < ntok; tb += TLW) {
@@ -789,13 +813,21 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_lean(const LeanParam
                             }
                             carry += take;
                             t0 += take;
-                            if (carry == 64u) {   /* a full round: its loads now, the pending round counted */
-                                Round q = fillr;
-                                q.hv = (uint32_t)key_hash(((uint64_t)q.k1 << 32) | q.k0, ((uint64_t)q.k3 << 32) | q.k2) & vmask;
-                                q.s4 = gload(vkeys + q.hv);
-                                q.t4 = gload(vkeys + ((q.hv + 1) & vmask));
-                                if (pending) count(resolve(pend));
-                                pend = q;
+                            if (carry == 64u) {
+                                /* a full round.  Order matters: the pending round is resolved
+                                 * first (its slots were loaded one round ago), then this round's
+                                 * loads go straight into the pending round's registers, now dead,
+                                 * and fly while the pending round is counted in LDS.  Issuing them
+                                 * before the resolve would keep two sets of loaded registers live
+                                 * and the copy between them waits for the loads (vmcnt). */
+                                const uint32_t key = pending ? resolve(pend) : 0u;
+                                pend = fillr;
+                                pend.hv = (uint32_t)key_hash(((uint64_t)pend.k1 << 32) | pend.k0,
+                                                             ((uint64_t)pend.k3 << 32) | pend.k2) & vmask;
+                                pend.s4 = gload(vkeys + pend.hv);
+                                pend.t4 = gload(vkeys + ((pend.hv + 1) & vmask));
+                                if (pf_due) prefetch();
+                                if (pending) count(key);
                                 pending = true;
                                 carry = 0;
                             }
@@ -804,16 +836,17 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_lean(const LeanParam
                         __builtin_amdgcn_wave_barrier();
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                     }
+                    if (pf_due) prefetch();   /* no full round in this step */
                 }
             }
             if (carry) {   /* the group's last, partial round (lanes >= carry hold no token) */
-                Round q = fillr;
-                if ((uint32_t)lane >= carry) q.e = 0u;
-                q.hv = (uint32_t)key_hash(((uint64_t)q.k1 << 32) | q.k0, ((uint64_t)q.k3 << 32) | q.k2) & vmask;
-                q.s4 = gload(vkeys + q.hv);
-                q.t4 = gload(vkeys + ((q.hv + 1) & vmask));
-                if (pending) count(resolve(pend));
-                pend = q;
+                const uint32_t key = pending ? resolve(pend) : 0u;
+                pend = fillr;
+                if ((uint32_t)lane >= carry) pend.e = 0u;
+                pend.hv = (uint32_t)key_hash(((uint64_t)pend.k1 << 32) | pend.k0, ((uint64_t)pend.k3 << 32) | pend.k2) & vmask;
+                pend.s4 = gload(vkeys + pend.hv);
+                pend.t4 = gload(vkeys + ((pend.hv + 1) & vmask));
+                if (pending) count(key);
                 pending = true;
                 carry = 0;
             }
