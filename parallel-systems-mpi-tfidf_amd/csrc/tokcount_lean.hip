@@ -49,12 +49,13 @@ constexpr int NT = 256;                   /* threads per workgroup */
 constexpr int WG_PER_CU = 4;              /* 16 waves per CU */
 constexpr int NWAVE = NT / 64;
 constexpr uint32_t WSTEP = 992;           /* bytes a wave step owns (lanes 1..62) */
-constexpr int TB = 2048;                  /* LDS table entries (u32 key + u32 count): 8 per thread */
-constexpr uint32_t DD = 4;                /* documents of a group with dense hot-term counters */
+constexpr int TB = 3072;                  /* LDS table entries (u32 key + u32 count): 12 per thread */
+constexpr uint32_t DD = 2;                /* documents of a group with dense hot-term counters */
 constexpr uint32_t HW = HOT_MAX / 2;      /* words per document: two u16 counters each */
 constexpr int EPT = TB / NT;
 constexpr uint32_t FILL_LIMIT = TB - NT * 2 - 64; /* claims after which overflow mode starts */
-constexpr int GCAP = 256;                 /* documents per group at most */
+constexpr int GCAP = 128;                 /* documents per group at most */
+constexpr uint32_t BQ = 128;              /* per-wave queue of keys for the bucket table */
 constexpr int TLW = 192;                  /* token entries per wave and pass */
 constexpr uint32_t LEN_LONG = 31u;        /* entry length field: term of >= 16 bytes / past the window */
 constexpr uint32_t BW = 4;                /* LDS table bucket width */
@@ -65,6 +66,7 @@ struct LShared {
     uint32_t TK[TB];                      /* key32 = 1 << 31 | doc-in-group << sb | slot (0: empty) */
     uint32_t TC[TB];                      /* its count */
     uint32_t dense[DD * HW];              /* hot terms of the group's first DD documents: u16 counts */
+    uint32_t bq[NWAVE][BQ];               /* keys waiting for a full round of the bucket table */
     uint64_t gdoc[GCAP + 1];              /* doc_off of the group's documents */
     uint32_t dsz[GCAP];                   /* docSize accumulators */
     union {
@@ -270,10 +272,10 @@ __device__ __forceinline__ uint32_t wave_agg_add_rtn(uint32_t* ctr, uint32_t idx
     return k;
 }
 
-/* The hot-term counters a thread owns in the flush: words w = tid + NT * k (k < 8) of
+/* The hot-term counters a thread owns in the flush: words w = tid + NT * k (k < DPT) of
  * S.dense, i.e. document k / 2, term ids 2 (tid + NT (k & 1)) and that + 1. */
 constexpr int DPT = (int)(DD * HW) / NT;
-static_assert(DPT == 8 && (DD * HW) % NT == 0, "dense words per thread");
+static_assert(HW == 2 * NT && (DD * HW) % NT == 0 && DD <= 4, "dense words per thread");
 __device__ __forceinline__ uint32_t nz16(uint32_t w) { return ((w & 0xFFFFu) != 0u ? 1u : 0u) + ((w >> 16) != 0u ? 1u : 0u); }
 
 /* Emits every table entry and every non-zero hot counter of the group as records and
@@ -631,6 +633,42 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_lean(const LeanParam
         const uint32_t wc = (uint32_t)__popcll(__ballot(claims != 0u));
         if (wc && lane == 0) (void)atomicAdd(&S.fill, wc);
     };
+    /* Keys for the bucket table wait in the wave's queue until 64 of them make a full round:
+     * the hot-term lanes of a round are done after one LDS add, and counting the rest in
+     * rounds of whatever lanes remain would run the whole bucket path for a third of a wave. */
+    uint32_t* const bq = S.bq[wid];
+    uint32_t bq_n = 0;                    /* wave-uniform */
+    auto enqueue = [&](uint32_t key) {
+        const uint64_t m = __ballot(key != 0u);
+        const uint32_t n = (uint32_t)__popcll(m);
+        if (!n) return;
+        const uint32_t pos = bq_n + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (key) bq[pos] = key;
+        bq_n += n;
+        if (bq_n >= 64u) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t k = bq[lane];
+            const uint32_t rest = bq_n - 64u;
+            const uint32_t kr = (uint32_t)lane < rest ? bq[64 + lane] : 0u;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if ((uint32_t)lane < rest) bq[lane] = kr;
+            bq_n = rest;
+            count(k);
+        }
+    };
+    auto drain_queue = [&]() {
+        if (bq_n) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            count((uint32_t)lane < bq_n ? bq[lane] : 0u);
+            bq_n = 0;
+        }
+    };
 
     /* chunk schedule: thread 0 claims from 8 sharded counters, two chunks ahead */
     uint32_t shard = blockIdx.x & 7u;
@@ -827,7 +865,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_lean(const LeanParam
                                 pend.s4 = gload(vkeys + pend.hv);
                                 pend.t4 = gload(vkeys + ((pend.hv + 1) & vmask));
                                 if (pf_due) prefetch();
-                                if (pending) count(key);
+                                if (pending) enqueue(key);
                                 pending = true;
                                 carry = 0;
                             }
@@ -846,11 +884,12 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_lean(const LeanParam
                 pend.hv = (uint32_t)key_hash(((uint64_t)pend.k1 << 32) | pend.k0, ((uint64_t)pend.k3 << 32) | pend.k2) & vmask;
                 pend.s4 = gload(vkeys + pend.hv);
                 pend.t4 = gload(vkeys + ((pend.hv + 1) & vmask));
-                if (pending) count(key);
+                if (pending) enqueue(key);
                 pending = true;
                 carry = 0;
             }
-            if (pending) { count(resolve(pend)); pending = false; }
+            if (pending) { enqueue(resolve(pend)); pending = false; }
+            drain_queue();
             if (ahead) {   /* the next chunk's document offsets, in flight during this flush */
                 const uint32_t nng = (ndl + 1 - ndf) < gcap ? (ndl + 1 - ndf) : gcap;
                 dpre = (uint32_t)tid <= nng ? P->c.doc_off[ndf + tid] : 0ull;
