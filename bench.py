@@ -46,12 +46,14 @@ def hip_device_sync():
         raise RuntimeError("hipDeviceSynchronize failed")
 
 
-K1_SOURCES = {"k_tokcount_st": "tokcount_st.hip",
+K1_SOURCES = {"k_tokcount_st": "tokcount_st.hip", "k_tokcount_win": "tokcount_win.hip",
               "k_tokcount_lean": "tokcount_lean.hip", "k_tokcount_vs": "tokcount_vs.hip", "k_tokcount": "tokcount.hip"}
 
 
 def k1_kernel(flags: int) -> str:
     """The tokenize+count kernel the last run used (tfidf_run_info.flags)."""
+    if flags & tfidf_abi.RUN_K1_WIN:
+        return "k_tokcount_win"
     if flags & tfidf_abi.RUN_K1_LEAN:
         return "k_tokcount_lean"
     if flags & tfidf_abi.RUN_K1_ST:

@@ -56,14 +56,17 @@ struct DevBuf {
     size_t cap = 0;
     int ensure(size_t bytes) {
         if (bytes <= cap && p) return 0;
+        const bool regrow = p != nullptr;
         if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
-        /* 1/8 headroom (at least 4 KiB): sizes that vary a little from run to run (the
-         * record totals after K1's overflow records, the partial-record sort buffers) must
-         * not reallocate in steady state — hipFree synchronises the device and a 1 GB
-         * hipMalloc inside a stage left the GPU idle for ~0.7 ms (the bench counts
-         * allocations in its timed steps).  Near the HBM capacity the headroom is dropped
-         * rather than failing a size that fits exactly. */
-        const size_t want = bytes < 256 ? 256 : bytes + (bytes / 8 > 4096 ? bytes / 8 : 4096);
+        /* 1/8 headroom (at least 4 KiB) on the first allocation, 1/2 on a regrowth: sizes
+         * that vary from run to run (the record totals after K1's overflow records, the
+         * partial-record sort buffers: K1's overflow mode depends on the order in which
+         * workgroups claim LDS entries) must not reallocate in steady state — hipFree
+         * synchronises the device and a 1 GB hipMalloc inside a stage left the GPU idle for
+         * ~0.7 ms (the bench counts allocations in its timed steps).  Near the HBM capacity
+         * the headroom is dropped rather than failing a size that fits exactly. */
+        const size_t head = regrow ? bytes / 2 : bytes / 8;
+        const size_t want = bytes < 256 ? 256 : bytes + (head > 4096 ? head : 4096);
         if (tfidf_dev_malloc(&p, want) == hipSuccess) { cap = want; return 0; }
         (void)hipGetLastError();
         p = nullptr;
@@ -101,8 +104,11 @@ struct tfidf_ctx {
     Xport* xp = nullptr;    /* peers of the DF exchange (RCCL or in-process); owned */
     int rank = 0, nranks = 1;
     bool timing = true;
-    int k1_mode = 0;        /* 0 auto (fused LDS-staged tokcount_st), 1 round-1 kernel (TFIDF_K1=vs),
-                               2 general K1 (TFIDF_K1=general), 4 round-2 kernel (TFIDF_K1=st):
+    int k1_mode = 0;        /* 0 auto (k_tokcount_st up to K1_ST_MAX_CAP slots, k_tokcount_vs beyond),
+                               1 round-1 kernel (TFIDF_K1=vs), 2 general K1 (TFIDF_K1=general),
+                               4 k_tokcount_st at any size <= K1_ST_MAX_CAP (TFIDF_K1=st); the
+                               experimental build only (make experimental, TFIDF_K1_EXPERIMENTAL):
+                               5 lean kernel (TFIDF_K1=lean), 6 windowed kernel (TFIDF_K1=win) —
                                cross-checks and A/B timing */
     bool stamps_on = false; /* env TFIDF_STAMPS=1 with the diagnostic library build */
     uint32_t ablate = 0;    /* env TFIDF_K1_ABLATE: K1 timing experiments, pipeline stops after K1 */
@@ -112,7 +118,8 @@ struct tfidf_ctx {
     DevBuf stamps;
     bool k1_vs = false;     /* last run used the slot-keyed kernel (default) */
     bool k1_st = false;     /* ... and of those the LDS-staged tokcount_st (else tokcount_vs) */
-    bool k1_lean = false;   /* ... or k_tokcount_lean (the default up to K1_ST_MAX_CAP slots) */
+    bool k1_lean = false;   /* ... or k_tokcount_lean (TFIDF_K1=lean) */
+    bool k1_win = false;    /* ... or k_tokcount_win (the default up to K1_WIN_MAX_CAP slots) */
     LeanParams* lp_host = nullptr;   /* pinned staging of k_tokcount_lean's parameter block */
     DevBuf lp_dev;
     hipEvent_t ev[S_NSTAGES + 1];
@@ -252,6 +259,10 @@ int tfidf_open(int device, tfidf_ctx** out) {
     if (km && !strcmp(km, "general")) ctx->k1_mode = 2;
     if (km && !strcmp(km, "vs")) ctx->k1_mode = 1;
     if (km && !strcmp(km, "st")) ctx->k1_mode = 4;
+#ifdef TFIDF_K1_EXPERIMENTAL
+    if (km && !strcmp(km, "lean")) ctx->k1_mode = 5;
+    if (km && !strcmp(km, "win")) ctx->k1_mode = 6;
+#endif
     const char* ks = getenv("TFIDF_STAMPS");
     ctx->stamps_on = ks && ks[0] == '1';
     const char* ka = getenv("TFIDF_K1_ABLATE");
@@ -516,7 +527,7 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     /* K1 variant: the slot-keyed kernel (tokcount_vs.hip) needs a 16-byte aligned corpus
      * base; TFIDF_K1=general selects the general kernel (cross-checks) */
     const bool aligned = (((uintptr_t)c.bytes & 15u) == 0);
-    ctx->k1_vs = aligned && (ctx->k1_mode <= 1 || ctx->k1_mode == 4);
+    ctx->k1_vs = aligned && (ctx->k1_mode <= 1 || ctx->k1_mode >= 4);
     if (ctx->k1_vs && ctx->vcap > K1_VS_MAX_CAP) return TFIDF_E_CAPACITY;
     /* ---- K1 ---- */
     mark(ctx, S_TOKCOUNT);
@@ -553,9 +564,11 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
      * K1_ST_MAX_CAP slots (config 4: ~1e7 terms, nearly every token a new (doc, term) pair)
      * its bucketed LDS count table runs full and the round-1 kernel is 2.3x faster (c4:
      * 11.5 vs 26.2 ms) */
-    ctx->k1_lean = ctx->k1_vs && ctx->k1_mode == 0 && ctx->vcap <= K1_ST_MAX_CAP;
-    ctx->k1_st = ctx->k1_vs && ctx->k1_mode == 4 && ctx->vcap <= K1_ST_MAX_CAP;
-    if (nchunks && ctx->k1_lean) {
+    ctx->k1_win = ctx->k1_vs && ctx->k1_mode == 6 && ctx->vcap <= K1_WIN_MAX_CAP;
+    ctx->k1_lean = ctx->k1_vs && ctx->k1_mode == 5 && ctx->vcap <= K1_ST_MAX_CAP;
+    ctx->k1_st = ctx->k1_vs && (ctx->k1_mode == 0 || ctx->k1_mode == 4) && ctx->vcap <= K1_ST_MAX_CAP;
+#ifdef TFIDF_K1_EXPERIMENTAL
+    if (nchunks && (ctx->k1_lean || ctx->k1_win)) {
         LeanParams& lp = *ctx->lp_host;
         lp.c = c;
         lp.v = vd;
@@ -567,8 +580,11 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
         /* pinned source: the copy is stream-ordered before the launch and the block is not
          * rewritten before the next run's copy (which follows this kernel on the stream) */
         HIPCHK(hipMemcpyAsync(ctx->lp_dev.p, &lp, sizeof(LeanParams), hipMemcpyHostToDevice, s));
-        LCHK(launch_tokcount_lean(ctx->lp_dev.as<LeanParams>(), lp, s));
-    } else if (nchunks && ctx->k1_st)
+        if (ctx->k1_win) LCHK(launch_tokcount_win(ctx->lp_dev.as<LeanParams>(), lp, s));
+        else LCHK(launch_tokcount_lean(ctx->lp_dev.as<LeanParams>(), lp, s));
+    } else
+#endif
+    if (nchunks && ctx->k1_st)
         LCHK(launch_tokcount_st(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
     else if (nchunks && ctx->k1_vs)
         LCHK(launch_tokcount_vs(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
@@ -583,7 +599,9 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
         return 2;
     }
     /* the lean K1's hot-term marks leave the keys before anything else reads them */
+#ifdef TFIDF_K1_EXPERIMENTAL
     if (nchunks && ctx->k1_lean) LCHK(launch_hot_unmark(vd.keys, o.hot_slot, o.hot_ctr, s));
+#endif
     /* the vocabulary's used-slot flags and count are enqueued before the host reads K1's
      * counters: one host round trip for both */
     const uint64_t cap = ctx->vcap;
@@ -681,9 +699,11 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     if (V <= 65536u) { ENSURE(ctx->rank16, (cap + HOT_SLOTS) * 2); r16 = ctx->rank16.as<uint16_t>(); }
     LCHK(launch_vocab_rank(ctx->sorted_dense, ctx->vslot.as<uint32_t>(), V, ctx->rank_of_slot.as<uint32_t>(),
                            ctx->slot_of_rank.as<uint32_t>(), r16, s));
+#ifdef TFIDF_K1_EXPERIMENTAL
     if (nchunks && ctx->k1_lean)
         LCHK(launch_hot_ranks(ctx->rank_of_slot.as<uint32_t>(), r16, cap, ctx->hot_slot.as<uint32_t>(),
                               (const uint32_t*)(cnt + 9), s));
+#endif
     /* ---- partial documents ---- */
     mark(ctx, S_MERGE);
     uint64_t R_total = R_main;
@@ -1126,7 +1146,7 @@ extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info) {
     for (int i = 0; i < S_NSTAGES; ++i) info->ms_stage[i] = ctx->ms_stage[i];
     info->nstages = S_NSTAGES;
     info->flags = (ctx->k1_vs ? TFIDF_RUN_K1_VS : 0u) | (ctx->k1_st ? TFIDF_RUN_K1_ST : 0u) |
-                  (ctx->k1_lean ? TFIDF_RUN_K1_LEAN : 0u);
+                  (ctx->k1_lean ? TFIDF_RUN_K1_LEAN : 0u) | (ctx->k1_win ? TFIDF_RUN_K1_WIN : 0u);
     info->device_allocs = g_dev_allocs.load(std::memory_order_relaxed);
     info->device_alloc_bytes = g_dev_alloc_bytes.load(std::memory_order_relaxed);
     return TFIDF_OK;

@@ -116,6 +116,11 @@ struct LeanParams {
     uint64_t c0, c1;
 };
 int launch_tokcount_lean(const LeanParams* dparams, const LeanParams& h, hipStream_t s);
+/* K1 windowed (tokcount_win.hip): block-wide 8 KiB windows, batched vocabulary loads; the
+ * same parameter block and contract as k_tokcount_lean without hot terms; vocabulary
+ * tables < 2^24 slots */
+int launch_tokcount_win(const LeanParams* dparams, const LeanParams& h, hipStream_t s);
+#define K1_WIN_MAX_CAP (1ull << 22)
 /* after k_tokcount_lean: clear the hot marks from the vocabulary keys (before any other
  * stage reads them) */
 int launch_hot_unmark(uint4* keys, const uint32_t* hot_slot, const uint32_t* hot_ctr, hipStream_t s);

@@ -712,8 +712,8 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_lean(const LeanParam
             gd0_cur = gd0;
             const uint32_t ng = (dlast + 1 - gd0) < gcap ? (dlast + 1 - gd0) : gcap;
             if (gd0 == dfirst && dpre_ok) {
+                static_assert(GCAP < NT, "one thread per group document offset");
                 if ((uint32_t)tid <= ng) S.gdoc[tid] = dpre;
-                if (tid == 0 && ng >= (uint32_t)NT) S.gdoc[NT] = P->c.doc_off[gd0 + NT];
             } else {
                 const uint64_t* doff = P->c.doc_off;
                 for (uint32_t k = tid; k <= ng; k += NT) S.gdoc[k] = doff[gd0 + k];

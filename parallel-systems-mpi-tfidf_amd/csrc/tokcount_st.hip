@@ -36,16 +36,6 @@
 #include "dev_vocab.h"
 #include "kernels.h"
 
-/* timing-only ablation builds (make variant NAME=s1 DEFS=-DK1S_ABL=1; results invalid):
- * 1 no vocabulary loads/compare (slot from the key), 2 no LDS counting, 4 no token rounds,
- * 8 no token entries (walk + flush only), 16 no corpus loads, 32 flush without record
- * writes, 64 flush = table clear only, 128 corpus bytes from the first MiB (no HBM latency),
- * 256 record space without the device atomics (few-document flush), 512 LDS counting with
- * plain read-modify-writes instead of LDS atomics, 1024 keys whose home bucket is full (or whose
- * claim was lost) dropped instead of probing on */
-#ifndef K1S_ABL
-#define K1S_ABL 0
-#endif
 
 /* Diagnostic build only (-DK1_STAMPS, make variant NAME=stamps DEFS=-DK1_STAMPS, run with
  * TFIDF_STAMPS=1): lane 0 of every wave sums s_memtime cycles per phase — 0 chunk set-up
@@ -73,41 +63,21 @@
 
 namespace {
 
-#ifndef K1S_NT
-#define K1S_NT 256
-#endif
-#ifndef K1S_TB
-#define K1S_TB 3584
-#endif
-constexpr int NT = K1S_NT;                /* threads per workgroup */
-#ifndef K1S_WGCU
-#define K1S_WGCU (1024 / K1S_NT)          /* workgroups per CU: 16 waves per CU */
-#endif
-constexpr int WG_PER_CU = K1S_WGCU;
+constexpr int NT = 256;                /* threads per workgroup */
+constexpr int WG_PER_CU = 4;                /* 16 waves per CU */
 constexpr int NWAVE = NT / 64;
 constexpr int WSTEP = 992;                /* bytes a wave step owns: lanes 1..62, one 16-byte group each;
                                              lane 0 holds the 16 bytes before (the byte before
                                              the step), lane 63 the 16 after (terms crossing the
                                              step end): no separate edge loads or edge lanes */
-constexpr int TB = K1S_TB;                /* LDS table entries (u32 key + u32 count): 14 per thread */
+constexpr int TB = 3584;                /* LDS table entries (u32 key + u32 count): 14 per thread */
 constexpr int EPT = TB / NT;
 constexpr uint32_t FILL_LIMIT = TB - NT * 2 - 64; /* claims after which overflow mode starts */
-#ifndef K1S_GCAP
-#define K1S_GCAP 256
-#endif
-constexpr int GCAP = K1S_GCAP;            /* documents per group at most (LDS arrays) */
+constexpr int GCAP = 256;            /* documents per group at most (LDS arrays) */
 static_assert(GCAP <= NT, "one thread per document of a group");
 constexpr uint32_t SLOT_BITS = 28;        /* vocabulary slots < 2^28 */
 constexpr int TLW = 192;                  /* token entries per wave and compaction pass */
 constexpr uint32_t LEN_LONG = 31u;
-#ifndef K1S_ENT
-#define K1S_ENT 0                         /* 1: unrolled token entries (A/B: more spills, slower) */
-#endif
-#ifndef K1S_PIPE
-#define K1S_PIPE 0                        /* 1: the pending round resolved before the next one is built in
-                                             place (no register copy of in-flight loads): 2.37 vs 2.38 ms
-                                             with by-value VocabDev, neither beats the default */
-#endif        /* token entry: term of >= 16 bytes or past the window */
 
 struct StShared {
     uint32_t TK[TB];                      /* key32 = 1 << 31 | doc-in-group << sb | slot (0: empty) */
@@ -167,8 +137,8 @@ __device__ __forceinline__ uint32_t compress4(uint32_t m) {   /* bits 7, 15, 23,
  * the next bucket with room (slots are only emptied by the flush, so a home bucket with an
  * empty slot proves a key is not further on).  With 4-slot buckets a c2 chunk's ~1000
  * keys in 896 buckets leave the home bucket full for ~2.6 % of new keys, which sends about
- * half of all rounds through bkt_slow (0.2 ms of K1, timing-only build K1S_ABL=1024);
- * 8-slot buckets (two ds_read_b128, K1S_BW=8) make that rare but cost the same in compares
+ * half of all rounds through bkt_slow (0.2 ms of K1, measured in round 2 with slow keys
+ * dropped); 8-slot buckets (two ds_read_b128, K1S_BW=8) make that rare but cost the same in compares
  * (c2 2.255 vs 2.222 ms, c5 2.441 vs 2.432 ms): 4-slot buckets stay. */
 #ifndef K1S_BW
 #define K1S_BW 4
@@ -349,11 +319,6 @@ __device__ void st_flush(StShared& S, const K1Out& o, uint32_t gd0, uint32_t ng,
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));   /* keep j * NT + tid out of the chunk loop (no spills) */
     lds_barrier();                  /* every wave's walk is done (the walk state aliases dcnt...) */
-    if (K1S_ABL & 64) {
-        for (int j = 0; j < EPT; ++j) tbl_clear(S, j * NT + tid);
-        lds_barrier();
-        return;
-    }
     if (tid < GCAP) { S.f.dcnt[tid] = 0; S.f.drun[tid] = 0; }
     lds_barrier();
     const uint32_t smask = (1u << sb) - 1u;
@@ -400,7 +365,6 @@ __device__ void st_flush(StShared& S, const K1Out& o, uint32_t gd0, uint32_t ng,
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
         const uint32_t key = ek[j];
-        if ((K1S_ABL & 32) && key) { tbl_clear(S, j * NT + tid); continue; }
         if (key) {
             const uint32_t rel = (key & 0x7FFFFFFFu) >> sb;
             const uint32_t k = wave_agg_add_rtn(&S.f.drun[0], rel);
@@ -429,11 +393,6 @@ __device__ void st_flush_few(StShared& S, const K1Out& o, uint32_t gd0, uint32_t
     asm volatile("" : "+v"(tid));
     const int lane = tid & 63, w = tid >> 6;
     lds_barrier();                  /* every wave's walk is done */
-    if (K1S_ABL & 64) {
-        for (int j = 0; j < EPT; ++j) tbl_clear(S, j * NT + tid);
-        lds_barrier();
-        return;
-    }
     const uint32_t smask = (1u << sb) - 1u;
     uint32_t ek[EPT], ec[EPT];
     uint32_t pk[FEW / 2] = {0, 0, 0, 0};
@@ -492,14 +451,8 @@ __device__ void st_flush_few(StShared& S, const K1Out& o, uint32_t gd0, uint32_t
         const uint32_t off = incl - packed;
         const uint32_t nrec = all & 0xFFFFu, npart = all >> 16;
         unsigned long long a0 = 0, a1 = 0;
-#if K1S_ABL & 256
-        /* timing only: records at a per-workgroup offset, no device atomic round trip */
-        a0 = (unsigned long long)blockIdx.x * 4096ull % (o.rec_cap > 8192 ? o.rec_cap - 8192 : 1);
-        a1 = (unsigned long long)blockIdx.x * 256ull % (o.part_cap > 8192 ? o.part_cap - 8192 : 1);
-#else
         if (lane == 0 && nrec) a0 = atomicAdd(o.rec_alloc, (unsigned long long)nrec);
         if (lane == 32 && npart) a1 = atomicAdd(o.part_alloc, (unsigned long long)npart);
-#endif
         const unsigned long long rb = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(a0 >> 32), 0) << 32) |
                                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a0, 0);
         const unsigned long long pb = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(a1 >> 32), 32) << 32) |
@@ -590,9 +543,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, cons
      * docSize; returns the LDS table key (0: no token) */
     auto resolve = [&](const Round& r) -> uint32_t {
         uint32_t slot = INVALID_SLOT;
-        if (K1S_ABL & 1) {
-            slot = r.kind ? (r.k0 ^ r.k1 * 7u ^ r.k2) & (uint32_t)v.mask : INVALID_SLOT;
-        } else if (r.kind == 1u) {
+        if (r.kind == 1u) {
             const bool hit0 = r.s4.x == r.k0 && r.s4.y == r.k1 && r.s4.z == r.k2 && r.s4.w == r.k3;
             const bool hit1 = r.t4.x == r.k0 && r.t4.y == r.k1 && r.t4.z == r.k2 && r.t4.w == r.k3;
             slot = hit0 ? r.hv : hit1 ? ((r.hv + 1) & (uint32_t)v.mask)
@@ -611,7 +562,6 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, cons
                 atomicAdd(&S.dsz[r.rel], 1u);
             }
         }
-        if (K1S_ABL & 2) return 0u;
         return slot == INVALID_SLOT ? 0u : (0x80000000u | (r.rel << sb) | slot);
     };
     /* The LDS count of a round: ONE ds_read_b128 of the key's home bucket; a match is
@@ -628,20 +578,11 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, cons
             const BktK kk = bkt_read(S, b);
             const uint32_t j = bkt_match(kk, key);
             if (j < BW) {
-#if K1S_ABL & 512
-                S.TC[BW * b + j] += 1u;   /* timing only: plain read-modify-write */
-#else
                 atomicAdd(&S.TC[BW * b + j], 1u);
-#endif
             } else {
                 const uint32_t e = bkt_empty(kk, key);
                 if (e < BW && !over) {
-#if K1S_ABL & 512
-                    const uint32_t old = S.TK[BW * b + e];
-                    if (old == 0u) S.TK[BW * b + e] = key;
-#else
                     const uint32_t old = atomicCAS(&S.TK[BW * b + e], 0u, key);
-#endif
                     if (old == 0u || old == key) {
                         atomicAdd(&S.TC[BW * b + e], 1u);
                         claims = old == 0u ? 1u : 0u;
@@ -653,7 +594,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, cons
                 }
             }
         }
-        if (!(K1S_ABL & 1024) && __ballot(slow) != 0ull) {   /* 1024: timing only, slow keys dropped */
+        if (__ballot(slow) != 0ull) {
             if (slow) claims = bkt_slow(S, o, key, b, over, gd0_cur, sb);
         }
         const uint32_t wc = (uint32_t)__popcll(__ballot(claims != 0u));
@@ -753,18 +694,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, cons
                         const uint64_t a1 = redirect ? nb0 + (uint64_t)wid * WSTEP + lane_off - 16ull
                                                      : gpos + 1ull * NWAVE * WSTEP; /* harmless past ge */
                         if (redirect) pfb = nb0;
-#if K1S_ABL & 128
-                        /* timing only: every step's bytes come from the corpus's first MiB
-                         * (L2/MALL-resident): the cost of the HBM latency of the prefetch */
-                        pf0 = ld16c(c.bytes, last_blk, a1 & ((1ull << 20) - 1ull));
-#elif K1S_ABL & 16
-                        /* timing only: text-like bytes without memory traffic */
-                        const uint32_t hsh = (uint32_t)(a1 >> 4) * 0x9E3779B1u;
-                        pf0 = make_uint4(0x20616263u ^ (hsh & 0x0F0F0F00u), 0x63202061u ^ (hsh & 0x000F0F00u),
-                                         0x61626320u ^ (hsh & 0x00000F0Fu), 0x20206162u ^ (hsh & 0x0F000000u));
-#else
                         pf0 = ld16c(c.bytes, last_blk, a1);
-#endif
                     }
                     /* the step's 64 groups into the wave's stage; this wave's reads of the
                      * previous step were issued before (LDS in order) */
@@ -781,20 +711,13 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, cons
                         wcur = wnext;
                         wnext = uni64(S.gdoc[wr + 1]);
                     }
-                    uint32_t ds = 0, dsn = 0, base = wr;   /* dsn: the starts of documents after wr */
-                    bool wemp = false;   /* wave-uniform: two documents start at one byte (an empty one) */
+                    uint32_t ds = 0, base = wr;
                     if (wnext < sb + WSTEP + 16 || wcur + 16 >= sb) {
-                        uint64_t sprev = ~0ull;
                         for (uint32_t k = wr; k <= ng; ++k) {   /* k = wr: a start AT sb is a start too */
                             const uint64_t sk = uni64(S.gdoc[k]);
                             if (sk >= sb + WSTEP + 16) break;
-                            wemp |= sk == sprev;
-                            sprev = sk;
                             base += (k > wr && sk < gpos) ? 1u : 0u;
-                            if (sk >= gpos && sk < gpos + 16) {
-                                ds |= 1u << (uint32_t)(sk - gpos);
-                                dsn |= k > wr ? 1u << (uint32_t)(sk - gpos) : 0u;
-                            }
+                            if (sk >= gpos && sk < gpos + 16) ds |= 1u << (uint32_t)(sk - gpos);
                         }
                     }
                     const uint32_t prev = (lane_prev(ws) >> 15) & 1u;
@@ -825,39 +748,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, cons
                     const uint32_t ntok = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
                     if (ntok == 0) continue;
                     tokens_wg += ntok;
-                    if (K1S_ABL & 8) { if (lane == 0) atomicAdd(&S.dsz[base], ntok); continue; }
                     for (uint32_t tb = 0; tb < ntok; tb += TLW) {
-#if K1S_ENT
-                        if (!wemp) {
-                            /* straight-line: a lane's first four tokens unrolled (a 16-byte
-                             * group rarely holds more), the document by counting the group's
-                             * document starts at or before the token (every start is a
-                             * distinct document when none is empty) */
-                            uint32_t sm = starts, idx = incl - nmine - tb;
-#pragma unroll
-                            for (int k = 0; k < 4; ++k) {
-                                const uint32_t i = (uint32_t)__builtin_ctz(sm | 0x10000u);
-                                sm &= sm - 1u;
-                                const uint32_t e = ((stop32 >> i) & ~1u) | (nul32 >> i);
-                                const uint32_t tz = (uint32_t)__builtin_ctz(e | 0x80000000u);
-                                const uint32_t len = (e && tz < 16u) ? tz : LEN_LONG;
-                                const uint32_t rel = base + (uint32_t)__popc(dsn & ((2u << i) - 1u));
-                                if (i < 16u && idx < (uint32_t)TLW)
-                                    tl[idx] = ((uint32_t)lane << 4 | i) | (len << 10) | (rel << 16);
-                                ++idx;
-                            }
-                            while (sm) {   /* the rare fifth token and beyond */
-                                const uint32_t i = (uint32_t)__builtin_ctz(sm);
-                                sm &= sm - 1u;
-                                const uint32_t e = ((stop32 >> i) & ~1u) | (nul32 >> i);
-                                const uint32_t tz = (uint32_t)__builtin_ctz(e | 0x80000000u);
-                                const uint32_t len = (e && tz < 16u) ? tz : LEN_LONG;
-                                const uint32_t rel = base + (uint32_t)__popc(dsn & ((2u << i) - 1u));
-                                if (idx < (uint32_t)TLW) tl[idx] = ((uint32_t)lane << 4 | i) | (len << 10) | (rel << 16);
-                                ++idx;
-                            }
-                        } else
-#endif
                         {
                             uint32_t sm = starts, idx = incl - nmine;
                             while (sm) {
@@ -885,18 +776,8 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, cons
                         STP(2);
                         /* ---- rounds of 64 tokens; the vocabulary loads of round r+1 are
                          * issued before round r is counted ---- */
-                        for (uint32_t t0 = 0; t0 < cnt && !(K1S_ABL & 4); t0 += 64) {
-#if K1S_PIPE
-                            /* the pending round is resolved FIRST (its loads were issued one
-                             * round ago), then the next round is built in place and its loads
-                             * fly while the pending round is counted: building into a second
-                             * Round and copying it over (`pend = q`) made the copy wait for
-                             * the loads just issued (s_waitcnt vmcnt(0) every round) */
-                            const uint32_t pkey = pending ? resolve(pend) : 0u;
-                            Round& q = pend;
-#else
+                        for (uint32_t t0 = 0; t0 < cnt; t0 += 64) {
                             Round q;
-#endif
                             const uint32_t t = t0 + lane;
                             const bool val = t < cnt;
                             const uint32_t e = val ? tl[t] : 0u;
@@ -915,19 +796,10 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, cons
                                                 : 0u;
                             /* the home slot and the next one: a key displaced by one slot
                              * (linear probing) resolves without a dependent load */
-#if K1S_ABL & 1
-                            q.s4 = make_uint4(q.k0, q.k1, q.k2, q.k3);
-                            q.t4 = q.s4;
-#else
                             q.s4 = gload(v.keys + q.hv);
                             q.t4 = gload(v.keys + ((q.hv + 1) & (uint32_t)v.mask));
-#endif
-#if K1S_PIPE
-                            if (pending) count(pkey);
-#else
                             if (pending) finish(pend);
                             pend = q;
-#endif
                             pending = true;
                         }
                         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -21,8 +21,9 @@ CLI_PATH = os.path.join(PKG_DIR, "bin", "tfidf")
 TFIDF_CORPUS_DEVICE = 1
 UNIQUE_ID_BYTES = 128
 RUN_K1_VS = 2   # tfidf_run_info.flags (include/tfidf.h): slot-keyed K1 ...
-RUN_K1_ST = 4   # ... run as k_tokcount_st (else k_tokcount_vs)
-RUN_K1_LEAN = 16  # ... run as k_tokcount_lean (default; TFIDF_K1=st: k_tokcount_st)
+RUN_K1_ST = 4   # ... run as k_tokcount_st (the default up to 4M vocabulary slots; else k_tokcount_vs)
+RUN_K1_LEAN = 16  # ... run as k_tokcount_lean (experimental library: TFIDF_LIB=exp TFIDF_K1=lean)
+RUN_K1_WIN = 32   # ... run as k_tokcount_win (experimental library: TFIDF_LIB=exp TFIDF_K1=win)
 
 # exported symbols declared by include/tfidf.h
 EXPORTS = [
