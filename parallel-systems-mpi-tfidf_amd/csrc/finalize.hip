@@ -14,6 +14,7 @@
  *   synthetic    device-side corpus generation (csrc/synth.h)
  */
 #include "dev_common.h"
+#include "dev_vocab.h"
 #include "kernels.h"
 #include "synth.h"
 
@@ -33,12 +34,6 @@ __device__ __forceinline__ uint4 u128_from(uint64_t lo, uint64_t hi) {
     return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
 __device__ __forceinline__ bool u128_eq(uint4 a, uint4 b) { return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w; }
-__device__ __forceinline__ bool u128_lt(uint4 a, uint4 b) {
-    if (a.w != b.w) return a.w < b.w;
-    if (a.z != b.z) return a.z < b.z;
-    if (a.y != b.y) return a.y < b.y;
-    return a.x < b.x;
-}
 }  // namespace
 
 /* ------------------------------------------------------------ vocabulary -- */
@@ -1901,60 +1896,126 @@ int launch_keys_by_rank(const uint4* vkeys, const uint32_t* slot_of_rank, uint32
     k_keys_by_rank<<<grid_for(V), NT, 0, s>>>(vkeys, slot_of_rank, V, out);
     return ok();
 }
-/* a run head of the sorted all-gathered keys starts a union id; the padding key of ranks
- * with fewer terms than the largest (all bytes 0xEE: byte 15 of a real key is 0x00, 0x09
- * or 0xFF) is not a term and gets no id */
-__global__ void k_union_heads(const uint4* __restrict__ k, uint64_t n, uint32_t* __restrict__ head) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint4 x = k[i];
-    const bool pad = x.x == 0xEEEEEEEEu && x.y == 0xEEEEEEEEu && x.z == 0xEEEEEEEEu && x.w == 0xEEEEEEEEu;
-    head[i] = (!pad && (i == 0 || !u128_eq(x, k[i - 1]))) ? 1u : 0u;
+/* ---- the hash-owner DF exchange (engine.cpp exchange_collective) ----
+ * Every term has one owner rank, picked by a hash of its identity key independent of the
+ * vocabulary slot hash.  A rank sends (key, local df) of each of its terms to the term's
+ * owner; the owner sums the df of equal keys in a hash table and answers every received
+ * entry with the global df, in the order received.  Per rank that moves and aggregates
+ * ~V_local entries, where the all-gather union it replaces sorted max V x nranks keys on
+ * every rank. */
+__device__ __forceinline__ uint32_t owner_of(const uint4 k, uint32_t R) {
+    const uint64_t lo = ((uint64_t)k.y << 32) | k.x, hi = ((uint64_t)k.w << 32) | k.z;
+    const uint64_t h = mix64(lo ^ (hi * 0x9E3779B97F4A7C15ull) ^ 0x5851F42D4C957F2Dull);
+    return (uint32_t)(((h >> 32) * (uint64_t)R) >> 32);
 }
-int launch_union_heads(const uint4* sorted, uint64_t n, uint32_t* head, hipStream_t s) {
-    if (!n) return 0;
-    k_union_heads<<<grid_for(n), NT, 0, s>>>(sorted, n, head);
-    return ok();
+constexpr uint32_t XO_MAXR = 1024;   /* ranks (tfidf_group_open's limit) */
+/* per-owner counts of this rank's terms (LDS histogram, one device atomic per block and owner) */
+__global__ void k_owner_count(const uint4* __restrict__ keys, uint32_t V, uint32_t R, uint32_t* __restrict__ cnt) {
+    __shared__ uint32_t h[XO_MAXR];
+    for (uint32_t o = threadIdx.x; o < R; o += blockDim.x) h[o] = 0;
+    __syncthreads();
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < V; r += gridDim.x * blockDim.x)
+        atomicAdd(&h[owner_of(keys[r], R)], 1u);
+    __syncthreads();
+    for (uint32_t o = threadIdx.x; o < R; o += blockDim.x)
+        if (h[o]) atomicAdd(&cnt[o], h[o]);
 }
-/* grank[r] = dense union id of my key r: binary search in the sorted union (with
- * duplicates), id = exclusive head scan at the first match */
-__global__ void k_union_lookup(const uint4* __restrict__ mine, uint32_t V, const uint4* __restrict__ u,
-                               const uint32_t* __restrict__ hscan, uint64_t nu, uint32_t* __restrict__ grank) {
-    uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= V) return;
-    uint4 k = mine[r];
-    uint64_t lo = 0, hi = nu;
-    while (lo < hi) {
-        uint64_t mid = (lo + hi) >> 1;
-        if (u128_lt(u[mid], k)) lo = mid + 1; else hi = mid;
+/* the send buffer grouped by owner (order inside an owner's segment is free: the replies
+ * come back in send order and send_idx maps them to term ranks).  cur[o] starts at 0. */
+__global__ void k_owner_scatter(const uint4* __restrict__ keys, const uint32_t* __restrict__ df, uint32_t V, uint32_t R,
+                                const uint32_t* __restrict__ cnt, uint32_t* __restrict__ cur, uint4* __restrict__ skey,
+                                uint32_t* __restrict__ sdf, uint32_t* __restrict__ sidx) {
+    __shared__ uint32_t h[XO_MAXR], base[XO_MAXR], seg[XO_MAXR];
+    /* segment starts: an exclusive scan of cnt (R <= 1024, serial per 256 entries is cheap) */
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (uint32_t o = 0; o < R; ++o) { seg[o] = acc; acc += cnt[o]; }
     }
-    grank[r] = hscan[lo];
+    for (uint32_t o = threadIdx.x; o < R; o += blockDim.x) h[o] = 0;
+    __syncthreads();
+    const uint32_t r0 = blockIdx.x * blockDim.x * 8;
+    uint32_t own[8], pos[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const uint32_t r = r0 + q * blockDim.x + threadIdx.x;
+        own[q] = r < V ? owner_of(keys[r], R) : 0xFFFFFFFFu;
+        pos[q] = own[q] != 0xFFFFFFFFu ? atomicAdd(&h[own[q]], 1u) : 0u;
+    }
+    __syncthreads();
+    for (uint32_t o = threadIdx.x; o < R; o += blockDim.x) base[o] = h[o] ? seg[o] + atomicAdd(&cur[o], h[o]) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const uint32_t r = r0 + q * blockDim.x + threadIdx.x;
+        if (own[q] == 0xFFFFFFFFu) continue;
+        const uint32_t p = base[own[q]] + pos[q];
+        skey[p] = keys[r];
+        sdf[p] = df[r];
+        sidx[p] = r;
+    }
 }
-int launch_union_lookup(const uint4* my_keys, uint32_t V, const uint4* ukeys, const uint32_t* hscan,
-                        uint64_t nu_sorted, const uint32_t* head, uint32_t* grank, hipStream_t s) {
-    (void)head;
+/* owner side: find-or-insert every received key (vocab_insert_s: the K1 vocabulary's
+ * lock-free insert) and add its df; rslot[i] = the entry's table slot */
+__global__ void k_owner_insert(const uint4* __restrict__ rkey, const uint32_t* __restrict__ rdf, uint64_t n,
+                               uint4* __restrict__ tkey, uint64_t* __restrict__ trep, uint64_t tmask,
+                               uint32_t* __restrict__ tdf, uint32_t* __restrict__ rslot, uint32_t* __restrict__ status) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 k = rkey[i];
+        const uint32_t sl = vocab_insert_s(tkey, trep, tmask, ((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z, 0,
+                                           status);
+        if (sl == INVALID_SLOT) { rslot[i] = 0u; continue; }   /* status says the table was full */
+        atomicAdd(&tdf[sl], rdf[i]);
+        rslot[i] = sl;
+    }
+}
+/* distinct keys the owner holds (its share of the global V) and the replies */
+__global__ void k_owner_reply(const uint32_t* __restrict__ rslot, uint64_t n, const uint32_t* __restrict__ tdf,
+                              uint32_t* __restrict__ reply) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) reply[i] = tdf[rslot[i]];
+}
+__global__ void k_table_used(const uint4* __restrict__ tkey, uint64_t cap, unsigned long long* __restrict__ used) {
+    uint32_t c = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * blockDim.x)
+        c += tkey[i].w != 0xEEEEEEEEu ? 1u : 0u;
+    c = wave_sum(c);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(used, (unsigned long long)c);
+}
+/* sender side: the global df of each sent term back at its rank */
+__global__ void k_owner_back(const uint32_t* __restrict__ back, const uint32_t* __restrict__ sidx, uint32_t V,
+                             uint32_t* __restrict__ df_global) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < V) df_global[sidx[p]] = back[p];
+}
+int launch_owner_partition(const uint4* keys, const uint32_t* df, uint32_t V, uint32_t R, uint32_t* cnt, uint32_t* cur,
+                           uint4* skey, uint32_t* sdf, uint32_t* sidx, hipStream_t s) {
+    if (R < 1 || R > XO_MAXR) return -3;
+    if (hipMemsetAsync(cnt, 0, (size_t)R * 4, s) != hipSuccess || hipMemsetAsync(cur, 0, (size_t)R * 4, s) != hipSuccess)
+        return -1;
     if (!V) return 0;
-    k_union_lookup<<<grid_for(V), NT, 0, s>>>(my_keys, V, ukeys, hscan, nu_sorted, grank);
+    const uint32_t nb = (V + NT * 8 - 1) / (NT * 8);
+    k_owner_count<<<nb < 1024 ? nb : 1024, NT, 0, s>>>(keys, V, R, cnt);
+    k_owner_scatter<<<nb, NT, 0, s>>>(keys, df, V, R, cnt, cur, skey, sdf, sidx);
     return ok();
 }
-__global__ void k_scatter_df(const uint32_t* __restrict__ df, const uint32_t* __restrict__ grank, uint32_t V,
-                             uint32_t* __restrict__ dfv) {
-    uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r < V) dfv[grank[r]] = df[r];
-}
-__global__ void k_gather_df(const uint32_t* __restrict__ dfv, const uint32_t* __restrict__ grank, uint32_t V,
-                            uint32_t* __restrict__ out) {
-    uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r < V) out[r] = dfv[grank[r]];
-}
-int launch_scatter_df(const uint32_t* df_local, const uint32_t* grank, uint32_t V, uint32_t* dfv, hipStream_t s) {
-    if (!V) return 0;
-    k_scatter_df<<<grid_for(V), NT, 0, s>>>(df_local, grank, V, dfv);
+int launch_owner_aggregate(const uint4* rkey, const uint32_t* rdf, uint64_t n, uint4* tkey, uint64_t* trep, uint64_t tcap,
+                           uint32_t* tdf, uint32_t* rslot, uint32_t* reply, unsigned long long* used, uint32_t* status,
+                           hipStream_t s) {
+    if (hipMemsetAsync(tkey, 0xEE, tcap * 16, s) != hipSuccess || hipMemsetAsync(tdf, 0, tcap * 4, s) != hipSuccess ||
+        hipMemsetAsync(used, 0, 8, s) != hipSuccess)
+        return -1;
+    if (n) {
+        const uint64_t nb = (n + NT - 1) / NT;
+        k_owner_insert<<<(unsigned)(nb < 8192 ? nb : 8192), NT, 0, s>>>(rkey, rdf, n, tkey, trep, tcap - 1, tdf, rslot, status);
+        k_owner_reply<<<grid_for(n), NT, 0, s>>>(rslot, n, tdf, reply);
+    }
+    const uint64_t nb = (tcap + NT - 1) / NT;
+    k_table_used<<<(unsigned)(nb < 4096 ? nb : 4096), NT, 0, s>>>(tkey, tcap, used);
     return ok();
 }
-int launch_gather_df(const uint32_t* dfv, const uint32_t* grank, uint32_t V, uint32_t* df_out, hipStream_t s) {
+int launch_owner_back(const uint32_t* back, const uint32_t* sidx, uint32_t V, uint32_t* df_global, hipStream_t s) {
     if (!V) return 0;
-    k_gather_df<<<grid_for(V), NT, 0, s>>>(dfv, grank, V, df_out);
+    k_owner_back<<<grid_for(V), NT, 0, s>>>(back, sidx, V, df_global);
     return ok();
 }
 /* in-process transport's all-reduce: out[i] = sum of rows[r * n + i] over r */

@@ -102,6 +102,22 @@ struct RcclXport final : Xport {
     int allreduce_sum_u32(uint32_t* buf, size_t n, hipStream_t s) override {
         return enqueue([&](ncclComm_t c) { return ncclAllReduce(buf, buf, n, ncclUint32, ncclSum, c, s); });
     }
+    int alltoallv(const void* send, const uint64_t* scnt, void* recv, const uint64_t* rcnt, size_t eb,
+                  hipStream_t s) override {
+        /* point-to-point pairs in one group: over xGMI every pair of GPUs has its own link */
+        return enqueue([&](ncclComm_t c) {
+            ncclResult_t r = ncclGroupStart();
+            uint64_t so = 0, ro = 0;
+            for (int p = 0; p < nranks && r == ncclSuccess; ++p) {
+                if (scnt[p]) r = ncclSend((const uint8_t*)send + so * eb, scnt[p] * eb, ncclUint8, p, c, s);
+                if (r == ncclSuccess && rcnt[p]) r = ncclRecv((uint8_t*)recv + ro * eb, rcnt[p] * eb, ncclUint8, p, c, s);
+                so += scnt[p];
+                ro += rcnt[p];
+            }
+            const ncclResult_t e = ncclGroupEnd();
+            return r != ncclSuccess ? r : e;
+        });
+    }
     void abort() override {
         if (clique) clique->abort_all();
         else if (own) { (void)ncclCommAbort(own); own = nullptr; }
@@ -121,6 +137,7 @@ struct Hub {
     std::vector<const void*> ptr;
     std::vector<int> dev;
     std::vector<uint64_t> w;
+    std::vector<uint64_t> sc;   /* alltoallv: rank r's count for peer p at sc[r * n + p] */
     /* returns false when a rank aborted */
     bool barrier() {
         std::unique_lock<std::mutex> lk(mu);
@@ -200,6 +217,35 @@ struct LocalXport final : Xport {
         if (launch_sum_rows_u32(tmp, (uint32_t)nranks, n, buf, s)) { abort(); return TFIDF_E_HIP; }
         return TFIDF_OK;
     }
+    int alltoallv(const void* send, const uint64_t* scnt, void* recv, const uint64_t* rcnt, size_t eb,
+                  hipStream_t s) override {
+        if (hipStreamSynchronize(s) != hipSuccess) { abort(); return TFIDF_E_HIP; }
+        hub->ptr[rank] = send;
+        for (int p = 0; p < nranks; ++p) hub->sc[(size_t)rank * nranks + p] = scnt[p];
+        if (!hub->barrier()) return TFIDF_E_PEER;
+        int rc = TFIDF_OK;
+        uint64_t ro = 0;
+        for (int p = 0; p < nranks && !rc; ++p) {
+            /* peer p's segment for this rank starts after its segments for ranks < rank */
+            uint64_t so = 0;
+            for (int q = 0; q < rank; ++q) so += hub->sc[(size_t)p * nranks + q];
+            const uint64_t n = hub->sc[(size_t)p * nranks + rank];
+            if (n != rcnt[p]) rc = TFIDF_E_STATE;
+            if (!rc && n) {
+                uint8_t* dst = (uint8_t*)recv + ro * eb;
+                const uint8_t* src = (const uint8_t*)hub->ptr[p] + so * eb;
+                const hipError_t e = hub->dev[p] == device
+                    ? hipMemcpyAsync(dst, src, n * eb, hipMemcpyDeviceToDevice, s)
+                    : hipMemcpyPeerAsync(dst, device, src, hub->dev[p], n * eb, s);
+                if (e != hipSuccess) rc = TFIDF_E_HIP;
+            }
+            ro += rcnt[p];
+        }
+        if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = TFIDF_E_HIP;
+        if (rc) { abort(); return rc; }
+        if (!hub->barrier()) return TFIDF_E_PEER;   /* no send buffer is reused before all copied */
+        return TFIDF_OK;
+    }
     void abort() override { hub->poison(); }
     const char* name() const override { return "local"; }
 };
@@ -250,6 +296,7 @@ int tfidf_group_open(int nranks, const int* devices, uint32_t flags, tfidf_group
         g->hub->ptr.assign((size_t)nranks, nullptr);
         g->hub->dev = dev;
         g->hub->w.assign(2 * (size_t)nranks, 0);
+        g->hub->sc.assign((size_t)nranks * nranks, 0);
         for (int r = 0; r < nranks && !rc; ++r) {
             LocalXport* x = new LocalXport();
             x->hub = g->hub;

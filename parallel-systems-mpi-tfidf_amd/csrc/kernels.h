@@ -212,11 +212,15 @@ int launch_score_order(const K5Args& a, Arena& ar, hipStream_t s, hipStream_t s2
 
 /* multi-GPU vocabulary agreement */
 int launch_keys_by_rank(const uint4* vkeys, const uint32_t* slot_of_rank, uint32_t V, uint4* out, hipStream_t s);
-int launch_union_heads(const uint4* sorted, uint64_t n, uint32_t* head, hipStream_t s);
-int launch_union_lookup(const uint4* my_keys, uint32_t V, const uint4* ukeys, const uint32_t* useq_head_scan,
-                        uint64_t nu_sorted, const uint32_t* head, uint32_t* grank, hipStream_t s);
-int launch_scatter_df(const uint32_t* df_local, const uint32_t* grank, uint32_t V, uint32_t* dfv, hipStream_t s);
-int launch_gather_df(const uint32_t* dfv, const uint32_t* grank, uint32_t V, uint32_t* df_out, hipStream_t s);
+/* hash-owner DF exchange: partition this rank's terms by owner (cnt[R] = terms per owner;
+ * cur[R] scratch), aggregate the received entries on the owner (table of tcap = 2^k slots;
+ * *used = distinct keys), write the returned global df at the term ranks */
+int launch_owner_partition(const uint4* keys, const uint32_t* df, uint32_t V, uint32_t R, uint32_t* cnt, uint32_t* cur,
+                           uint4* skey, uint32_t* sdf, uint32_t* sidx, hipStream_t s);
+int launch_owner_aggregate(const uint4* rkey, const uint32_t* rdf, uint64_t n, uint4* tkey, uint64_t* trep, uint64_t tcap,
+                           uint32_t* tdf, uint32_t* rslot, uint32_t* reply, unsigned long long* used, uint32_t* status,
+                           hipStream_t s);
+int launch_owner_back(const uint32_t* back, const uint32_t* sidx, uint32_t V, uint32_t* df_global, hipStream_t s);
 
 /* synthetic corpus generation on the device */
 struct SynSpecDev;

@@ -124,16 +124,31 @@ __global__ __launch_bounds__(RS_NT) void k_rs_hist(const K* __restrict__ keys, u
     hist[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
 }
 
+/* One digit pass of the LSD sort over a tile of RS_TILE keys: a stable local counting
+ * sort in LDS, then coalesced stores.  Wave w owns the tile's items [w * 512, w * 512 + 512)
+ * in eight rounds of 64; each round's lanes find the lanes with the same digit by eight
+ * ballots (a wave64 multisplit) and take their rank from the wave's running per-digit
+ * counter (wave-private: no barrier per round).  The per-digit counts of the four waves
+ * then give every item its position in the tile's digit-sorted order, the keys are staged
+ * there in LDS, and each thread writes staged items tid, tid + 256, ...: consecutive
+ * threads store consecutive positions of one digit's run (the previous scatter stored
+ * every key straight from its lane, one scattered 16-byte store per key, with three
+ * block barriers per 256 keys).  Global position = the tile's base for the digit (the
+ * digit-major scan of the per-tile histograms) + the offset inside the run. */
 template <typename K, bool FUSED>
 __global__ __launch_bounds__(RS_NT) void k_rs_scatter(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                      K* __restrict__ kout, uint32_t* __restrict__ vout,
                                                      uint64_t n, int p, const uint32_t* __restrict__ offs,
                                                      uint32_t nblocks) {
-    __shared__ uint32_t run[256];
-    __shared__ uint32_t boff[256];
-    __shared__ uint32_t wcnt[RS_NT / 64][256];
+    __shared__ K sk[RS_TILE];
+    __shared__ uint32_t sv[RS_TILE];
+    __shared__ uint32_t wc[RS_NT / 64][256];   /* per-wave running counts, then per-wave prefixes */
+    __shared__ uint32_t dstart[256];           /* tile-local start of each digit's run */
+    __shared__ uint32_t gbase[256];            /* global position of the run */
+    __shared__ uint32_t wsum[RS_NT / 64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    run[tid] = 0;
+#pragma unroll
+    for (int q = 0; q < RS_NT / 64; ++q) wc[q][tid] = 0;
     if (FUSED) {
         /* offs is the raw digit-major histogram: this block's base for digit tid is the
          * count of smaller digits everywhere plus digit tid in earlier blocks */
@@ -153,44 +168,67 @@ __global__ __launch_bounds__(RS_NT) void k_rs_scatter(const K* __restrict__ kin,
             tot += c;
         }
         uint32_t all;
-        boff[tid] = block_excl_scan<RS_NT>(tot, &wcnt[0][0], &all) + pre;
+        gbase[tid] = block_excl_scan<RS_NT>(tot, wsum, &all) + pre;
     } else {
-        boff[tid] = offs[(uint64_t)tid * nblocks + blockIdx.x];
+        gbase[tid] = offs[(uint64_t)tid * nblocks + blockIdx.x];
+        __syncthreads();
+    }
+    const uint64_t t0 = (uint64_t)blockIdx.x * RS_TILE;
+    const uint64_t wb = t0 + (uint64_t)w * (RS_IT * 64);
+    const uint64_t lt = (1ull << lane) - 1ull;
+    K k[RS_IT];
+    uint32_t v[RS_IT], d[RS_IT], r[RS_IT];
+#pragma unroll
+    for (int j = 0; j < RS_IT; ++j) {
+        const uint64_t idx = wb + (uint64_t)j * 64 + lane;
+        const bool valid = idx < n;
+        k[j] = valid ? kin[idx] : K{};
+        v[j] = valid ? vin[idx] : 0u;
+        d[j] = valid ? digit_of(k[j], p) : 0u;
     }
 #pragma unroll
-    for (int q = 0; q < RS_NT / 64; ++q) wcnt[q][tid] = 0;
-    __syncthreads();
-    const uint64_t lt = (1ull << lane) - 1ull;
-    uint64_t base = (uint64_t)blockIdx.x * RS_TILE + tid;
     for (int j = 0; j < RS_IT; ++j) {
-        uint64_t idx = base + (uint64_t)j * RS_NT;
-        bool valid = idx < n;
-        K k{};
-        uint32_t v = 0, d = 0;
-        if (valid) { k = kin[idx]; v = vin[idx]; d = digit_of(k, p); }
+        const bool valid = wb + (uint64_t)j * 64 + lane < n;
         uint64_t m = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
-            bool bit = (d >> b) & 1u;
-            uint64_t bb = __ballot(valid && bit);
+            const bool bit = (d[j] >> b) & 1u;
+            const uint64_t bb = __ballot(valid && bit);
             m &= bit ? bb : ~bb;
         }
-        uint32_t lrank = (uint32_t)__popcll(m & lt);
-        if (valid && lrank == 0) wcnt[w][d] = (uint32_t)__popcll(m);
-        __syncthreads();
-        if (valid) {
-            uint32_t pre = run[d] + lrank;
-            for (int q = 0; q < w; ++q) pre += wcnt[q][d];
-            uint32_t o = boff[d] + pre;
-            kout[o] = k;
-            vout[o] = v;
-        }
-        __syncthreads();
-        uint32_t add = 0;
+        const uint32_t lrank = (uint32_t)__popcll(m & lt);
+        /* the wave's LDS operations run in order: every lane reads the counter before the
+         * group leader adds the group's size */
+        r[j] = valid ? wc[w][d[j]] + lrank : 0u;
+        if (valid && lrank == 0) wc[w][d[j]] += (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    {   /* thread tid = digit tid: wave prefixes and the tile-local run start */
+        uint32_t c[RS_NT / 64], tot = 0;
 #pragma unroll
-        for (int q = 0; q < RS_NT / 64; ++q) { add += wcnt[q][tid]; wcnt[q][tid] = 0; }
-        run[tid] += add;
-        __syncthreads();
+        for (int q = 0; q < RS_NT / 64; ++q) { c[q] = wc[q][tid]; wc[q][tid] = tot; tot += c[q]; }
+        uint32_t all;
+        dstart[tid] = block_excl_scan<RS_NT>(tot, wsum, &all);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RS_IT; ++j) {
+        if (wb + (uint64_t)j * 64 + lane >= n) continue;
+        const uint32_t pos = dstart[d[j]] + wc[w][d[j]] + r[j];
+        sk[pos] = k[j];
+        sv[pos] = v[j];
+    }
+    __syncthreads();
+    const uint32_t tn = n - t0 < (uint64_t)RS_TILE ? (uint32_t)(n - t0) : (uint32_t)RS_TILE;
+#pragma unroll
+    for (int q = 0; q < RS_IT; ++q) {
+        const uint32_t i = (uint32_t)tid + (uint32_t)q * RS_NT;
+        if (i >= tn) continue;
+        const K kk = sk[i];
+        const uint32_t dd = digit_of(kk, p);
+        const uint64_t o = (uint64_t)gbase[dd] + (i - dstart[dd]);
+        kout[o] = kk;
+        vout[o] = sv[i];
     }
 }
 

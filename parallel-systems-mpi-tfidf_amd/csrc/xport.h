@@ -5,7 +5,8 @@
  * (TFIDF.c:209-222,291-326) between OS processes.  Here a context (one GPU shard) talks
  * to its peers through an Xport:
  *
- *   RcclXport   ncclAllGather / ncclAllReduce over xGMI: one communicator rank per GPU,
+ *   RcclXport   ncclAllGather / ncclAllReduce / grouped ncclSend-ncclRecv over xGMI: one
+ *               communicator rank per GPU,
  *               either one process per GPU (tfidf_comm_init, torch.distributed launch) or
  *               one process driving every GPU (tfidf_group_open, ncclCommInitAll).
  *   LocalXport  contexts of one process that share a device (tfidf_group_open with a
@@ -36,6 +37,12 @@ struct Xport {
     virtual int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
     /* in-place device sum of n u32 over the ranks */
     virtual int allreduce_sum_u32(uint32_t* buf, size_t n, hipStream_t s) = 0;
+    /* device all-to-all with per-peer counts of `eb`-byte elements (host arrays of nranks):
+     * this rank's elements for peer p are send[so[p] .. so[p] + scnt[p]) and peer p's for
+     * this rank land at recv[ro[p] ..), so, ro the exclusive prefix sums of scnt, rcnt
+     * (rcnt[p] must equal peer p's scnt[rank]) */
+    virtual int alltoallv(const void* send, const uint64_t* scnt, void* recv, const uint64_t* rcnt, size_t eb,
+                          hipStream_t s) = 0;
     /* a rank failed between collectives: release the peers (they return errors) */
     virtual void abort() = 0;
     virtual const char* name() const = 0;

@@ -2,16 +2,17 @@
 
 K shards of one corpus run through tfidf_group_* on K contexts.  On the one-GPU test box
 the contexts share device 0 and exchange through the in-process transport (xport.h): the
-engine code is the one the RCCL clique runs — the status/size agreement, the padded key
-all-gather, the union radix sort, k_union_heads / k_union_lookup, the DF scatter, the
-all-reduce and the gather.  Against the single-rank oracle (TFIDF.c:209-222,291-326 DF
-combine; :253-273 gather + sort):
+engine code is the one the RCCL clique runs — the status/size agreement, the per-owner
+partition of each rank's terms (a hash of the identity key picks the owner rank), the
+count all-gather, the (key, df) all-to-all, the owners' hash aggregation, the all-to-all
+of the global df back, and the global V.  Against the single-rank oracle (TFIDF.c:209-222,
+291-326 DF combine; :253-273 gather + sort):
   * the shards' GPU-formatted texts, concatenated in rank order, are the oracle's
     output.txt byte for byte;
   * every pair's count, docSize and global DF, and every score, are bit-exact;
   * every rank reports the same global vocabulary size = the oracle's distinct terms.
-The 1-rank RCCL communicator case runs the same exchange with ncclAllGather /
-ncclAllReduce (no `nranks > 1` shortcut any more)."""
+The 1-rank RCCL communicator case runs the same exchange with ncclAllGather and grouped
+ncclSend / ncclRecv (no `nranks > 1` shortcut)."""
 import os
 import shutil
 import subprocess
@@ -138,9 +139,9 @@ def test_group_error_releases_peers():
 
 @pytest.mark.parametrize("failing", [0, 1, 2])
 def test_exchange_failure_after_allgather_aborts_peers(failing, monkeypatch):
-    """A rank-local failure INSIDE the exchange (after the key all-gather, past the
-    agreement: TFIDF_TEST_XFAIL_RANK) aborts the transport; the peers, already on their way
-    into the DF all-reduce, return TFIDF_E_PEER instead of waiting, the group reports the
+    """A rank-local failure INSIDE the exchange (after the per-owner count all-gather, past
+    the agreement: TFIDF_TEST_XFAIL_RANK) aborts the transport; the peers, already on their
+    way into the next collective, return TFIDF_E_PEER instead of waiting, the group reports the
     failing rank's own error, and the next run of the group starts afresh (the in-process
     hub is reset).  The same engine path (exchange_df -> Xport::abort) aborts every RCCL
     communicator of a clique."""
@@ -156,8 +157,9 @@ def test_exchange_failure_after_allgather_aborts_peers(failing, monkeypatch):
 
 
 def test_rccl_single_rank_runs_the_exchange():
-    """A 1-rank RCCL communicator: exchange_df runs (agreement, ncclAllGather of the keys,
-    union, ncclAllReduce) and the results are unchanged."""
+    """A 1-rank RCCL communicator: exchange_df runs (agreement, the count ncclAllGather, the
+    self all-to-all by ncclSend / ncclRecv, the owner aggregation) and the results are
+    unchanged."""
     p = tfidf_configs.plan("c2", scale=0.002)
     data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
     with tfidf_abi.Engine(0) as e:

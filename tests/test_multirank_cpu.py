@@ -3,9 +3,11 @@ exchange that engine.cpp:exchange_df performs with RCCL, restated over torch.dis
 
 Each rank takes its shard of the corpus (contiguous "docN@" strcmp-order ranges,
 tfidf_configs.plan(rank, nranks)), computes its local (term, df) with the oracle, then
-  1. all-gathers its term keys and builds the sorted union -> identical global term ids
-     on every rank (ncclAllGather of identity keys + radix sort in exchange_df),
-  2. all-reduces a dense DF vector over those ids (ncclAllReduce(sum)),
+  1. sends every (term, local df) to the term's owner rank, a hash of the term (the
+     per-owner partition + all-to-all of exchange_df),
+  2. each owner sums the df of equal terms and sends every entry's global df back to its
+     sender in the order received (the owner's hash aggregation + the reply all-to-all);
+     global V = the owners' distinct terms summed,
   3. rescores its pairs with the global DF and N (TFIDF.c:202,243-245).
 The concatenation of the ranks' output lines in rank order must equal the single-rank
 oracle output (the reference's gather + qsort, TFIDF.c:253-273, are not needed).
@@ -48,22 +50,37 @@ def _rank_main(rank, world, port, cfg, scale, outdir):
         # local df per local term (the oracle's df is over this shard's documents)
         df_local = np.zeros(len(terms), dtype=np.int64)
         df_local[loc["term"]] = loc["df"]
-        # 1. key all-gather -> sorted union -> global ids (strcmp order of "word\t")
-        gathered = [None] * world
-        dist.all_gather_object(gathered, terms)
-        union = sorted(set(t for ts in gathered for t in ts), key=lambda t: t + b"\t")
-        gid = {t: i for i, t in enumerate(union)}
-        # 2. dense DF all-reduce
-        dfv = torch.zeros(len(union), dtype=torch.int64)
+        # 1. (term, local df) to the owners; all_gather_object restates the all-to-all
+        import zlib
+        out = [[] for _ in range(world)]
         for t, d in zip(terms, df_local):
-            dfv[gid[t]] = int(d)
-        dist.all_reduce(dfv, op=dist.ReduceOp.SUM)
+            out[zlib.crc32(t) % world].append((t, int(d)))
+        sent = [None] * world
+        dist.all_gather_object(sent, out)
+        recv = [sent[q][rank] for q in range(world)]        # what each peer sent this owner
+        # 2. the owner sums per distinct term and answers every entry in order
+        tot = {}
+        for seg in recv:
+            for t, d in seg:
+                tot[t] = tot.get(t, 0) + d
+        replies = [[tot[t] for t, _ in seg] for seg in recv]
+        back_all = [None] * world
+        dist.all_gather_object(back_all, replies)
+        gdf = {}
+        for o in range(world):
+            for (t, _), g in zip(out[o], back_all[o][rank]):
+                gdf[t] = g
+        nv = torch.tensor([len(tot)], dtype=torch.int64)
+        dist.all_reduce(nv, op=dist.ReduceOp.SUM)
+        if rank == 0:
+            with open(os.path.join(outdir, "vglobal.txt"), "w") as f:
+                f.write(str(int(nv.item())))
         # 3. rescore with global df and N, emit this shard's lines in output order
         N = p["ndocs_total"]
         lines = []
         for d, t, c, ds in zip(loc["doc"], loc["term"], loc["count"], loc["docsize"]):
             w = terms[t]
-            df = int(dfv[gid[w]])
+            df = gdf[w]
             score = (float(c) / float(ds)) * math.log(1.0 * N / df)
             lines.append(b"doc%d@%s\t%s\n" % (int(d), w, (b"%.16f" % score)))
         shard = b"".join(lines)
@@ -87,8 +104,9 @@ def test_two_rank_shards_concatenate_to_single_rank_output(tmp_path, cfg, scale,
         got = f.read()
     p = tfidf_configs.plan(cfg, scale=scale)
     data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
-    ref = oracle_py.run(data, off, p["doc_ids"], p["ndocs_total"], arrays=False)["output_txt"]
-    assert got == ref
+    full = oracle_py.run(data, off, p["doc_ids"], p["ndocs_total"])
+    assert got == full["output_txt"]
+    assert int((tmp_path / "vglobal.txt").read_text()) == len(full["terms"])
 
 
 def test_shard_plan_is_a_partition_in_name_order():
