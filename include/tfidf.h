@@ -34,7 +34,9 @@ enum tfidf_status {
     TFIDF_E_NOINPUT = -6,   /* ./input cannot be opened        (TFIDF.c:100-103) */
     TFIDF_E_NODOC = -7,     /* input/docN cannot be opened     (TFIDF.c:134-138) */
     TFIDF_E_OUTPUT = -8,    /* output.txt cannot be written    (TFIDF.c:274-278) */
-    TFIDF_E_CAPACITY = -9,  /* an internal table could not be grown */
+    TFIDF_E_CAPACITY = -9,  /* an internal table could not be grown, or a term (a token's bytes
+                               up to its first NUL) is 16 MiB or longer: its offset/length
+                               word holds 24 length bits */
     TFIDF_E_STATE = -10,    /* call out of order (e.g. fetch before run) */
     TFIDF_E_PEER = -11      /* another rank of the DF exchange failed (this rank did not) */
 };

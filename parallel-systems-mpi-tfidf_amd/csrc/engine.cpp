@@ -626,9 +626,10 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
         ctx->npairs = 0;
         return 2;
     }
-    /* the hot-term marks of k_tokcount_st (and the lean kernel) leave the keys before anything
-     * else reads them */
-    if (nchunks && (ctx->k1_st || ctx->k1_lean)) LCHK(launch_hot_unmark(vd.keys, o.hot_slot, o.hot_ctr, s));
+    /* the lean K1's hot-term marks leave the keys before anything else reads them */
+#ifdef TFIDF_K1_EXPERIMENTAL
+    if (nchunks && ctx->k1_lean) LCHK(launch_hot_unmark(vd.keys, o.hot_slot, o.hot_ctr, s));
+#endif
     /* the vocabulary's used-slot flags and count are enqueued before the host reads K1's
      * counters: one host round trip for both */
     const uint64_t cap = ctx->vcap;
@@ -726,9 +727,11 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     if (V <= 65536u) { ENSURE(ctx->rank16, (cap + HOT_SLOTS) * 2); r16 = ctx->rank16.as<uint16_t>(); }
     LCHK(launch_vocab_rank(ctx->sorted_dense, ctx->vslot.as<uint32_t>(), V, ctx->rank_of_slot.as<uint32_t>(),
                            ctx->slot_of_rank.as<uint32_t>(), r16, s));
-    if (nchunks && (ctx->k1_st || ctx->k1_lean))
+#ifdef TFIDF_K1_EXPERIMENTAL
+    if (nchunks && ctx->k1_lean)
         LCHK(launch_hot_ranks(ctx->rank_of_slot.as<uint32_t>(), r16, cap, ctx->hot_slot.as<uint32_t>(),
                               (const uint32_t*)(cnt + 9), s));
+#endif
     /* ---- partial documents ---- */
     mark(ctx, S_MERGE);
     uint64_t R_total = R_main;

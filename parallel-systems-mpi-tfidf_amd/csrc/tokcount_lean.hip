@@ -949,3 +949,33 @@ int launch_tokcount_lean(const LeanParams* dparams, const LeanParams& h, hipStre
                                                   (uint32_t)n, h.c.lo, h.c.hi, last_blk);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+/* ---- hot terms after K1 (dev_vocab.h) ---- */
+__global__ void k_hot_unmark(uint4* __restrict__ keys, const uint32_t* __restrict__ hot_slot,
+                             const uint32_t* __restrict__ hot_ctr) {
+    const uint32_t n = min(*hot_ctr, HOT_MAX);
+    for (uint32_t id = threadIdx.x; id < n; id += blockDim.x) {
+        const uint32_t sl = hot_slot[id];
+        keys[sl].w = unhot_w(keys[sl].w);
+    }
+}
+int launch_hot_unmark(uint4* keys, const uint32_t* hot_slot, const uint32_t* hot_ctr, hipStream_t s) {
+    k_hot_unmark<<<1, 1024, 0, s>>>(keys, hot_slot, hot_ctr);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+__global__ void k_hot_ranks(uint32_t* __restrict__ rank_of_slot, uint16_t* __restrict__ rank16, uint64_t cap,
+                            const uint32_t* __restrict__ hot_slot, const uint32_t* __restrict__ hot_ctr) {
+    const uint32_t n = min(*hot_ctr, HOT_MAX);
+    for (uint32_t id = threadIdx.x; id < HOT_MAX; id += blockDim.x) {
+        const uint32_t r = id < n ? rank_of_slot[hot_slot[id]] : 0u;
+        rank_of_slot[cap + id] = r;
+        if (rank16) rank16[cap + id] = (uint16_t)(id < n ? rank16[hot_slot[id]] : 0u);
+    }
+}
+int launch_hot_ranks(uint32_t* rank_of_slot, uint16_t* rank16, uint64_t cap, const uint32_t* hot_slot,
+                     const uint32_t* hot_ctr, hipStream_t s) {
+    static_assert(HOT_SLOTS == HOT_MAX, "rank maps sized for every hot id");
+    k_hot_ranks<<<1, 1024, 0, s>>>(rank_of_slot, rank16, cap, hot_slot, hot_ctr);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

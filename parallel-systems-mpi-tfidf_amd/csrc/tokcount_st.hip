@@ -70,19 +70,10 @@ constexpr int WSTEP = 992;                /* bytes a wave step owns: lanes 1..62
                                              lane 0 holds the 16 bytes before (the byte before
                                              the step), lane 63 the 16 after (terms crossing the
                                              step end): no separate edge loads or edge lanes */
-constexpr int TB = 3072;                  /* LDS table entries (u32 key + u32 count): 12 per thread */
+constexpr int TB = 3584;                /* LDS table entries (u32 key + u32 count): 14 per thread */
 constexpr int EPT = TB / NT;
 constexpr uint32_t FILL_LIMIT = TB - NT * 2 - 64; /* claims after which overflow mode starts */
-constexpr int GCAP = 128;                 /* documents per group at most (LDS arrays) */
-/* Hot terms (dev_vocab.h): the first HOT_MAX distinct short terms of a run carry an id in
- * their vocabulary key; in the group's first DD documents such a token is counted with one
- * LDS add into a dense u16 counter (HW words per document, two counters each) instead of the
- * bucket table's read-compare-add chain.  A group spans at most 16 KiB + BIG_DOC bytes, so
- * no u16 counter can wrap. */
-constexpr uint32_t DD = 2;
-constexpr uint32_t HW = HOT_MAX / 2;
-constexpr int DPT = (int)(DD * HW) / NT;  /* dense words per thread in the flush */
-static_assert(HW == 2 * NT && (DD * HW) % NT == 0 && DD <= 4, "dense words per thread");
+constexpr int GCAP = 256;            /* documents per group at most (LDS arrays) */
 static_assert(GCAP <= NT, "one thread per document of a group");
 constexpr uint32_t SLOT_BITS = 28;        /* vocabulary slots < 2^28 */
 constexpr int TLW = 192;                  /* token entries per wave and compaction pass */
@@ -106,11 +97,9 @@ struct StShared {
         } f;
     };
     uint4 sel[16];                        /* v_perm selectors of a term of length n */
-    uint32_t dense[DD * HW];              /* hot terms of the group's first DD documents: u16 counts */
     uint64_t fbase[8];                    /* st_flush_few: first record of each document */
     uint8_t dpart[GCAP];                  /* document has overflow records */
     uint32_t fill;                        /* table claims of the group */
-    uint32_t hot_closed;                  /* this workgroup saw the hot ids run out */
     uint64_t cur_chunk, nxt_chunk;        /* dynamic chunk schedule: this chunk and the next */
     uint32_t wsum[NWAVE];
     unsigned long long rec_base, part_base;
@@ -221,12 +210,8 @@ __device__ __forceinline__ uint64_t uni64(uint64_t x) {
 /* (VocabDev by reference puts the kernel's copy in scratch, so the rounds reload the table
  * pointer / mask with scratch loads; passed by value it stays in SGPRs, but then 14 more
  * SGPRs spill and K1 measured 2.37-2.38 vs 2.23 ms on c2: kept by reference) */
-/* (the output block's fields by value: a K1Out reference would put the kernel's copy in
- * scratch too, and the flush reads it) */
-__device__ __noinline__ uint64_t slow_slot(const uint8_t* __restrict__ bytes, const VocabDev& v, uint32_t* status,
-                                           uint32_t* hot_slot, uint32_t* hot_ctr, uint32_t* hot_closed, uint64_t p0,
-                                           uint64_t dend) {
-    uint32_t hid = HOT_NONE;
+__device__ __noinline__ uint32_t slow_slot(const uint8_t* __restrict__ bytes, const VocabDev& v, uint64_t p0,
+                                           uint64_t dend, uint32_t* status) {
     uint64_t p = p0;
     while (p < dend && !is_ws(bytes[p])) ++p;
     uint64_t n = 0;
@@ -239,27 +224,14 @@ __device__ __noinline__ uint64_t slow_slot(const uint8_t* __restrict__ bytes, co
             if (k < 8) lo |= b << (8 * k); else hi |= b << (8 * (k - 8));
         }
         make_short_key(lo, hi, (uint32_t)n, &klo, &khi);
-        const uint32_t sl = vocab_insert_hot(v.keys, v.rep, v.mask, klo, khi, 0, status, hot_slot, hot_ctr,
-                                             hot_closed, &hid);
-        return ((uint64_t)hid << 32) | sl;
+        return vocab_insert(v, klo, khi, 0, status);
     }
     make_long_key(bytes + p0, n, &klo, &khi);
     /* rep = (length << 40) | offset holds 24 length bits: a term of 16 MiB or more would be
      * emitted truncated, so the run fails with TFIDF_E_CAPACITY instead */
     if (n >= 0xFFFFFFull) atomicOr(status, ST_TERM_LONG);
     const uint64_t rep = ((n < 0xFFFFFFull ? n : 0xFFFFFFull) << 40) | p0;
-    const uint32_t sl = vocab_insert_hot(v.keys, v.rep, v.mask, klo, khi, rep, status, hot_slot, hot_ctr, hot_closed,
-                                         &hid);
-    return ((uint64_t)hid << 32) | sl;
-}
-/* the vocabulary miss path of a short term (lock-free insert; a new short term of <= 13
- * bytes may take a hot id): hid << 32 | slot */
-__device__ __noinline__ uint64_t miss_slot(const VocabDev& v, uint32_t* status, uint32_t* hot_slot, uint32_t* hot_ctr,
-                                           uint32_t* hot_closed, uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
-    uint32_t hid = HOT_NONE;
-    const uint32_t sl = vocab_insert_hot(v.keys, v.rep, v.mask, ((uint64_t)k1 << 32) | k0, ((uint64_t)k3 << 32) | k2, 0,
-                                         status, hot_slot, hot_ctr, hot_closed, &hid);
-    return ((uint64_t)hid << 32) | sl;
+    return vocab_insert(v, klo, khi, rep, status);
 }
 
 __device__ __noinline__ void overflow_record(unsigned long long* part_alloc, uint64_t part_cap, uint32_t* part_doc,
@@ -342,13 +314,8 @@ __device__ __forceinline__ uint32_t wave_agg_add_rtn(uint32_t* ctr, uint32_t idx
  * size or overflowed to the partial stream.  Per-document counts (wave-aggregated LDS
  * adds), a block scan of them, then every entry is written straight to its record slot
  * (its rank inside its document from a wave-aggregated LDS counter): no LDS staging pass. */
-__device__ __forceinline__ uint32_t nz16(uint32_t w) { return ((w & 0xFFFFu) != 0u ? 1u : 0u) + ((w >> 16) != 0u ? 1u : 0u); }
-
-/* A hot term's record carries slot cap + id (its rank comes from rank_of_slot[cap + id],
- * launch_hot_ranks); the dense counters of document k / 2 of each thread's word k hold the
- * term ids 2 (tid + NT (k & 1)) and that + 1. */
 __device__ void st_flush(StShared& S, const K1Out& o, uint32_t gd0, uint32_t ng, uint64_t cs, uint64_t ce,
-                         uint32_t sb, uint32_t cap) {
+                         uint32_t sb) {
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));   /* keep j * NT + tid out of the chunk loop (no spills) */
     lds_barrier();                  /* every wave's walk is done (the walk state aliases dcnt...) */
@@ -360,11 +327,6 @@ __device__ void st_flush(StShared& S, const K1Out& o, uint32_t gd0, uint32_t ng,
     for (int j = 0; j < EPT; ++j) {
         tbl_read(S, j * NT + tid, ek[j], ec[j]);
         if (ek[j]) wave_agg_add(&S.f.dcnt[0], (ek[j] & 0x7FFFFFFFu) >> sb);
-    }
-#pragma unroll
-    for (int k = 0; k < DPT; ++k) {
-        const uint32_t n = nz16(S.dense[tid + NT * k]);
-        if (n) atomicAdd(&S.f.dcnt[k >> 1], n);
     }
     lds_barrier();
     uint32_t packed = 0;
@@ -417,27 +379,6 @@ __device__ void st_flush(StShared& S, const K1Out& o, uint32_t gd0, uint32_t ng,
             tbl_clear(S, j * NT + tid);
         }
     }
-    auto emit = [&](uint32_t rel, uint32_t k, uint32_t slot, uint32_t c) {
-        const uint32_t dof = S.f.doff[rel];
-        if (S.f.dstate[rel] == 2) {
-            const uint64_t q = rb + (dof & 0xFFFFu) + k;
-            if (rec_ok) { o.rec_slot[q] = slot; o.rec_cnt[q] = c; }
-        } else {
-            const uint64_t q = pb + (dof >> 16) + k;
-            if (part_ok) { o.part_doc[q] = gd0 + rel; o.part_slot[q] = slot; o.part_cnt[q] = c; }
-        }
-    };
-#pragma unroll
-    for (int k = 0; k < DPT; ++k) {
-        const uint32_t w = S.dense[tid + NT * k];
-        if (w) {
-            const uint32_t rel = (uint32_t)k >> 1, id = 2u * ((uint32_t)tid + NT * ((uint32_t)k & 1u));
-            uint32_t r = atomicAdd(&S.f.drun[rel], nz16(w));
-            if (w & 0xFFFFu) emit(rel, r++, cap + id, w & 0xFFFFu);
-            if (w >> 16) emit(rel, r, cap + id + 1u, w >> 16);
-            S.dense[tid + NT * k] = 0u;
-        }
-    }
 }
 
 /* The flush of a group of at most FEW documents (most c2 chunks hold one or two): every
@@ -447,7 +388,7 @@ __device__ void st_flush(StShared& S, const K1Out& o, uint32_t gd0, uint32_t ng,
  * + rank with no LDS atomic.  Same output as st_flush. */
 constexpr uint32_t FEW = 8;
 __device__ void st_flush_few(StShared& S, const K1Out& o, uint32_t gd0, uint32_t ng, uint64_t cs, uint64_t ce,
-                             uint32_t sb, uint32_t cap) {
+                             uint32_t sb) {
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
     const int lane = tid & 63, w = tid >> 6;
@@ -465,14 +406,7 @@ __device__ void st_flush_few(StShared& S, const K1Out& o, uint32_t gd0, uint32_t
                 pk[q] += (rel >> 1) == q ? (1u << (16 * (rel & 1u))) : 0u;
         }
     }
-    /* dense words: document k / 2 of each word k -> field (k / 2) & 1 of pk[k / 4] */
-    uint32_t dw[DPT];
-#pragma unroll
-    for (int k = 0; k < DPT; ++k) {
-        dw[k] = S.dense[tid + NT * k];
-        pk[k >> 2] += nz16(dw[k]) << (16 * ((k >> 1) & 1));
-    }
-    /* block exclusive scan of the FEW/2 packed words (fields never carry: totals <= TB + DD HOT_MAX) */
+    /* block exclusive scan of the FEW/2 packed words (fields never carry: totals <= TB) */
     uint32_t inc[FEW / 2];
 #pragma unroll
     for (uint32_t q = 0; q < FEW / 2; ++q) {
@@ -561,32 +495,6 @@ __device__ void st_flush_few(StShared& S, const K1Out& o, uint32_t gd0, uint32_t
             tbl_clear(S, j * NT + tid);
         }
     }
-    /* dense counters after the table entries: the per-document ranks continue (the scan
-     * counted them in the same order) */
-    auto emit = [&](uint32_t rel, uint32_t slot, uint32_t c) {
-        uint32_t r = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < FEW / 2; ++q)
-            if ((rel >> 1) == q) {
-                r = (rank[q] >> (16 * (rel & 1u))) & 0xFFFFu;
-                rank[q] += 1u << (16 * (rel & 1u));
-            }
-        const uint64_t fb = S.fbase[rel];
-        if (fb != ~0ull) {
-            const uint64_t qq = fb + r;
-            if (S.f.dstate[rel] == 2) { o.rec_slot[qq] = slot; o.rec_cnt[qq] = c; }
-            else { o.part_doc[qq] = gd0 + rel; o.part_slot[qq] = slot; o.part_cnt[qq] = c; }
-        }
-    };
-#pragma unroll
-    for (int k = 0; k < DPT; ++k) {
-        if (dw[k]) {
-            const uint32_t rel = (uint32_t)k >> 1, id = 2u * ((uint32_t)tid + NT * ((uint32_t)k & 1u));
-            if (dw[k] & 0xFFFFu) emit(rel, cap + id, dw[k] & 0xFFFFu);
-            if (dw[k] >> 16) emit(rel, cap + id + 1u, dw[k] >> 16);
-            S.dense[tid + NT * k] = 0u;
-        }
-    }
 }
 
 /* v_perm selector dword k of a term of length n: byte j of the key dword is data byte j
@@ -611,8 +519,6 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, cons
     const uint64_t last_blk = c.nbytes ? ((c.nbytes - 1) & ~(uint64_t)15) : 0;
 
     for (int j = 0; j < EPT; ++j) tbl_clear(S, j * NT + tid);
-    for (uint32_t j = (uint32_t)tid; j < DD * HW; j += NT) S.dense[j] = 0u;
-    if (tid == 0) S.hot_closed = 0u;
     if (tid < 64) {
         const uint32_t n = (uint32_t)tid >> 2, k = (uint32_t)tid & 3u;
         (&S.sel[n].x)[k] = perm_sel(n, k);
@@ -636,23 +542,15 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, cons
     /* resolve a round: vocabulary slot (miss path: lock-free insert / long term) and
      * docSize; returns the LDS table key (0: no token) */
     auto resolve = [&](const Round& r) -> uint32_t {
-        uint32_t slot = INVALID_SLOT, hid = HOT_NONE;
+        uint32_t slot = INVALID_SLOT;
         if (r.kind == 1u) {
-            /* a slot's hot mark (key bytes 14-15) is not part of the term */
-            const bool hit0 = r.s4.x == r.k0 && r.s4.y == r.k1 && r.s4.z == r.k2 && unhot_w(r.s4.w) == r.k3;
-            const bool hit1 = r.t4.x == r.k0 && r.t4.y == r.k1 && r.t4.z == r.k2 && unhot_w(r.t4.w) == r.k3;
-            if (hit0 || hit1) {
-                slot = hit0 ? r.hv : ((r.hv + 1) & (uint32_t)v.mask);
-                hid = hot_id_w(hit0 ? r.s4.w : r.t4.w);
-            } else {
-                const uint64_t sh = miss_slot(v, o.status, o.hot_slot, o.hot_ctr, &S.hot_closed, r.k0, r.k1, r.k2, r.k3);
-                slot = (uint32_t)sh;
-                hid = (uint32_t)(sh >> 32);
-            }
+            const bool hit0 = r.s4.x == r.k0 && r.s4.y == r.k1 && r.s4.z == r.k2 && r.s4.w == r.k3;
+            const bool hit1 = r.t4.x == r.k0 && r.t4.y == r.k1 && r.t4.z == r.k2 && r.t4.w == r.k3;
+            slot = hit0 ? r.hv : hit1 ? ((r.hv + 1) & (uint32_t)v.mask)
+                                      : vocab_insert(v, ((uint64_t)r.k1 << 32) | r.k0, ((uint64_t)r.k3 << 32) | r.k2, 0,
+                                                     o.status);
         } else if (r.kind == 2u) {
-            const uint64_t sh = slow_slot(c.bytes, v, o.status, o.hot_slot, o.hot_ctr, &S.hot_closed, r.ap, S.gdoc[r.rel + 1]);
-            slot = (uint32_t)sh;
-            hid = (uint32_t)(sh >> 32);
+            slot = slow_slot(c.bytes, v, r.ap, S.gdoc[r.rel + 1], o.status);
         }
         /* docSize: one LDS add per wave when the round's tokens share a document */
         const uint64_t vm = __ballot(r.kind != 0u);
@@ -664,12 +562,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, cons
                 atomicAdd(&S.dsz[r.rel], 1u);
             }
         }
-        if (slot == INVALID_SLOT) return 0u;
-        if (hid != HOT_NONE && r.rel < DD) {   /* hot term of one of the first DD documents */
-            atomicAdd(&S.dense[r.rel * HW + (hid >> 1)], 1u << (16u * (hid & 1u)));
-            return 0u;
-        }
-        return 0x80000000u | (r.rel << sb) | slot;
+        return slot == INVALID_SLOT ? 0u : (0x80000000u | (r.rel << sb) | slot);
     };
     /* The LDS count of a round: ONE ds_read_b128 of the key's home bucket; a match is
      * counted with a non-returning add, a new key claims a free slot of the bucket with one
@@ -768,8 +661,8 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, cons
             gd0_cur = gd0;
             const uint32_t ng = (dlast + 1 - gd0) < gcap ? (dlast + 1 - gd0) : gcap;
             if (gd0 == dfirst && dpre_ok) {
-                static_assert(GCAP < NT, "one thread per group document offset");
                 if ((uint32_t)tid <= ng) S.gdoc[tid] = dpre;
+                if (tid == 0 && ng >= (uint32_t)NT) S.gdoc[NT] = c.doc_off[gd0 + NT];
             } else {
                 for (uint32_t k = tid; k <= ng; k += NT) S.gdoc[k] = c.doc_off[gd0 + k];
             }
@@ -929,8 +822,8 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, cons
             lds_barrier();
 #endif
             STP(5);
-            if (ng <= FEW) st_flush_few(S, o, gd0, ng, cs, ce, sb, (uint32_t)v.mask + 1u);
-            else st_flush(S, o, gd0, ng, cs, ce, sb, (uint32_t)v.mask + 1u);
+            if (ng <= FEW) st_flush_few(S, o, gd0, ng, cs, ce, sb);
+            else st_flush(S, o, gd0, ng, cs, ce, sb);
             STP(6);
             if ((uint32_t)tid < ng) {
                 const uint32_t n = S.dsz[tid];
@@ -985,35 +878,5 @@ int launch_tokcount_st(const CorpusDev& c, const uint64_t* chunk_start, const ui
     const uint32_t sb = (uint32_t)__builtin_popcountll(v.mask);
     const uint32_t gcap = (1u << (31u - sb)) >= (uint32_t)GCAP ? (uint32_t)GCAP : (1u << (31u - sb));
     k_tokcount_st<<<(unsigned)grid, NT, 0, s>>>(c, chunk_start, chunk_doc, c0, c1, v, o, sb, gcap);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-/* ---- hot terms after K1 (dev_vocab.h) ---- */
-__global__ void k_hot_unmark(uint4* __restrict__ keys, const uint32_t* __restrict__ hot_slot,
-                             const uint32_t* __restrict__ hot_ctr) {
-    const uint32_t n = min(*hot_ctr, HOT_MAX);
-    for (uint32_t id = threadIdx.x; id < n; id += blockDim.x) {
-        const uint32_t sl = hot_slot[id];
-        keys[sl].w = unhot_w(keys[sl].w);
-    }
-}
-int launch_hot_unmark(uint4* keys, const uint32_t* hot_slot, const uint32_t* hot_ctr, hipStream_t s) {
-    k_hot_unmark<<<1, 1024, 0, s>>>(keys, hot_slot, hot_ctr);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-__global__ void k_hot_ranks(uint32_t* __restrict__ rank_of_slot, uint16_t* __restrict__ rank16, uint64_t cap,
-                            const uint32_t* __restrict__ hot_slot, const uint32_t* __restrict__ hot_ctr) {
-    const uint32_t n = min(*hot_ctr, HOT_MAX);
-    for (uint32_t id = threadIdx.x; id < HOT_MAX; id += blockDim.x) {
-        const uint32_t r = id < n ? rank_of_slot[hot_slot[id]] : 0u;
-        rank_of_slot[cap + id] = r;
-        if (rank16) rank16[cap + id] = (uint16_t)(id < n ? rank16[hot_slot[id]] : 0u);
-    }
-}
-int launch_hot_ranks(uint32_t* rank_of_slot, uint16_t* rank16, uint64_t cap, const uint32_t* hot_slot,
-                     const uint32_t* hot_ctr, hipStream_t s) {
-    static_assert(HOT_SLOTS == HOT_MAX, "rank maps sized for every hot id");
-    k_hot_ranks<<<1, 1024, 0, s>>>(rank_of_slot, rank16, cap, hot_slot, hot_ctr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

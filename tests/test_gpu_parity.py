@@ -461,3 +461,19 @@ def test_score_document_classes_vs_oracle(engine):
     data, off = docs_to_arrays(docs)
     res = check_vs_oracle(engine, data, off)
     assert res["npairs"] > 20000
+
+
+def test_term_of_16_mib_is_a_capacity_error(engine):
+    """A token of 16 MiB or more (one document without whitespace) is legal input for the
+    reference; here its vocabulary entry cannot hold the length (24 bits), and the run
+    fails cleanly with TFIDF_E_CAPACITY (include/tfidf.h) instead of emitting a truncated
+    term.  The same engine then runs a normal corpus."""
+    big = np.full((16 << 20) + 7, ord("a"), dtype=np.uint8)
+    data = np.concatenate([np.frombuffer(b"x y\n", dtype=np.uint8), big])
+    off = np.array([0, 4, len(data)], dtype=np.uint64)
+    with pytest.raises(tfidf_abi.TfidfError) as ei:
+        engine.run_host(data, off)
+    assert ei.value.rc == -9
+    g = load_golden("g1_whitespace")
+    engine.run_host(g["data"], g["off"])
+    assert engine.fetch()["output_txt"] == g["output"]
