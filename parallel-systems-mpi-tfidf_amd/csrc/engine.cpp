@@ -167,7 +167,7 @@ struct tfidf_ctx {
      * owner (key, local df, term rank), the owner side (received keys and df, their table
      * slots, the replies, the aggregation table), the returned global df, the count matrix */
     DevBuf x_mine, x_skey, x_sdf, x_sidx, x_back, x_cnt;
-    DevBuf x_rkey, x_rdf, x_rslot, x_reply, x_tkey, x_trep, x_tdf;
+    DevBuf x_rkey, x_rdf, x_rslot, x_reply, x_tkey, x_tdf;
     /* sizes the local part of a run hands to the exchange and the stages after it */
     uint32_t run_N = 0, run_V = 0;
     uint64_t run_cap = 0, run_R_total = 0;
@@ -324,7 +324,7 @@ void tfidf_close(tfidf_ctx* ctx) {
                       &ctx->doc_toff, &ctx->text, &ctx->out_term, &ctx->out_cnt,
                       &ctx->out_score, &ctx->idf_rank, &ctx->large_list, &ctx->split_tasks, &ctx->cls_off, &ctx->x_mine, &ctx->x_skey, &ctx->x_sdf,
                       &ctx->x_sidx, &ctx->x_back, &ctx->x_cnt, &ctx->x_rkey, &ctx->x_rdf, &ctx->x_rslot, &ctx->x_reply,
-                      &ctx->x_tkey, &ctx->x_trep, &ctx->x_tdf, &ctx->stamps, &ctx->big_list, &ctx->big_idx, &ctx->dense_cnt, &ctx->kcnt,
+                      &ctx->x_tkey, &ctx->x_tdf, &ctx->stamps, &ctx->big_list, &ctx->big_idx, &ctx->dense_cnt, &ctx->kcnt,
                       &ctx->tile_cnt};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i <= S_NSTAGES; ++i) (void)hipEventDestroy(ctx->ev[i]);
@@ -451,8 +451,8 @@ static int exchange_collective(tfidf_ctx* ctx, uint32_t V) {
         return TFIDF_E_HIP;
     }
     /* the owner side, sized from the received count; agreed like step 2 */
-    uint64_t tcap = 1024;
-    while (tcap < 2 * nrecv) tcap *= 2;
+    uint64_t tcap = 1024;   /* load <= 2/3: short probe runs, half the clear of a 2x table */
+    while (tcap < nrecv + nrecv / 2) tcap *= 2;
     int arc = 0;
     auto ens = [&](DevBuf& b, size_t bytes) { if (!arc && b.ensure(bytes) != 0) arc = TFIDF_E_NOMEM; };
     ens(ctx->x_rkey, nrecv * 16 + 16);
@@ -460,7 +460,6 @@ static int exchange_collective(tfidf_ctx* ctx, uint32_t V) {
     ens(ctx->x_rslot, nrecv * 4 + 4);
     ens(ctx->x_reply, nrecv * 4 + 4);
     ens(ctx->x_tkey, tcap * 16);
-    ens(ctx->x_trep, tcap * 8);
     ens(ctx->x_tdf, tcap * 4);
     rc = exchange_agree(ctx, arc, 0, nullptr);
     if (rc == 1) rc = TFIDF_E_STATE;
@@ -471,9 +470,9 @@ static int exchange_collective(tfidf_ctx* ctx, uint32_t V) {
     if (rc) return rc;
     /* the owner: df summed per distinct key, every received entry answered in order */
     unsigned long long* used = cnt + 10;
-    XCHK(launch_owner_aggregate(ctx->x_rkey.as<uint4>(), ctx->x_rdf.as<uint32_t>(), nrecv, ctx->x_tkey.as<uint4>(),
-                                ctx->x_trep.as<uint64_t>(), tcap, ctx->x_tdf.as<uint32_t>(), ctx->x_rslot.as<uint32_t>(),
-                                ctx->x_reply.as<uint32_t>(), used, (uint32_t*)(cnt + 11), s));
+    XCHK(launch_owner_aggregate(ctx->x_rkey.as<uint4>(), ctx->x_rdf.as<uint32_t>(), nrecv, ctx->x_tkey.as<uint4>(), tcap,
+                                ctx->x_tdf.as<uint32_t>(), ctx->x_rslot.as<uint32_t>(), ctx->x_reply.as<uint32_t>(), used,
+                                (uint32_t*)(cnt + 3), s));
     rc = xp->alltoallv(ctx->x_reply.p, rcnt.data(), ctx->x_back.p, scnt.data(), 4, s);
     if (rc) return rc;
     XCHK(launch_owner_back(ctx->x_back.as<uint32_t>(), ctx->x_sidx.as<uint32_t>(), V, ctx->df_global.as<uint32_t>(), s));

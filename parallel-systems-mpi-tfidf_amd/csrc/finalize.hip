@@ -1954,18 +1954,63 @@ __global__ void k_owner_scatter(const uint4* __restrict__ keys, const uint32_t* 
         sidx[p] = r;
     }
 }
-/* owner side: find-or-insert every received key (vocab_insert_s: the K1 vocabulary's
- * lock-free insert) and add its df; rslot[i] = the entry's table slot */
+/* owner side: find-or-insert of a received key into the owner's table (the claim protocol
+ * of the vocabulary's vocab_insert_s: EMPTY -> PENDING by CAS, low word, then the high word
+ * published); *claimed when this call inserted it.  The table holds >= 1.5x the received
+ * entries, so a probe run ends. */
+__device__ uint32_t owner_insert(uint4* __restrict__ keys, uint64_t mask, uint64_t klo, uint64_t khi, bool* claimed) {
+    uint64_t h = key_hash(klo, khi) & mask;
+    for (uint64_t probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
+        unsigned long long* slot = reinterpret_cast<unsigned long long*>(&keys[h]);
+        const uint4 s = keys[h];
+        uint64_t lo = ((uint64_t)s.y << 32) | s.x, hi = ((uint64_t)s.w << 32) | s.z;
+        if (hi == khi && lo == klo) return (uint32_t)h;
+        if (hi != KEY_EMPTY_HI && hi != KEY_PENDING_HI) continue;
+        if (hi == KEY_EMPTY_HI) {
+            const unsigned long long old = atomicCAS(&slot[1], (unsigned long long)KEY_EMPTY_HI,
+                                                     (unsigned long long)KEY_PENDING_HI);
+            if (old == KEY_EMPTY_HI) {
+                atomicExch(&slot[0], (unsigned long long)klo);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                atomicExch(&slot[1], (unsigned long long)khi);
+                *claimed = true;
+                return (uint32_t)h;
+            }
+            hi = old;
+        }
+        while (hi == KEY_PENDING_HI) {
+            __builtin_amdgcn_s_sleep(2);
+            hi = atomicOr(&slot[1], 0ull);
+        }
+        if (hi == khi) {
+            lo = atomicOr(&slot[0], 0ull);
+            if (lo == klo) return (uint32_t)h;
+        }
+    }
+    return INVALID_SLOT;
+}
+/* every received key into the owner's table, its df added; rslot[i] = the entry's slot,
+ * *used += distinct keys (one claim each) */
 __global__ void k_owner_insert(const uint4* __restrict__ rkey, const uint32_t* __restrict__ rdf, uint64_t n,
-                               uint4* __restrict__ tkey, uint64_t* __restrict__ trep, uint64_t tmask,
-                               uint32_t* __restrict__ tdf, uint32_t* __restrict__ rslot, uint32_t* __restrict__ status) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint4 k = rkey[i];
-        const uint32_t sl = vocab_insert_s(tkey, trep, tmask, ((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z, 0,
-                                           status);
-        if (sl == INVALID_SLOT) { rslot[i] = 0u; continue; }   /* status says the table was full */
-        atomicAdd(&tdf[sl], rdf[i]);
-        rslot[i] = sl;
+                               uint4* __restrict__ tkey, uint64_t tmask, uint32_t* __restrict__ tdf,
+                               uint32_t* __restrict__ rslot, unsigned long long* __restrict__ used,
+                               uint32_t* __restrict__ status) {
+    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < n; i0 += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = i0 + threadIdx.x;
+        bool claimed = false;
+        if (i < n) {
+            const uint4 k = rkey[i];
+            const uint32_t sl = owner_insert(tkey, tmask, ((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z, &claimed);
+            if (sl == INVALID_SLOT) {   /* not reachable at the table's load */
+                atomicOr(status, ST_BOUNDS);
+                rslot[i] = 0u;
+            } else {
+                atomicAdd(&tdf[sl], rdf[i]);
+                rslot[i] = sl;
+            }
+        }
+        const uint32_t c = (uint32_t)__popcll(__ballot(claimed));
+        if ((threadIdx.x & 63) == 0 && c) atomicAdd(used, (unsigned long long)c);
     }
 }
 /* distinct keys the owner holds (its share of the global V) and the replies */
@@ -1973,13 +2018,6 @@ __global__ void k_owner_reply(const uint32_t* __restrict__ rslot, uint64_t n, co
                               uint32_t* __restrict__ reply) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) reply[i] = tdf[rslot[i]];
-}
-__global__ void k_table_used(const uint4* __restrict__ tkey, uint64_t cap, unsigned long long* __restrict__ used) {
-    uint32_t c = 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * blockDim.x)
-        c += tkey[i].w != 0xEEEEEEEEu ? 1u : 0u;
-    c = wave_sum(c);
-    if ((threadIdx.x & 63) == 0 && c) atomicAdd(used, (unsigned long long)c);
 }
 /* sender side: the global df of each sent term back at its rank */
 __global__ void k_owner_back(const uint32_t* __restrict__ back, const uint32_t* __restrict__ sidx, uint32_t V,
@@ -1998,19 +2036,17 @@ int launch_owner_partition(const uint4* keys, const uint32_t* df, uint32_t V, ui
     k_owner_scatter<<<nb, NT, 0, s>>>(keys, df, V, R, cnt, cur, skey, sdf, sidx);
     return ok();
 }
-int launch_owner_aggregate(const uint4* rkey, const uint32_t* rdf, uint64_t n, uint4* tkey, uint64_t* trep, uint64_t tcap,
-                           uint32_t* tdf, uint32_t* rslot, uint32_t* reply, unsigned long long* used, uint32_t* status,
-                           hipStream_t s) {
+int launch_owner_aggregate(const uint4* rkey, const uint32_t* rdf, uint64_t n, uint4* tkey, uint64_t tcap, uint32_t* tdf,
+                           uint32_t* rslot, uint32_t* reply, unsigned long long* used, uint32_t* status, hipStream_t s) {
     if (hipMemsetAsync(tkey, 0xEE, tcap * 16, s) != hipSuccess || hipMemsetAsync(tdf, 0, tcap * 4, s) != hipSuccess ||
         hipMemsetAsync(used, 0, 8, s) != hipSuccess)
         return -1;
     if (n) {
         const uint64_t nb = (n + NT - 1) / NT;
-        k_owner_insert<<<(unsigned)(nb < 8192 ? nb : 8192), NT, 0, s>>>(rkey, rdf, n, tkey, trep, tcap - 1, tdf, rslot, status);
+        k_owner_insert<<<(unsigned)(nb < 8192 ? nb : 8192), NT, 0, s>>>(rkey, rdf, n, tkey, tcap - 1, tdf, rslot, used,
+                                                                        status);
         k_owner_reply<<<grid_for(n), NT, 0, s>>>(rslot, n, tdf, reply);
     }
-    const uint64_t nb = (tcap + NT - 1) / NT;
-    k_table_used<<<(unsigned)(nb < 4096 ? nb : 4096), NT, 0, s>>>(tkey, tcap, used);
     return ok();
 }
 int launch_owner_back(const uint32_t* back, const uint32_t* sidx, uint32_t V, uint32_t* df_global, hipStream_t s) {

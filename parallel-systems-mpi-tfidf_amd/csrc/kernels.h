@@ -213,13 +213,12 @@ int launch_score_order(const K5Args& a, Arena& ar, hipStream_t s, hipStream_t s2
 /* multi-GPU vocabulary agreement */
 int launch_keys_by_rank(const uint4* vkeys, const uint32_t* slot_of_rank, uint32_t V, uint4* out, hipStream_t s);
 /* hash-owner DF exchange: partition this rank's terms by owner (cnt[R] = terms per owner;
- * cur[R] scratch), aggregate the received entries on the owner (table of tcap = 2^k slots;
+ * cur[R] scratch), aggregate the received entries on the owner (table of tcap = 2^k >= 1.5 n slots;
  * *used = distinct keys), write the returned global df at the term ranks */
 int launch_owner_partition(const uint4* keys, const uint32_t* df, uint32_t V, uint32_t R, uint32_t* cnt, uint32_t* cur,
                            uint4* skey, uint32_t* sdf, uint32_t* sidx, hipStream_t s);
-int launch_owner_aggregate(const uint4* rkey, const uint32_t* rdf, uint64_t n, uint4* tkey, uint64_t* trep, uint64_t tcap,
-                           uint32_t* tdf, uint32_t* rslot, uint32_t* reply, unsigned long long* used, uint32_t* status,
-                           hipStream_t s);
+int launch_owner_aggregate(const uint4* rkey, const uint32_t* rdf, uint64_t n, uint4* tkey, uint64_t tcap, uint32_t* tdf,
+                           uint32_t* rslot, uint32_t* reply, unsigned long long* used, uint32_t* status, hipStream_t s);
 int launch_owner_back(const uint32_t* back, const uint32_t* sidx, uint32_t V, uint32_t* df_global, hipStream_t s);
 
 /* synthetic corpus generation on the device */
