@@ -100,7 +100,9 @@ int tfidf_abi_version(void);
 
 /* ---- multi-GPU: one process per GPU; replaces MPI_Init/Comm_size/Comm_rank
  *      (TFIDF.c:82,91-92) and the DF combine MPI_Reduce(CustomReduce)+MPI_Bcast
- *      (TFIDF.c:209-222,291-326) with RCCL collectives over xGMI. */
+ *      (TFIDF.c:209-222,291-326) with RCCL collectives over xGMI: each term's global df is
+ *      summed by an owner rank (a hash of the term) after an all-to-all of (term, df) and
+ *      returned by a second all-to-all (grouped ncclSend / ncclRecv). */
 #define TFIDF_UNIQUE_ID_BYTES 128
 int tfidf_comm_unique_id(uint8_t id[TFIDF_UNIQUE_ID_BYTES]);
 /* Attaches an RCCL communicator rank (ncclCommInitRank).  From then on every tfidf_run
@@ -110,7 +112,7 @@ int tfidf_comm_unique_id(uint8_t id[TFIDF_UNIQUE_ID_BYTES]);
  * the others return TFIDF_E_PEER instead of waiting.
  * Abort contract: a failure agreed before the exchange's collectives (a local error, a
  * capacity retry) needs nothing from the caller.  A rank-local failure AFTER the agreement
- * (inside the key all-gather / DF all-reduce sequence) aborts this rank's communicator; its
+ * (inside the count all-gather / (key, df) all-to-all sequence) aborts this rank's communicator; its
  * peers may then be blocked inside a collective, and with one process per GPU only the
  * caller can reach them: it must make every other rank call ncclCommAbort on its own
  * communicator (e.g. by tfidf_close on those contexts after its out-of-band failure notice)

@@ -669,7 +669,8 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     ENSURE(ctx->dseq1, (size_t)N * 4 + 4);
     {
         hipStream_t s2 = ctx->stream2;
-        const size_t need2 = (size_t)256 * 4 * ((N + 2047) / 2048 + 1) + (1u << 20);
+        /* the radix histograms, or the tile sort's staging (20 B per document) */
+        const size_t need2 = (size_t)256 * 4 * ((N + 2047) / 2048 + 1) + (size_t)N * 20 + (1u << 20);
         if (need2 > ctx->arena2_buf.cap && ctx->arena2_buf.ensure(need2) != 0) return TFIDF_E_NOMEM;
         ctx->arena2.base = (uint8_t*)ctx->arena2_buf.p;
         ctx->arena2.cap = ctx->arena2_buf.cap;
@@ -678,8 +679,13 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
         HIPCHK(hipStreamWaitEvent(s2, ctx->ev_fork, 0));
         LCHK(launch_doc_keys(dev_ids, N, ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), s2));
         /* base-11 keys of 10 digits are < 11^10 < 2^35: five bytes, no probe */
-        int dc = radix_sort_u64(ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), ctx->dkey1.as<uint64_t>(),
-                                ctx->dseq1.as<uint32_t>(), N, 0x1Fu, ctx->arena2, s2);
+        /* up to SORT_TILE_MAXN documents: two launches (tile bitonic sort + rank) instead of
+         * two per digit byte */
+        int dc = N <= SORT_TILE_MAXN
+            ? tile_sort_u64(ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), ctx->dkey1.as<uint64_t>(),
+                            ctx->dseq1.as<uint32_t>(), N, ctx->arena2, s2)
+            : radix_sort_u64(ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), ctx->dkey1.as<uint64_t>(),
+                             ctx->dseq1.as<uint32_t>(), N, 0x1Fu, ctx->arena2, s2);
         LCHK(dc);
         ctx->order = dc ? ctx->dseq1.as<uint32_t>() : ctx->dseq0.as<uint32_t>();
         HIPCHK(hipEventRecord(ctx->ev_order, s2));
@@ -793,8 +799,11 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
                 for (uint32_t b = 0; b < (rb + 7) / 8; ++b) pm |= 1u << b;
                 for (uint32_t b = 0; b < (db + 7) / 8; ++b) pm |= 1u << (4 + b);
             }
-            int pc = radix_sort_u64(ctx->pkey0.as<uint64_t>(), ctx->pseq0.as<uint32_t>(), ctx->pkey1.as<uint64_t>(),
-                                    ctx->pseq1.as<uint32_t>(), Qs, pm, ar, s);
+            int pc = Qs <= SORT_TILE_MAXN   /* c2's ~1e5 partial records: two launches, not two per byte */
+                ? tile_sort_u64(ctx->pkey0.as<uint64_t>(), ctx->pseq0.as<uint32_t>(), ctx->pkey1.as<uint64_t>(),
+                                ctx->pseq1.as<uint32_t>(), Qs, ar, s)
+                : radix_sort_u64(ctx->pkey0.as<uint64_t>(), ctx->pseq0.as<uint32_t>(), ctx->pkey1.as<uint64_t>(),
+                                 ctx->pseq1.as<uint32_t>(), Qs, pm, ar, s);
             LCHK(pc);
             uint64_t* pk = pc ? ctx->pkey1.as<uint64_t>() : ctx->pkey0.as<uint64_t>();
             uint32_t* ps = pc ? ctx->pseq1.as<uint32_t>() : ctx->pseq0.as<uint32_t>();
