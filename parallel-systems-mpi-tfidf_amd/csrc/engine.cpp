@@ -713,19 +713,37 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     ENSURE(ctx->slot_of_rank, (size_t)V * 4 + 4);
     LCHK(launch_vocab_compact(vd, cap, ctx->dense.as<uint32_t>(), c, ctx->vslot.as<uint32_t>(), ctx->skey0.as<uint4>(),
                               ctx->seq0.as<uint32_t>(), s));
-    int cur;
     if (V <= SORT_TILE_MAXN) { /* two launches, no varying-byte probe (no host sync) */
-        cur = tile_sort_u128(ctx->skey0.as<uint4>(), ctx->seq0.as<uint32_t>(), ctx->skey1.as<uint4>(),
+        const int cur = tile_sort_u128(ctx->skey0.as<uint4>(), ctx->seq0.as<uint32_t>(), ctx->skey1.as<uint4>(),
                              ctx->seq1.as<uint32_t>(), V, ar, s);
+        LCHK(cur);
+        ctx->sorted_skey = cur ? ctx->skey1.as<uint4>() : ctx->skey0.as<uint4>();
+        ctx->sorted_dense = cur ? ctx->seq1.as<uint32_t>() : ctx->seq0.as<uint32_t>();
     } else {
+        /* two u64 LSD sorts over the varying bytes: the keys' low halves, then (stable) the
+         * high halves gathered in that order; skey0 stays in dense order, skey1 holds the
+         * two u64 ping-pong buffers (c4: 12-byte instead of 20-byte pairs per digit pass) */
         uint32_t vm = 0;
         LCHK(key_varying_bytes_u128(ctx->skey0.as<uint4>(), V, &vm, ar, s));
-        cur = radix_sort_u128(ctx->skey0.as<uint4>(), ctx->seq0.as<uint32_t>(), ctx->skey1.as<uint4>(),
-                              ctx->seq1.as<uint32_t>(), V, vm, ar, s);
+        uint64_t* const ka = (uint64_t*)ctx->skey1.p;
+        uint64_t* const kb = ka + V;
+        uint32_t* const sa = ctx->seq0.as<uint32_t>();
+        uint32_t* const sbq = ctx->seq1.as<uint32_t>();
+        LCHK(launch_sortkey_half(ctx->skey0.as<uint4>(), V, nullptr, 0, ka, s));
+        const int c1 = radix_sort_u64(ka, sa, kb, sbq, V, vm & 0xFFu, ar, s);
+        LCHK(c1);
+        uint64_t* const kc = c1 ? kb : ka;
+        uint32_t* const sc = c1 ? sbq : sa;
+        LCHK(launch_sortkey_half(ctx->skey0.as<uint4>(), V, sc, 1, kc, s));
+        const int c2 = radix_sort_u64(kc, sc, c1 ? ka : kb, c1 ? sa : sbq, V, (vm >> 8) & 0xFFu, ar, s);
+        LCHK(c2);
+        ctx->sorted_dense = c2 ? (c1 ? sa : sbq) : sc;
+        ctx->sorted_skey = nullptr;
+        if (st & ST_HAS_LONG) {   /* the fix-up reads the keys in sorted order */
+            LCHK(launch_gather_u128(ctx->skey0.as<uint4>(), ctx->sorted_dense, V, ctx->skey1.as<uint4>(), s));
+            ctx->sorted_skey = ctx->skey1.as<uint4>();
+        }
     }
-    LCHK(cur);
-    ctx->sorted_skey = cur ? ctx->skey1.as<uint4>() : ctx->skey0.as<uint4>();
-    ctx->sorted_dense = cur ? ctx->seq1.as<uint32_t>() : ctx->seq0.as<uint32_t>();
     if (st & ST_HAS_LONG)   /* terms of >= 16 bytes exist: order the ones tied on 16 bytes */
         LCHK(launch_vocab_long_fixup(ctx->sorted_skey, ctx->sorted_dense, ctx->vslot.as<uint32_t>(), vd, c, V, ar, s));
     uint16_t* r16 = nullptr;

@@ -90,6 +90,33 @@ __global__ void k_vocab_rank(const uint32_t* __restrict__ sorted_dense, const ui
     slot_of_rank[r] = s;
     if (rank16) rank16[s] = (uint16_t)r;
 }
+
+/* The vocabulary sort of large V as two u64 LSD sorts (the low 8 bytes of the 16-byte
+ * strcmp keys, then, stable, the high 8 in that order): every digit pass moves 12-byte
+ * (key half, id) pairs instead of 20-byte (key, id) pairs, for one 8-byte gather of the
+ * high halves between the two sorts.  out[i] = half of k[seq ? seq[i] : i]. */
+__global__ void k_sortkey_half(const uint4* __restrict__ k, uint64_t n, const uint32_t* __restrict__ seq, int hi,
+                               uint64_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint4 x = k[seq ? seq[i] : i];
+    out[i] = hi ? (((uint64_t)x.w << 32) | x.z) : (((uint64_t)x.y << 32) | x.x);
+}
+int launch_sortkey_half(const uint4* k, uint64_t n, const uint32_t* seq, int hi, uint64_t* out, hipStream_t s) {
+    if (!n) return 0;
+    k_sortkey_half<<<grid_for(n), NT, 0, s>>>(k, n, seq, hi, out);
+    return ok();
+}
+__global__ void k_gather_u128(const uint4* __restrict__ k, const uint32_t* __restrict__ seq, uint64_t n,
+                              uint4* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = k[seq[i]];
+}
+int launch_gather_u128(const uint4* k, const uint32_t* seq, uint64_t n, uint4* out, hipStream_t s) {
+    if (!n) return 0;
+    k_gather_u128<<<grid_for(n), NT, 0, s>>>(k, seq, n, out);
+    return ok();
+}
 int launch_vocab_rank(const uint32_t* sorted_dense, const uint32_t* vslot, uint32_t V, uint32_t* rank_of_slot,
                       uint32_t* slot_of_rank, uint16_t* rank16, hipStream_t s) {
     k_vocab_rank<<<grid_for(V), NT, 0, s>>>(sorted_dense, vslot, V, rank_of_slot, slot_of_rank, rank16);

@@ -134,6 +134,10 @@ int launch_hot_ranks(uint32_t* rank_of_slot, uint16_t* rank16, uint64_t cap, con
 int launch_vocab_flags(const VocabDev& v, uint64_t cap, uint32_t* flags, hipStream_t s);
 int launch_vocab_compact(const VocabDev& v, uint64_t cap, const uint32_t* dense_of_slot, const CorpusDev& c,
                          uint32_t* vslot, uint4* sortkey, uint32_t* seq, hipStream_t s);
+/* large-V vocabulary sort as two u64 sorts: key halves (in seq order when seq != null) and
+ * the sorted keys gathered back (long-term fix-up only) */
+int launch_sortkey_half(const uint4* k, uint64_t n, const uint32_t* seq, int hi, uint64_t* out, hipStream_t s);
+int launch_gather_u128(const uint4* k, const uint32_t* seq, uint64_t n, uint4* out, hipStream_t s);
 int launch_vocab_rank(const uint32_t* sorted_dense, const uint32_t* vslot, uint32_t V, uint32_t* rank_of_slot,
                       uint32_t* slot_of_rank, uint16_t* rank16, hipStream_t s);
 /* long terms tied on their first 16 bytes: ordered by iterated segmented sorts (host loop,
