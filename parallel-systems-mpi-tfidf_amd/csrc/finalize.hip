@@ -728,7 +728,9 @@ __global__ __launch_bounds__(DFS_NT) void k_dfs_count(uint32_t* __restrict__ rec
 #pragma unroll
     for (uint32_t e = 0; e < DFS_PER; ++e) {
         const uint64_t i = t0 + (uint64_t)e * DFS_NT;
-        sl[e] = i < nrec ? rec_slot[i] : 0xFFFFFFFFu;
+        /* the records stream through once: non-temporal, so they do not push the rank map
+         * the gathers below hit out of the caches */
+        sl[e] = i < nrec ? __builtin_nontemporal_load(&rec_slot[i]) : 0xFFFFFFFFu;
     }
 #pragma unroll
     for (uint32_t e = 0; e < DFS_PER; ++e) {
@@ -741,7 +743,7 @@ __global__ __launch_bounds__(DFS_NT) void k_dfs_count(uint32_t* __restrict__ rec
         const uint64_t i = t0 + (uint64_t)e * DFS_NT;
         if (i >= nrec) continue;
         if (sl[e] >= V) { atomicOr(status, ST_BOUNDS); continue; }   /* never expected */
-        if (i < ranked_from) rec_slot[i] = sl[e];   /* records carry term ranks from here on */
+        if (i < ranked_from) __builtin_nontemporal_store(sl[e], &rec_slot[i]);   /* records carry term ranks from here on */
         atomicAdd(&h[sl[e] / DFS_SLICE], 1u);
     }
     __syncthreads();
@@ -764,7 +766,7 @@ __global__ __launch_bounds__(DFS_NT) void k_dfs_scatter(const uint32_t* __restri
 #pragma unroll
     for (uint32_t e = 0; e < DFS_PER; ++e) {
         const uint64_t i = t0 + (uint64_t)e * DFS_NT;
-        r[e] = i < nrec ? rec_rank[i] : 0xFFFFFFFFu;
+        r[e] = i < nrec ? __builtin_nontemporal_load(&rec_rank[i]) : 0xFFFFFFFFu;
     }
 #pragma unroll
     for (uint32_t e = 0; e < DFS_PER; ++e) {
