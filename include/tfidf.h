@@ -118,7 +118,7 @@ int tfidf_comm_unique_id(uint8_t id[TFIDF_UNIQUE_ID_BYTES]);
  * communicator (e.g. by tfidf_close on those contexts after its out-of-band failure notice)
  * — tfidf_group_* does exactly this for its clique.  A context whose communicator was
  * aborted returns TFIDF_E_PEER / TFIDF_E_STATE from then on: close and reopen it. */
-int tfidf_comm_init(tfidf_ctx* ctx, const uint8_t id[TFIDF_UNIQUE_ID_BYTES], int rank, int nranks);
+int tfidf_comm_init(tfidf_ctx* ctx, const uint8_t id[TFIDF_UNIQUE_ID_BYTES], int rank, int nranks);   /* nranks <= 1024 */
 
 /* ---- one process, several shards: the drop-in for `mpirun -np P ./TFIDF`
  *      (TFIDF.c:82-92 process group, :125-130 document -> rank assignment, :253-273

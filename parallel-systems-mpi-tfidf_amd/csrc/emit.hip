@@ -7,9 +7,12 @@
  *                double's integer significand with 128-bit arithmetic (glibc printf's
  *                result for every finite x >= 0 below 2^63 / 10^16; scores are
  *                tf * log(N/df) <= log(2^32) < 23)
+ *   digits       u32 arithmetic only: 8-digit halves split into 4 and 2 digits by
+ *                multiply-shift, packed as ASCII words
  *   lines        one wave per document: its lines' lengths, a wave scan for their
- *                offsets, then each lane writes its line into the wave's LDS stage and
- *                the wave copies the round out with 16-byte stores
+ *                offsets, then each lane writes its line into the wave's LDS stage with
+ *                five unaligned stores and the wave copies the round out with 16-byte
+ *                stores
  */
 #include "kernels.h"
 #include "dev_common.h"
@@ -55,26 +58,61 @@ __device__ __forceinline__ bool fixed16(double x, uint64_t& q) {
     return true;
 }
 
-__device__ __forceinline__ uint32_t ndig(uint64_t v) {
+/* decimal digits of a u32 */
+__device__ __forceinline__ uint32_t ndig32(uint32_t v) {
     uint32_t n = 1;
-    while (v >= 10ull) { v /= 10ull; ++n; }
+    for (uint32_t t = 10u; n < 10u && v >= t; t *= 10u) ++n;
     return n;
 }
 
-/* writes v's n decimal digits ending before p + n */
-__device__ __forceinline__ void put_dec(uint8_t* p, uint64_t v, uint32_t n) {
-    for (uint32_t i = n; i-- > 0;) { p[i] = (uint8_t)('0' + (uint32_t)(v % 10ull)); v /= 10ull; }
+/* x < 10^4 as 4 ASCII digits, the most significant in the lowest byte */
+__device__ __forceinline__ uint32_t ascii4(uint32_t x) {
+    const uint32_t h = (x * 5243u) >> 19, l = x - h * 100u;   /* x / 100, exact below 43699 */
+    const uint32_t h1 = (h * 103u) >> 10, l1 = (l * 103u) >> 10; /* y / 10, exact below 179 */
+    return 0x30303030u | h1 | ((h - h1 * 10u) << 8) | (l1 << 16) | ((l - l1 * 10u) << 24);
+}
+/* x < 10^8 as 8 ASCII digits */
+__device__ __forceinline__ uint64_t ascii8(uint32_t x) {
+    const uint32_t a = x / 10000u;
+    return (uint64_t)ascii4(a) | ((uint64_t)ascii4(x - a * 10000u) << 32);
 }
 
-/* "%.16f" of a fixed16 value: integer digits, '.', 16 fraction digits */
-__device__ __forceinline__ uint32_t score_len(uint64_t q) { return ndig(q / P16) + 17u; }
-__device__ __forceinline__ void put_score(uint8_t* p, uint64_t q) {
-    const uint64_t ip = q / P16, fr = q % P16;
-    const uint32_t ni = ndig(ip);
-    put_dec(p, ip, ni);
-    p[ni] = '.';
-    put_dec(p + ni + 1, fr / 100000000ull, 8);
-    put_dec(p + ni + 9, fr % 100000000ull, 8);
+/* unaligned stores (gfx950 DS and global accesses take any byte address) */
+__device__ __forceinline__ void st16(uint8_t* p, uint64_t lo, uint64_t hi) {
+    __builtin_memcpy(p, &lo, 8);
+    __builtin_memcpy(p + 8, &hi, 8);
+}
+__device__ __forceinline__ void st4(uint8_t* p, uint32_t v) { __builtin_memcpy(p, &v, 4); }
+
+/* A score's integer part: q / 10^16 = floor(x), since rounding x * 10^16 to an integer
+ * never reaches the next multiple of 10^16 (the doubles below an integer n >= 1 are at
+ * least 2^-53 > 0.5e-16 from it). */
+struct Score {
+    uint64_t q;      /* round(x * 10^16) */
+    uint32_t ip;     /* integer part, < 923 */
+    uint32_t ni;     /* its digits */
+};
+__device__ __forceinline__ uint32_t ndig3(uint32_t ip) { return ip < 10u ? 1u : ip < 100u ? 2u : 3u; }
+
+/* "%.16f" of q: integer digits, '.', 16 fraction digits, written with three unaligned
+ * stores (the first may write up to 3 bytes past the '.', which the next overwrites) */
+__device__ __forceinline__ void put_score(uint8_t* p, const Score& sc) {
+    const uint64_t fr = sc.q - (uint64_t)sc.ip * P16;
+    const uint32_t f0 = (uint32_t)(fr / 100000000ull), f1 = (uint32_t)(fr - (uint64_t)f0 * 100000000ull);
+    st4(p, (ascii4(sc.ip) >> (8u * (4u - sc.ni))) | (0x2Eu << (8u * sc.ni)));
+    st16(p + sc.ni + 1u, ascii8(f0), ascii8(f1));
+}
+
+/* "doc" id '@' as 16 bytes (3 + at most 10 + 1 used, the rest zero) */
+__device__ __forceinline__ void doc_prefix(uint32_t id, uint32_t nid, uint64_t& lo, uint64_t& hi) {
+    const uint32_t h = id / 100000000u;                                  /* <= 42 */
+    /* the zero-padded 10 digits at bytes 0..9, then the leading zeros shifted out */
+    unsigned __int128 d = (unsigned __int128)(ascii4(h) >> 16) |
+                          ((unsigned __int128)ascii8(id - h * 100000000u) << 16);
+    d >>= 8u * (10u - nid);
+    d = (d << 24) | (unsigned __int128)0x636F64u | ((unsigned __int128)0x40u << (8u * (3u + nid)));
+    lo = (uint64_t)d;
+    hi = (uint64_t)(d >> 64);
 }
 
 /* per term rank: its byte length and where its bytes are (short terms: the 16-byte key,
@@ -121,43 +159,59 @@ __device__ __forceinline__ uint32_t doc_id_of(const EmitArgs& a, uint32_t i) {
     return a.doc_ids ? a.doc_ids[d] : d + 1u;
 }
 
-/* "doc" id '@' word '\t' score '\n' */
-__device__ __forceinline__ uint32_t line_len(const EmitArgs& a, uint32_t nid, uint64_t p, uint64_t& q) {
-    if (!fixed16(a.score[p], q)) { atomicOr(a.status, ST_BOUNDS); q = 0; }
-    return 3u + nid + 1u + a.tlen[a.term[p]] + 1u + score_len(q) + 1u;
+/* the score of pair p; an out-of-range score flags ST_BOUNDS and prints as 0 */
+__device__ __forceinline__ Score score_of(const EmitArgs& a, uint64_t p) {
+    Score sc;
+    const double x = a.score[p];
+    if (fixed16(x, sc.q)) {
+        sc.ip = (uint32_t)x;
+    } else {
+        atomicOr(a.status, ST_BOUNDS);
+        sc.q = 0;
+        sc.ip = 0;
+    }
+    sc.ni = ndig3(sc.ip);
+    return sc;
 }
+/* its integer digits only (the length pass): floor(x) without the exact product, which
+ * only the range check at the top of the range needs */
+__device__ __forceinline__ uint32_t score_ni(const EmitArgs& a, uint64_t p) {
+    const double x = a.score[p];
+    if (!((uint64_t)__double_as_longlong(x) >> 63) && x < 512.0) return ndig3((uint32_t)x);
+    uint64_t q;
+    if (!fixed16(x, q)) { atomicOr(a.status, ST_BOUNDS); return 1u; }
+    return ndig3((uint32_t)x);
+}
+
+/* "doc" id '@' word '\t' score '\n': nid + wl + ni + 23 bytes */
+__device__ __forceinline__ uint32_t line_len(uint32_t nid, uint32_t wl, uint32_t ni) { return nid + wl + ni + 23u; }
 
 __global__ __launch_bounds__(NT) void k_doc_text_bytes(EmitArgs a) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t stride = gridDim.x * (NT / 64);
     for (uint32_t i = blockIdx.x * (NT / 64) + (threadIdx.x >> 6); i < a.ndocs; i += stride) {
         const uint64_t p0 = a.out_off[i], p1 = a.out_off[i + 1];
-        const uint32_t nid = ndig(doc_id_of(a, i));
+        const uint32_t nid = ndig32(doc_id_of(a, i));
         uint64_t sum = 0;
-        for (uint64_t p = p0 + lane; p < p1; p += 64) {
-            uint64_t q;
-            sum += line_len(a, nid, p, q);
-        }
+        for (uint64_t p = p0 + lane; p < p1; p += 64) sum += line_len(nid, a.tlen[a.term[p]], score_ni(a, p));
         /* wave sum of 64-bit values: two 32-bit halves (a document's text < 2^32 * 64) */
         const uint32_t lo = wave_sum((uint32_t)sum & 0xFFFFFFu), hi = wave_sum((uint32_t)(sum >> 24));
         if (lane == 0) a.doc_bytes[i] = (uint64_t)lo + ((uint64_t)hi << 24);
     }
 }
 
-/* writes one line ("doc" id '@' word '\t' score '\n') of a short term at o */
-__device__ __forceinline__ void put_line(uint8_t* o, uint32_t id, uint32_t nid, const uint4& k, uint32_t wl,
-                                         uint64_t q) {
-    o[0] = 'd'; o[1] = 'o'; o[2] = 'c';
-    put_dec(o + 3, id, nid);
-    o += 3 + nid;
-    *o++ = '@';
-    const uint32_t w[4] = {k.x, k.y, k.z, k.w};
-    for (uint32_t j = 0; j < wl; ++j) o[j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
-    o += wl;
-    *o++ = '\t';
-    put_score(o, q);
-    o += score_len(q);
-    *o = '\n';
+/* writes one line ("doc" id '@' word '\t' score '\n') of a short term at o, with
+ * unaligned stores that stay inside the line: the 16-byte prefix (its zero tail is
+ * overwritten by the word), the 16-byte key (word, its TAB, then bytes the score
+ * overwrites), the score, the newline */
+__device__ __forceinline__ void put_line(uint8_t* o, uint64_t pre_lo, uint64_t pre_hi, uint32_t nid, const uint4& k,
+                                         uint32_t wl, const Score& sc) {
+    st16(o, pre_lo, pre_hi);
+    o += 4u + nid;
+    st16(o, ((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z);
+    o += wl + 1u;
+    put_score(o, sc);
+    o[sc.ni + 17u] = '\n';
 }
 
 /* One wave per document.  A round of 64 lines is assembled in the wave's LDS stage at
@@ -172,22 +226,29 @@ __global__ __launch_bounds__(NT) void k_doc_text_write(EmitArgs a) {
     const uint32_t stride = gridDim.x * (NT / 64);
     for (uint32_t i = blockIdx.x * (NT / 64) + (threadIdx.x >> 6); i < a.ndocs; i += stride) {
         const uint64_t p0 = a.out_off[i], p1 = a.out_off[i + 1];
-        const uint32_t id = doc_id_of(a, i), nid = ndig(id);
+        const uint32_t id = doc_id_of(a, i), nid = ndig32(id);
+        uint64_t pre_lo, pre_hi;
+        doc_prefix(id, nid, pre_lo, pre_hi);
         uint64_t base = a.doc_text[i];
         for (uint64_t r0 = p0; r0 < p1; r0 += 64) {
             const uint64_t p = r0 + lane;
             const bool v = p < p1;
-            uint64_t q = 0;
-            uint32_t len = 0, t = 0;
+            Score sc{0ull, 0u, 1u};
+            uint32_t len = 0, wl = 0;
             uint4 k = make_uint4(0u, 0u, 0u, 0u);
-            if (v) { t = a.term[p]; len = line_len(a, nid, p, q); k = a.tkey[t]; }
-            const uint32_t wl = v ? a.tlen[t] : 0u;
+            if (v) {
+                const uint32_t t = a.term[p];
+                k = a.tkey[t];
+                wl = a.tlen[t];
+                sc = score_of(a, p);
+                len = line_len(nid, wl, sc.ni);
+            }
             const uint32_t incl = wave_incl_scan(len);
             const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
             const bool has_long = __ballot(v && k.w == 0xFFFFFFFFu) != 0ull;
             if (!has_long && tot <= STG) {
                 const uint32_t ph = (uint32_t)(base & 15u);          /* global 16-byte phase */
-                if (v) put_line(sg + ph + (incl - len), id, nid, k, wl, q);
+                if (v) put_line(sg + ph + (incl - len), pre_lo, pre_hi, nid, k, wl, sc);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -208,19 +269,17 @@ __global__ __launch_bounds__(NT) void k_doc_text_write(EmitArgs a) {
             } else if (v) {
                 uint8_t* o = a.text + base + (incl - len);
                 if (k.w == 0xFFFFFFFFu) { /* long term (a short key always holds its TAB): corpus bytes */
-                    o[0] = 'd'; o[1] = 'o'; o[2] = 'c';
-                    put_dec(o + 3, id, nid);
-                    o += 3 + nid;
-                    *o++ = '@';
+                    /* the prefix's zero tail lies inside the word (a long term has >= 16 bytes) */
+                    st16(o, pre_lo, pre_hi);
+                    o += 4u + nid;
                     const uint8_t* src = a.corpus + ((((uint64_t)k.y << 32) | k.x) & 0xFFFFFFFFFFull);
                     for (uint32_t j = 0; j < wl; ++j) o[j] = src[j];
                     o += wl;
                     *o++ = '\t';
-                    put_score(o, q);
-                    o += score_len(q);
-                    *o = '\n';
+                    put_score(o, sc);
+                    o[sc.ni + 17u] = '\n';
                 } else {
-                    put_line(o, id, nid, k, wl, q);
+                    put_line(o, pre_lo, pre_hi, nid, k, wl, sc);
                 }
             }
             base += tot;
@@ -235,9 +294,11 @@ __global__ void k_format_f64(const double* __restrict__ v, uint64_t n, uint8_t* 
     if (i >= n) return;
     uint8_t* o = out + i * 32;
     for (int j = 0; j < 32; ++j) o[j] = 0;
-    uint64_t q;
-    if (!fixed16(v[i], q)) { atomicOr(status, ST_BOUNDS); return; }
-    put_score(o, q);
+    Score sc;
+    if (!fixed16(v[i], sc.q)) { atomicOr(status, ST_BOUNDS); return; }
+    sc.ip = (uint32_t)v[i];
+    sc.ni = ndig3(sc.ip);
+    put_score(o, sc);
 }
 
 }  // namespace

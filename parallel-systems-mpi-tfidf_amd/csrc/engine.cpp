@@ -351,7 +351,8 @@ int tfidf_comm_unique_id(uint8_t id[TFIDF_UNIQUE_ID_BYTES]) {
 }
 
 int tfidf_comm_init(tfidf_ctx* ctx, const uint8_t id[TFIDF_UNIQUE_ID_BYTES], int rank, int nranks) {
-    if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return TFIDF_E_INVAL;
+    /* ranks <= 1024: the DF exchange's per-owner counts live in LDS (k_owner_count) */
+    if (!ctx || !id || nranks < 1 || nranks > 1024 || rank < 0 || rank >= nranks) return TFIDF_E_INVAL;
     HIPCHK(hipSetDevice(ctx->device));
     tfidf_ctx_attach_xport(ctx, nullptr);
     ncclUniqueId u;

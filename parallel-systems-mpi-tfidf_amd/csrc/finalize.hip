@@ -23,6 +23,10 @@
  * its pointers reach loads as generic (flat) pointers, whose loads also count in lgkmcnt and
  * make every LDS wait wait for them too */
 #define G(p) ((GLOBAL_AS std::remove_pointer_t<decltype(p)>*)(p))
+/* streams the score stage reads or writes once (records in, the SoA output): non-temporal,
+ * so they do not push the per-rank idf table its gathers hit out of the caches */
+template <class T> __device__ __forceinline__ T ntl(const T* p) { return __builtin_nontemporal_load((const GLOBAL_AS T*)p); }
+template <class T> __device__ __forceinline__ void nts(T* p, T v) { __builtin_nontemporal_store(v, (GLOBAL_AS T*)p); }
 
 namespace {
 constexpr int NT = 256;
@@ -952,9 +956,9 @@ __global__ void k_idf_of_rank(const uint32_t* __restrict__ df_of_rank, const uin
  * df of a pair are per-document / per-term values the fetch expands on the host. */
 __device__ __forceinline__ void k5_emit(const K5Args& a, uint64_t o, double ds, uint32_t rank, uint32_t cnt) {
     const double tf = (double)cnt / ds;   /* TFIDF.c:202 */
-    G(a.out_term)[o] = rank;
-    G(a.out_cnt)[o] = cnt;
-    G(a.out_score)[o] = tf * G(a.idf_rank)[rank]; /* TFIDF.c:243-244 (idf from the host-libm LUT) */
+    nts(&a.out_term[o], (uint32_t)(rank));
+    nts(&a.out_cnt[o], (uint32_t)(cnt));
+    nts(&a.out_score[o], (double)(tf * G(a.idf_rank)[rank])); /* TFIDF.c:243-244 (idf from the host-libm LUT) */
 }
 
 /* records hold term ranks once the DF pass has run (k_df_hist_* rewrite them in place) */
@@ -1042,16 +1046,16 @@ __device__ __noinline__ void k5_radix(uint32_t rank_bits, const uint32_t* rec_cn
         }
 #pragma unroll
         for (int q = 0; q < K5_BATCH; ++q) {
-            cnt[q] = G(rec_cnt)[rb + (key[q] & ((1u << K5_IDX_BITS) - 1u))];
+            cnt[q] = ntl(&rec_cnt[rb + (key[q] & ((1u << K5_IDX_BITS) - 1u))]);
             idf[q] = G(idf_rank)[key[q] >> K5_IDX_BITS];
         }
 #pragma unroll
         for (int q = 0; q < K5_BATCH; ++q) {
             const uint32_t j = j0 + 64 * q + lane;
             if (j < n) {
-                G(out_term)[ob + j] = key[q] >> K5_IDX_BITS;
-                G(out_cnt)[ob + j] = cnt[q];
-                G(out_score)[ob + j] = ((double)cnt[q] / ds) * idf[q]; /* TFIDF.c:202,243-244 */
+                nts(&out_term[ob + j], (uint32_t)(key[q] >> K5_IDX_BITS));
+                nts(&out_cnt[ob + j], (uint32_t)(cnt[q]));
+                nts(&out_score[ob + j], (double)(((double)cnt[q] / ds) * idf[q])); /* TFIDF.c:202,243-244 */
             }
         }
     }
@@ -1077,8 +1081,8 @@ __device__ __forceinline__ void k5_prefetch(const K5Args& a, const uint4& m, uin
     for (int q = 0; q < K5_PF; ++q) {
         const uint32_t j = 64u * q + lane;
         const bool v = ok && j < n;
-        s[q] = v ? G(a.rec_slot)[rb + j] : 0u;
-        c[q] = v ? G(a.rec_cnt)[rb + j] : 0u;
+        s[q] = v ? ntl(&a.rec_slot[rb + j]) : 0u;
+        c[q] = v ? ntl(&a.rec_cnt[rb + j]) : 0u;
     }
 }
 
@@ -1134,8 +1138,8 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
 #pragma unroll
             for (int q = K5_PF; q < K5_RQ; ++q) {
                 const uint32_t j = 64u * q + lane;
-                sx[q - K5_PF] = j < n ? G(a.rec_slot)[rb + j] : 0u;
-                if (j < n) buf0[j] = G(a.rec_cnt)[rb + j];
+                sx[q - K5_PF] = j < n ? ntl(&a.rec_slot[rb + j]) : 0u;
+                if (j < n) buf0[j] = ntl(&a.rec_cnt[rb + j]);
             }
 #pragma unroll
             for (int q = K5_PF; q < K5_RQ; ++q) {
@@ -1209,9 +1213,9 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
                 if (j < n) {
                     const uint64_t o = ob + pos[q];
                     const uint32_t cnt = buf0[j];
-                    G(a.out_term)[o] = r[q];
-                    G(a.out_cnt)[o] = cnt;
-                    G(a.out_score)[o] = ((double)cnt / ds) * idf[q];   /* TFIDF.c:202,243-244 */
+                    nts(&a.out_term[o], (uint32_t)(r[q]));
+                    nts(&a.out_cnt[o], (uint32_t)(cnt));
+                    nts(&a.out_score[o], (double)(((double)cnt / ds) * idf[q]));   /* TFIDF.c:202,243-244 */
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1302,9 +1306,9 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
                 for (int e = 0; e < EB; ++e) {
                     if (64u * (q0 + e) + lane < n) {
                         const uint64_t o = ob + pos[e];
-                        G(a.out_term)[o] = r[q0 + e];
-                        G(a.out_cnt)[o] = cnt[e];
-                        G(a.out_score)[o] = ((double)cnt[e] / ds) * idf[e];   /* TFIDF.c:202,243-244 */
+                        nts(&a.out_term[o], (uint32_t)(r[q0 + e]));
+                        nts(&a.out_cnt[o], (uint32_t)(cnt[e]));
+                        nts(&a.out_score[o], (double)(((double)cnt[e] / ds) * idf[e]));   /* TFIDF.c:202,243-244 */
                     }
                 }
             }
@@ -1374,9 +1378,9 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
             for (int q = 0; q < EB; ++q) {
                 const uint32_t j = j0 + 64 * q + lane;
                 if (j < n) {
-                    G(a.out_term)[ob + j] = key[q] >> K5_IDX_BITS;
-                    G(a.out_cnt)[ob + j] = cnt[q];
-                    G(a.out_score)[ob + j] = ((double)cnt[q] / ds) * idf[q]; /* TFIDF.c:202,243-244 */
+                    nts(&a.out_term[ob + j], (uint32_t)(key[q] >> K5_IDX_BITS));
+                    nts(&a.out_cnt[ob + j], (uint32_t)(cnt[q]));
+                    nts(&a.out_score[ob + j], (double)(((double)cnt[q] / ds) * idf[q])); /* TFIDF.c:202,243-244 */
                 }
             }
         }
@@ -1442,8 +1446,8 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
 #pragma unroll
             for (int e = 0; e < K5L_EB; ++e) {
                 const uint32_t j = j0 + NT * e + tid;
-                rk[e] = j < n ? G(a.rec_slot)[rb + j] : 0u;
-                cn[e] = j < n ? G(a.rec_cnt)[rb + j] : 0u;
+                rk[e] = j < n ? ntl(&a.rec_slot[rb + j]) : 0u;
+                cn[e] = j < n ? ntl(&a.rec_cnt[rb + j]) : 0u;
             }
 #pragma unroll
             for (int e = 0; e < K5L_EB; ++e) {
@@ -1455,9 +1459,9 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
             for (int e = 0; e < K5L_EB; ++e) {
                 const uint32_t j = j0 + NT * e + tid;
                 if (j < n) {
-                    G(a.out_term)[ob + j] = rk[e];
-                    G(a.out_cnt)[ob + j] = cn[e];
-                    G(a.out_score)[ob + j] = ((double)cn[e] / ds) * f[e];   /* TFIDF.c:202,243-244 */
+                    nts(&a.out_term[ob + j], (uint32_t)(rk[e]));
+                    nts(&a.out_cnt[ob + j], (uint32_t)(cn[e]));
+                    nts(&a.out_score[ob + j], (double)(((double)cn[e] / ds) * f[e]));   /* TFIDF.c:202,243-244 */
                 }
             }
         }
@@ -1468,8 +1472,8 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
 #pragma unroll
         for (int e = 0; e < K5L_EB; ++e) {
             const uint32_t j = j0 + NT * e + tid;
-            sl[e] = j < n ? G(a.rec_slot)[rb + j] : 0u;
-            cn[e] = j < n ? G(a.rec_cnt)[rb + j] : 0u;
+            sl[e] = j < n ? ntl(&a.rec_slot[rb + j]) : 0u;
+            cn[e] = j < n ? ntl(&a.rec_cnt[rb + j]) : 0u;
         }
 #pragma unroll
         for (int e = 0; e < K5L_EB; ++e) {
@@ -1532,9 +1536,9 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
                 for (int e = 0; e < K5L_EB; ++e) {
                     if (p0 + NT * e + tid < n) {
                         const uint64_t o = ob + ps[e];
-                        G(a.out_term)[o] = kk[e];
-                        G(a.out_cnt)[o] = cn[e];
-                        G(a.out_score)[o] = ((double)cn[e] / ds) * f[e];   /* TFIDF.c:202,243-244 */
+                        nts(&a.out_term[o], (uint32_t)(kk[e]));
+                        nts(&a.out_cnt[o], (uint32_t)(cn[e]));
+                        nts(&a.out_score[o], (double)(((double)cn[e] / ds) * f[e]));   /* TFIDF.c:202,243-244 */
                     }
                 }
             }
@@ -1735,8 +1739,8 @@ __global__ __launch_bounds__(256, K5S_OCC) void k_score_small(K5Args a) {
         for (int q = 0; q < Q; ++q) {
             const uint32_t j = 64u * q + lane;
             const bool v = j < d.n;
-            r[q] = v ? G(a.rec_slot)[d.rb + j] : 0xFFFFFFFFu;
-            c[q] = v ? G(a.rec_cnt)[d.rb + j] : 0u;
+            r[q] = v ? ntl(&a.rec_slot[d.rb + j]) : 0xFFFFFFFFu;
+            c[q] = v ? ntl(&a.rec_cnt[d.rb + j]) : 0u;
         }
     };
     auto load_idf = [&](const K5SDoc& d, uint32_t (&r)[Q], double (&f)[Q]) {
@@ -1799,9 +1803,9 @@ __global__ __launch_bounds__(256, K5S_OCC) void k_score_small(K5Args a) {
         for (int q = 0; q < Q; ++q) {
             if (64u * q + lane < n) {
                 const uint64_t o = D0.ob + pos[q];
-                G(a.out_term)[o] = r0[q];
-                G(a.out_cnt)[o] = c0[q];
-                G(a.out_score)[o] = ((double)c0[q] / D0.ds) * f0[q];   /* TFIDF.c:202,243-244 */
+                nts(&a.out_term[o], (uint32_t)(r0[q]));
+                nts(&a.out_cnt[o], (uint32_t)(c0[q]));
+                nts(&a.out_score[o], (double)(((double)c0[q] / D0.ds) * f0[q]));   /* TFIDF.c:202,243-244 */
             }
         }
         D0 = D1;
@@ -1831,8 +1835,8 @@ __global__ __launch_bounds__(256) void k_emit_split(K5Args a) {
 #pragma unroll
             for (int e = 0; e < K5L_EB; ++e) {
                 const uint32_t j = j0 + 256u * e + threadIdx.x;
-                rk[e] = j < j1 ? G(a.rec_slot)[rb + j] : 0u;
-                cn[e] = j < j1 ? G(a.rec_cnt)[rb + j] : 0u;
+                rk[e] = j < j1 ? ntl(&a.rec_slot[rb + j]) : 0u;
+                cn[e] = j < j1 ? ntl(&a.rec_cnt[rb + j]) : 0u;
             }
 #pragma unroll
             for (int e = 0; e < K5L_EB; ++e) {
@@ -1844,9 +1848,9 @@ __global__ __launch_bounds__(256) void k_emit_split(K5Args a) {
             for (int e = 0; e < K5L_EB; ++e) {
                 const uint32_t j = j0 + 256u * e + threadIdx.x;
                 if (j < j1) {
-                    G(a.out_term)[ob + j] = rk[e];
-                    G(a.out_cnt)[ob + j] = cn[e];
-                    G(a.out_score)[ob + j] = ((double)cn[e] / ds) * f[e];   /* TFIDF.c:202,243-244 */
+                    nts(&a.out_term[ob + j], (uint32_t)(rk[e]));
+                    nts(&a.out_cnt[ob + j], (uint32_t)(cn[e]));
+                    nts(&a.out_score[ob + j], (double)(((double)cn[e] / ds) * f[e]));   /* TFIDF.c:202,243-244 */
                 }
             }
         }
@@ -2081,19 +2085,6 @@ int launch_owner_aggregate(const uint4* rkey, const uint32_t* rdf, uint64_t n, u
 int launch_owner_back(const uint32_t* back, const uint32_t* sidx, uint32_t V, uint32_t* df_global, hipStream_t s) {
     if (!V) return 0;
     k_owner_back<<<grid_for(V), NT, 0, s>>>(back, sidx, V, df_global);
-    return ok();
-}
-/* in-process transport's all-reduce: out[i] = sum of rows[r * n + i] over r */
-__global__ void k_sum_rows_u32(const uint32_t* __restrict__ rows, uint32_t nrows, uint64_t n, uint32_t* __restrict__ out) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    uint32_t s = 0;
-    for (uint32_t r = 0; r < nrows; ++r) s += rows[(uint64_t)r * n + i];
-    out[i] = s;
-}
-int launch_sum_rows_u32(const uint32_t* rows, uint32_t nrows, uint64_t n, uint32_t* out, hipStream_t s) {
-    if (!n) return 0;
-    k_sum_rows_u32<<<grid_for(n), NT, 0, s>>>(rows, nrows, n, out);
     return ok();
 }
 

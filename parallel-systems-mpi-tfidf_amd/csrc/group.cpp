@@ -99,9 +99,6 @@ struct RcclXport final : Xport {
     int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
         return enqueue([&](ncclComm_t c) { return ncclAllGather(send, recv, bytes, ncclUint8, c, s); });
     }
-    int allreduce_sum_u32(uint32_t* buf, size_t n, hipStream_t s) override {
-        return enqueue([&](ncclComm_t c) { return ncclAllReduce(buf, buf, n, ncclUint32, ncclSum, c, s); });
-    }
     int alltoallv(const void* send, const uint64_t* scnt, void* recv, const uint64_t* rcnt, size_t eb,
                   hipStream_t s) override {
         /* point-to-point pairs in one group: over xGMI every pair of GPUs has its own link */
@@ -169,11 +166,6 @@ struct Hub {
 struct LocalXport final : Xport {
     Hub* hub = nullptr;
     int device = 0;
-    uint32_t* tmp = nullptr;
-    size_t tmp_cap = 0;
-    ~LocalXport() override {
-        if (tmp) (void)hipFree(tmp);
-    }
     int words(const uint64_t mine[2], uint64_t* all, hipStream_t s) override {
         (void)s;
         hub->w[2 * rank] = mine[0];
@@ -200,21 +192,6 @@ struct LocalXport final : Xport {
         if (rc) { abort(); return rc; }
         /* every rank has copied every send buffer before any of them is reused */
         if (!hub->barrier()) return TFIDF_E_PEER;
-        return TFIDF_OK;
-    }
-    int allreduce_sum_u32(uint32_t* buf, size_t n, hipStream_t s) override {
-        if (!n) return hub->barrier() ? TFIDF_OK : TFIDF_E_PEER;
-        const size_t need = n * (size_t)nranks * 4;
-        if (need > tmp_cap) {
-            if (tmp) (void)hipFree(tmp);
-            tmp = nullptr;
-            tmp_cap = 0;
-            if (tfidf_dev_malloc((void**)&tmp, need) != hipSuccess) { abort(); return TFIDF_E_NOMEM; }
-            tmp_cap = need;
-        }
-        int rc = allgather(buf, tmp, n * 4, s);
-        if (rc) return rc;
-        if (launch_sum_rows_u32(tmp, (uint32_t)nranks, n, buf, s)) { abort(); return TFIDF_E_HIP; }
         return TFIDF_OK;
     }
     int alltoallv(const void* send, const uint64_t* scnt, void* recv, const uint64_t* rcnt, size_t eb,

@@ -5,7 +5,7 @@
  * (TFIDF.c:209-222,291-326) between OS processes.  Here a context (one GPU shard) talks
  * to its peers through an Xport:
  *
- *   RcclXport   ncclAllGather / ncclAllReduce / grouped ncclSend-ncclRecv over xGMI: one
+ *   RcclXport   ncclAllGather / grouped ncclSend-ncclRecv over xGMI: one
  *               communicator rank per GPU,
  *               either one process per GPU (tfidf_comm_init, torch.distributed launch) or
  *               one process driving every GPU (tfidf_group_open, ncclCommInitAll).
@@ -13,7 +13,7 @@
  *               device listed twice, e.g. K shards on the 1-GPU test box): the same
  *               operations as device-to-device copies between the contexts' buffers, with
  *               host barriers.  The engine code above the interface is identical, so the
- *               union / lookup / scatter / gather kernels and the status agreement run
+ *               owner partition / aggregate / reply kernels and the status agreement run
  *               unchanged with K > 1 ranks on one GPU.
  *
  * Every operation is collective: all ranks call it in the same order.  `words` is the
@@ -35,8 +35,6 @@ struct Xport {
     virtual int words(const uint64_t mine[2], uint64_t* all, hipStream_t s) = 0;
     /* device all-gather: recv[r * bytes ...] = rank r's send[0 .. bytes) */
     virtual int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
-    /* in-place device sum of n u32 over the ranks */
-    virtual int allreduce_sum_u32(uint32_t* buf, size_t n, hipStream_t s) = 0;
     /* device all-to-all with per-peer counts of `eb`-byte elements (host arrays of nranks):
      * this rank's elements for peer p are send[so[p] .. so[p] + scnt[p]) and peer p's for
      * this rank land at recv[ro[p] ..), so, ro the exclusive prefix sums of scnt, rcnt
@@ -58,6 +56,5 @@ hipError_t tfidf_dev_malloc(void** p, size_t bytes);
 
 /* group.cpp */
 Xport* make_rccl_xport(void* nccl_comm, int rank, int nranks, int device);   /* takes the comm */
-int launch_sum_rows_u32(const uint32_t* rows, uint32_t nrows, uint64_t n, uint32_t* out, hipStream_t s);
 
 #endif
