@@ -111,7 +111,6 @@ struct tfidf_ctx {
                                5 lean kernel (TFIDF_K1=lean), 6 windowed kernel (TFIDF_K1=win) —
                                cross-checks and A/B timing */
     bool stamps_on = false; /* env TFIDF_STAMPS=1 with the diagnostic library build */
-    uint32_t ablate = 0;    /* env TFIDF_K1_ABLATE: K1 timing experiments, pipeline stops after K1 */
     int xfail_rank = -1;    /* env TFIDF_TEST_XFAIL_RANK (tests): this rank fails inside the exchange of
                                its first run, right after the key all-gather (the abort path of
                                exchange_df) */
@@ -181,7 +180,7 @@ struct tfidf_ctx {
     const uint32_t* order = nullptr;
     /* last run */
     bool have_result = false;
-    bool have_info = false;   /* run counters/timings valid (also after an ablation run) */
+    bool have_info = false;   /* run counters/timings valid */
     uint64_t run_nbytes = 0;  /* corpus bytes of the last run (its bounds, read once by the run) */
     tfidf_corpus corpus{};
     const uint8_t* dev_bytes = nullptr;
@@ -268,12 +267,11 @@ int tfidf_open(int device, tfidf_ctx** out) {
 #endif
     const char* ks = getenv("TFIDF_STAMPS");
     ctx->stamps_on = ks && ks[0] == '1';
-    const char* ka = getenv("TFIDF_K1_ABLATE");
-    ctx->ablate = ka ? (uint32_t)strtoul(ka, nullptr, 0) : 0u;
     const char* kx = getenv("TFIDF_TEST_XFAIL_RANK");
     ctx->xfail_rank = kx ? atoi(kx) : -1;
-    /* diagnostics: initial vocabulary capacity (power of two) and the load it may reach
-     * before the run is repeated with a larger table (TFIDF_VLOAD percent, default 50) */
+    /* diagnostics: initial vocabulary capacity (power of two) and the loads it may reach
+     * before the run is repeated with a larger table (TFIDF_VLOAD percent below 16M slots,
+     * default 12; TFIDF_VLOAD_BIG from 16M slots on, default 45) */
     const char* kv = getenv("TFIDF_VCAP");
     if (kv) {
         uint64_t c = strtoull(kv, nullptr, 0);
@@ -513,9 +511,9 @@ static int exchange_df(tfidf_ctx* ctx, int local_rc, uint32_t V) {
 }
 
 /* The local stages of one attempt (this shard only, no collective): K0, K1, vocabulary,
- * merge, local DF.  Returns 0, 1 to retry with grown capacities, 2 for a timing ablation
- * run (nothing after K1 is valid), <0 on error.  Also checks that the main arena holds
- * what the stages after the exchange need, so that they never ask for a retry. */
+ * merge, local DF.  Returns 0, 1 to retry with grown capacities, <0 on error.  Also
+ * checks that the main arena holds what the stages after the exchange need, so that they
+ * never ask for a retry. */
 static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids, uint64_t Nt) {
     hipStream_t s = ctx->stream;
     Arena& ar = ctx->arena;
@@ -579,7 +577,6 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     o.chunk_shard = cnt + 16;
     o.status = (uint32_t*)(cnt + 3);
     o.stamps = nullptr;
-    o.ablate = ctx->ablate;
     ENSURE(ctx->hot_slot, (size_t)HOT_SLOTS * 4);
     o.hot_slot = ctx->hot_slot.as<uint32_t>();
     o.hot_ctr = (uint32_t*)(cnt + 9);   /* zeroed with the run's counters */
@@ -619,13 +616,6 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     else if (nchunks)
         LCHK(launch_tokcount(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
     mark(ctx, S_VOCAB);
-    if (ctx->ablate) { /* timing experiment: results are invalid, stop after K1 */
-        for (int st2 = S_MERGE; st2 <= S_NSTAGES; ++st2) mark(ctx, st2);
-        HIPCHK(hipStreamSynchronize(s));
-        ctx->V = 0;
-        ctx->npairs = 0;
-        return 2;
-    }
     /* the lean K1's hot-term marks leave the keys before anything else reads them */
 #ifdef TFIDF_K1_EXPERIMENTAL
     if (nchunks && ctx->k1_lean) LCHK(launch_hot_unmark(vd.keys, o.hot_slot, o.hot_ctr, s));
@@ -1006,7 +996,6 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
  * transport: decided by all ranks together), <0 on error. */
 static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids, uint64_t Nt) {
     int rc = run_local(ctx, c, dev_ids, Nt);
-    if (rc == 2) return 0;   /* timing ablation (single rank): stop after K1 */
     mark(ctx, S_EXCHANGE);
     if (ctx->xp) {
         rc = exchange_df(ctx, rc, ctx->run_V);
@@ -1060,9 +1049,6 @@ static int run_prepare(tfidf_ctx* ctx, const tfidf_corpus* in, CorpusDev& c, con
         HIPCHK(hipStreamSynchronize(s));
     }
     if (hi > in->nbytes || lo > hi) return TFIDF_E_INVAL;
-    /* timing ablations stop after K1, before the exchange: single-rank only (with a transport
-     * this error goes through the agreement, so every rank stops) */
-    if (ctx->ablate && ctx->xp) return TFIDF_E_INVAL;
     c.nbytes = in->nbytes;
     c.ndocs = N;
     c.lo = lo;
@@ -1106,8 +1092,7 @@ extern "C" int tfidf_run(tfidf_ctx* ctx, const tfidf_corpus* in) {
     ctx->dev_ids = dev_ids;
     ctx->ndocs = N;
     ctx->ndocs_total = Nt;
-    /* an ablation run (timing experiment) leaves no valid result: fetch/format refuse it */
-    ctx->have_result = ctx->ablate == 0;
+    ctx->have_result = true;
     ctx->have_info = true;
     if (ctx->timing) {
         for (int i = 0; i < S_NSTAGES; ++i) {

@@ -72,8 +72,6 @@ struct K1Out {
     unsigned long long* ntokens;
     unsigned long long* chunk_ctr;   /* K1 dynamic chunk schedule (zeroed per run) */
     unsigned long long* chunk_shard; /* tokcount_st: 8 sharded chunk counters (zeroed per run) */
-    uint32_t ablate;             /* timing experiments only (env TFIDF_K1_ABLATE; results invalid):
-                                    1 no vocabulary lookup, 2 no LDS counting, 4 no token walk */
     unsigned long long* stamps;  /* diagnostic build only: K1_NSTAMP phase cycle sums, WG count,
                                     then K1_NCOUNT event counters */
     uint32_t* hot_slot;          /* k_tokcount_lean: vocabulary slot of hot term id (HOT_MAX) */

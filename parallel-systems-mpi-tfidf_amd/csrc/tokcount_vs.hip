@@ -37,13 +37,6 @@
 #include "dev_vocab.h"
 #include "kernels.h"
 
-/* timing-only ablation builds (make abl): 1 no vocabulary load, 2 no LDS counting,
- * 4 no token rounds, 8 no token-list writes, 16 no docSize adds, 32 no corpus loads,
- * 64 no claim accounting, 128 first LDS probe only */
-#ifndef K1_ABL
-#define K1_ABL 0
-#endif
-
 namespace {
 
 #ifndef K1_NT
@@ -291,9 +284,7 @@ __device__ void vs_flush(VsShared& S, const K1Out& o, uint32_t gd0, uint32_t ng,
     if ((uint32_t)tid < ng) S.doff[tid] = off;
     const uint32_t nrec = tot & 0xFFFFu, npart = tot >> 16, ntot = nrec + npart;
     /* the two allocations in different waves, so their L2 round trips overlap */
-    if (K1_ABL & 256) { /* timing only: no allocation round trip (records overwrite each other) */
-        if (tid == 0) { S.rec_base = (blockIdx.x * 4096ull) % (o.rec_cap > 8192 ? o.rec_cap - 8192 : 1); S.part_base = 0; }
-    } else if (tid == 0) {
+    if (tid == 0) {
         const unsigned long long rb = nrec ? atomicAdd(o.rec_alloc, (unsigned long long)nrec) : 0ull;
         if (rb + nrec > o.rec_cap) atomicOr(o.status, ST_REC_FULL);
         S.rec_base = rb;
@@ -399,7 +390,7 @@ __global__ __launch_bounds__(NT, K1_WAVES_PER_SIMD) void k_tokcount_vs(CorpusDev
         }
         STAMP(st, 7);
         /* docSize: one LDS add per wave when the round's tokens share a document */
-        if (!(K1_ABL & 16)) {
+        {
             const uint64_t vm = __ballot(r.kind != 0u);
             if (vm) {
                 const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.rel);
@@ -411,7 +402,6 @@ __global__ __launch_bounds__(NT, K1_WAVES_PER_SIMD) void k_tokcount_vs(CorpusDev
             }
         }
         STAMP(st, 8);
-        if (K1_ABL & 2) return;
         /* invalid slot: status flagged, the run is retried */
         const uint64_t key = slot == INVALID_SLOT ? ~0ull : (((uint64_t)r.rel << SLOT_BITS) | slot);
         const uint32_t hl = tbl_hash(key) & (TB - 1);
@@ -430,16 +420,11 @@ __global__ __launch_bounds__(NT, K1_WAVES_PER_SIMD) void k_tokcount_vs(CorpusDev
         const bool claimed = valid && old == 0ull && !over;
         if (hit) atomicAdd(&S.T[hl], 1ull);
         uint32_t claims = claimed ? 1u : 0u;
-#if !(K1_ABL & 128)
         const bool rest = valid && !hit && !claimed;
         if (__ballot(rest) != 0ull) {
             if (rest) claims = tbl_count(S, o, key, hl, old, nx, over, gd0_cur);
         }
-#else
-        (void)nx;
-#endif
         STAMP(st, 9);
-        if (K1_ABL & 64) return;
         /* claims -> overflow mode: one LDS add per wave and round */
         const uint32_t wc = (uint32_t)__popcll(__ballot(claims != 0u));
         if (wc && lane == 0) {
@@ -493,13 +478,8 @@ __global__ __launch_bounds__(NT, K1_WAVES_PER_SIMD) void k_tokcount_vs(CorpusDev
                     const uint4 cur = pf0, edge = pe0;
                     {
                         const uint64_t a1 = gpos + 1ull * NWAVE * WSTEP; /* harmless past ge */
-#if K1_ABL & 32
-                        pf0 = make_uint4(0x20616161u ^ (uint32_t)a1, 0x61612061u, 0x61206161u, 0x20616161u);
-                        pe0 = pf0;
-#else
                         pf0 = ld16c(c.bytes, last_blk, a1);
                         if (edge_lane) pe0 = ld16c(c.bytes, last_blk, a1 + eoff);
-#endif
                     }
                     STAMP(st, 11);
                     /* ---- classify (per lane, one 16-byte group) ---- */
@@ -556,9 +536,7 @@ __global__ __launch_bounds__(NT, K1_WAVES_PER_SIMD) void k_tokcount_vs(CorpusDev
                             while (sm) {
                                 const uint32_t i = __builtin_ctz(sm);
                                 sm &= sm - 1;
-#if !(K1_ABL & 8)
                                 if (idx - base < (uint32_t)TLW) tl[idx - base] = (uint16_t)((lane << 4) | i);
-#endif
                                 ++idx;
                             }
                         }
@@ -570,7 +548,7 @@ __global__ __launch_bounds__(NT, K1_WAVES_PER_SIMD) void k_tokcount_vs(CorpusDev
                         /* ---- resolve + count, 64 tokens per round, all lanes busy; the
                          * vocabulary loads of round r+1 are issued before round r is
                          * counted (one round in flight, also across steps) ---- */
-                        for (uint32_t t0 = 0; t0 < cnt && !(K1_ABL & 4); t0 += 64) {
+                        for (uint32_t t0 = 0; t0 < cnt; t0 += 64) {
                             Round q;
                             {
                                 const uint32_t t = t0 + lane;
@@ -598,20 +576,10 @@ __global__ __launch_bounds__(NT, K1_WAVES_PER_SIMD) void k_tokcount_vs(CorpusDev
                                 for (uint32_t k = wr + 1; k < kend; ++k) rel += uni64(S.gdoc[k]) <= q.ap ? 1u : 0u;
                                 q.rel = rel;
                                 q.hv = q.kind == 1u ? (uint32_t)(key_hash(q.klo, q.khi) & v.mask) : 0u;
-#if K1_ABL & 1
-                                q.s4 = make_uint4((uint32_t)q.klo, (uint32_t)(q.klo >> 32), (uint32_t)q.khi, (uint32_t)(q.khi >> 32));
-                                q.t4 = q.s4;
-                                if (q.kind == 2u) q.kind = 1u;
-#else
                                 /* the home slot and the next one: a key displaced by one slot
                                  * (linear probing) still resolves without a dependent load */
                                 q.s4 = v.keys[q.hv];
-#ifdef K1_NO_T4
-                                q.t4 = make_uint4(0xEEEEEEEEu, 0xEEEEEEEEu, 0xEEEEEEEEu, 0xEEEEEEEEu);
-#else
                                 q.t4 = v.keys[(q.hv + 1) & (uint32_t)v.mask];
-#endif
-#endif
                             }
                             STAMP(st, 6);
                             if (pending) claims_finish(pend);
