@@ -175,8 +175,7 @@ __device__ __forceinline__ Score score_of(const EmitArgs& a, uint64_t p) {
 }
 /* its integer digits only (the length pass): floor(x) without the exact product, which
  * only the range check at the top of the range needs */
-__device__ __forceinline__ uint32_t score_ni(const EmitArgs& a, uint64_t p) {
-    const double x = a.score[p];
+__device__ __forceinline__ uint32_t score_ni(const EmitArgs& a, double x) {
     if (!((uint64_t)__double_as_longlong(x) >> 63) && x < 512.0) return ndig3((uint32_t)x);
     uint64_t q;
     if (!fixed16(x, q)) { atomicOr(a.status, ST_BOUNDS); return 1u; }
@@ -193,7 +192,20 @@ __global__ __launch_bounds__(NT) void k_doc_text_bytes(EmitArgs a) {
         const uint64_t p0 = a.out_off[i], p1 = a.out_off[i + 1];
         const uint32_t nid = ndig32(doc_id_of(a, i));
         uint64_t sum = 0;
-        for (uint64_t p = p0 + lane; p < p1; p += 64) sum += line_len(nid, a.tlen[a.term[p]], score_ni(a, p));
+        /* four lines per lane in flight: the term -> length gathers wait on the term loads */
+        for (uint64_t p = p0 + lane; p < p1; p += 4 * 64) {
+            uint32_t t[4];
+            double x[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint64_t q = p + 64u * k;
+                t[k] = q < p1 ? a.term[q] : 0u;
+                x[k] = q < p1 ? a.score[q] : 0.0;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (p + 64u * k < p1) sum += line_len(nid, a.tlen[t[k]], score_ni(a, x[k]));
+        }
         /* wave sum of 64-bit values: two 32-bit halves (a document's text < 2^32 * 64) */
         const uint32_t lo = wave_sum((uint32_t)sum & 0xFFFFFFu), hi = wave_sum((uint32_t)(sum >> 24));
         if (lane == 0) a.doc_bytes[i] = (uint64_t)lo + ((uint64_t)hi << 24);
@@ -214,10 +226,19 @@ __device__ __forceinline__ void put_line(uint8_t* o, uint64_t pre_lo, uint64_t p
     o[sc.ni + 17u] = '\n';
 }
 
-/* One wave per document.  A round of 64 lines is assembled in the wave's LDS stage at
- * the text's 16-byte phase, then copied out with 16-byte stores (whole chunks) and byte
- * stores (the round's first and last partial chunk); rounds holding a long term (bytes in
- * the corpus, up to any length) or more than STG bytes write their lines directly. */
+/* text[at + j] = stage[j] for j in [lo, hi) of one 16-byte chunk (hi <= 16): one byte per
+ * lane — the chunks a document shares with its neighbours */
+__device__ __forceinline__ void put_part(uint8_t* gb, const uint8_t* sg, uint32_t lo, uint32_t hi, uint32_t lane) {
+    if (lane >= lo && lane < hi) gb[lane] = sg[lane];
+}
+
+/* One wave per document.  A round of 64 lines is assembled in the wave's LDS stage behind
+ * the bytes the previous round left (fewer than 16: the stage starts at a 16-byte boundary
+ * of the text), its whole 16-byte chunks go out with 16-byte stores and the partial last
+ * chunk moves to the front of the stage for the next round.  Byte stores only where the
+ * document's text shares a chunk with its neighbours (its first and last chunk).  Rounds
+ * holding a long term (bytes in the corpus, up to any length) or more than the stage
+ * write their lines directly. */
 constexpr uint32_t STG = 4096;
 __global__ __launch_bounds__(NT) void k_doc_text_write(EmitArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[NT / 64][STG + 16];
@@ -229,7 +250,10 @@ __global__ __launch_bounds__(NT) void k_doc_text_write(EmitArgs a) {
         const uint32_t id = doc_id_of(a, i), nid = ndig32(id);
         uint64_t pre_lo, pre_hi;
         doc_prefix(id, nid, pre_lo, pre_hi);
-        uint64_t base = a.doc_text[i];
+        /* stage byte j <-> text[g0 + j]; stage [lo0, fill) holds text not yet written, the
+         * bytes before lo0 belong to the previous document (or were written directly) */
+        uint64_t g0 = a.doc_text[i] & ~15ull;
+        uint32_t fill = (uint32_t)(a.doc_text[i] & 15u), lo0 = fill;
         for (uint64_t r0 = p0; r0 < p1; r0 += 64) {
             const uint64_t p = r0 + lane;
             const bool v = p < p1;
@@ -246,44 +270,58 @@ __global__ __launch_bounds__(NT) void k_doc_text_write(EmitArgs a) {
             const uint32_t incl = wave_incl_scan(len);
             const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
             const bool has_long = __ballot(v && k.w == 0xFFFFFFFFu) != 0ull;
-            if (!has_long && tot <= STG) {
-                const uint32_t ph = (uint32_t)(base & 15u);          /* global 16-byte phase */
-                if (v) put_line(sg + ph + (incl - len), pre_lo, pre_hi, nid, k, wl, sc);
+            if (!has_long && tot <= STG - fill) {
+                if (v) put_line(sg + fill + (incl - len), pre_lo, pre_hi, nid, k, wl, sc);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                /* stage[c*16 .. c*16+16) <-> text[base - ph + c*16 ..) */
-                uint8_t* gb = a.text + (base - ph);
-                const uint32_t end = ph + tot, nch = (end + 15u) >> 4;
-                for (uint32_t c = lane; c < nch; c += 64) {
-                    const uint32_t lo = c * 16u, hi = lo + 16u;
-                    if (lo >= ph && hi <= end) {
-                        *reinterpret_cast<uint4*>(gb + lo) = *reinterpret_cast<const uint4*>(sg + lo);
+                uint8_t* gb = a.text + g0;
+                const uint32_t end = fill + tot, nfull = end >> 4;
+                for (uint32_t c = lane; c < nfull; c += 64)
+                    if (c != 0u || lo0 == 0u)
+                        *reinterpret_cast<uint4*>(gb + 16u * c) = *reinterpret_cast<const uint4*>(sg + 16u * c);
+                if (nfull) {
+                    if (lo0) put_part(gb, sg, lo0, 16u, lane);
+                    lo0 = 0;
+                    /* the partial last chunk to the front (this wave's LDS accesses are in order) */
+                    if (lane == 0)
+                        *reinterpret_cast<uint4*>(sg) = *reinterpret_cast<const uint4*>(sg + 16u * nfull);
+                    g0 += 16u * nfull;
+                }
+                fill = end & (nfull ? 15u : ~0u);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            } else {
+                if (fill > lo0) put_part(a.text + g0, sg, lo0, fill, lane);
+                if (v) {
+                    uint8_t* o = a.text + g0 + fill + (incl - len);
+                    if (k.w == 0xFFFFFFFFu) { /* long term (a short key always holds its TAB): corpus bytes */
+                        /* the prefix's zero tail lies inside the word (a long term has >= 16 bytes) */
+                        st16(o, pre_lo, pre_hi);
+                        o += 4u + nid;
+                        const uint8_t* src = a.corpus + ((((uint64_t)k.y << 32) | k.x) & 0xFFFFFFFFFFull);
+                        for (uint32_t j = 0; j < wl; ++j) o[j] = src[j];
+                        o += wl;
+                        *o++ = '\t';
+                        put_score(o, sc);
+                        o[sc.ni + 17u] = '\n';
                     } else {
-                        for (uint32_t b = lo > ph ? lo : ph; b < (hi < end ? hi : end); ++b) gb[b] = sg[b];
+                        put_line(o, pre_lo, pre_hi, nid, k, wl, sc);
                     }
                 }
+                const uint64_t nb = g0 + fill + tot;
+                g0 = nb & ~15ull;
+                fill = lo0 = (uint32_t)(nb & 15u);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            } else if (v) {
-                uint8_t* o = a.text + base + (incl - len);
-                if (k.w == 0xFFFFFFFFu) { /* long term (a short key always holds its TAB): corpus bytes */
-                    /* the prefix's zero tail lies inside the word (a long term has >= 16 bytes) */
-                    st16(o, pre_lo, pre_hi);
-                    o += 4u + nid;
-                    const uint8_t* src = a.corpus + ((((uint64_t)k.y << 32) | k.x) & 0xFFFFFFFFFFull);
-                    for (uint32_t j = 0; j < wl; ++j) o[j] = src[j];
-                    o += wl;
-                    *o++ = '\t';
-                    put_score(o, sc);
-                    o[sc.ni + 17u] = '\n';
-                } else {
-                    put_line(o, pre_lo, pre_hi, nid, k, wl, sc);
-                }
             }
-            base += tot;
         }
+        if (fill > lo0) put_part(a.text + g0, sg, lo0, fill, lane);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 

@@ -23,11 +23,9 @@
  * its pointers reach loads as generic (flat) pointers, whose loads also count in lgkmcnt and
  * make every LDS wait wait for them too */
 #define G(p) ((GLOBAL_AS std::remove_pointer_t<decltype(p)>*)(p))
-/* the records the score stage reads once: non-temporal loads, so they do not push the
- * per-rank idf table its gathers hit out of the caches */
-template <class T> __device__ __forceinline__ T ntl(const T* p) { return __builtin_nontemporal_load((const GLOBAL_AS T*)p); }
-/* K5's outputs: plain stores (non-temporal ones measured slower on c4, 3.50 vs 3.05 ms:
- * documents of few pairs leave partial lines) */
+/* K5's outputs: plain stores.  Non-temporal ones measured c2's score stage 0.753 -> 0.727
+ * ms but c4's 3.05 -> 4.1 ms, non-temporal record loads no change on either
+ * (profiles/r03_nt_emit_ab.txt) */
 template <class T> __device__ __forceinline__ void sto(T* p, T v) { *(GLOBAL_AS T*)p = v; }
 
 namespace {
@@ -1048,7 +1046,7 @@ __device__ __noinline__ void k5_radix(uint32_t rank_bits, const uint32_t* rec_cn
         }
 #pragma unroll
         for (int q = 0; q < K5_BATCH; ++q) {
-            cnt[q] = ntl(&rec_cnt[rb + (key[q] & ((1u << K5_IDX_BITS) - 1u))]);
+            cnt[q] = rec_cnt[rb + (key[q] & ((1u << K5_IDX_BITS) - 1u))];
             idf[q] = G(idf_rank)[key[q] >> K5_IDX_BITS];
         }
 #pragma unroll
@@ -1083,8 +1081,8 @@ __device__ __forceinline__ void k5_prefetch(const K5Args& a, const uint4& m, uin
     for (int q = 0; q < K5_PF; ++q) {
         const uint32_t j = 64u * q + lane;
         const bool v = ok && j < n;
-        s[q] = v ? ntl(&a.rec_slot[rb + j]) : 0u;
-        c[q] = v ? ntl(&a.rec_cnt[rb + j]) : 0u;
+        s[q] = v ? a.rec_slot[rb + j] : 0u;
+        c[q] = v ? a.rec_cnt[rb + j] : 0u;
     }
 }
 
@@ -1140,8 +1138,8 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
 #pragma unroll
             for (int q = K5_PF; q < K5_RQ; ++q) {
                 const uint32_t j = 64u * q + lane;
-                sx[q - K5_PF] = j < n ? ntl(&a.rec_slot[rb + j]) : 0u;
-                if (j < n) buf0[j] = ntl(&a.rec_cnt[rb + j]);
+                sx[q - K5_PF] = j < n ? a.rec_slot[rb + j] : 0u;
+                if (j < n) buf0[j] = a.rec_cnt[rb + j];
             }
 #pragma unroll
             for (int q = K5_PF; q < K5_RQ; ++q) {
@@ -1448,8 +1446,8 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
 #pragma unroll
             for (int e = 0; e < K5L_EB; ++e) {
                 const uint32_t j = j0 + NT * e + tid;
-                rk[e] = j < n ? ntl(&a.rec_slot[rb + j]) : 0u;
-                cn[e] = j < n ? ntl(&a.rec_cnt[rb + j]) : 0u;
+                rk[e] = j < n ? a.rec_slot[rb + j] : 0u;
+                cn[e] = j < n ? a.rec_cnt[rb + j] : 0u;
             }
 #pragma unroll
             for (int e = 0; e < K5L_EB; ++e) {
@@ -1474,8 +1472,8 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
 #pragma unroll
         for (int e = 0; e < K5L_EB; ++e) {
             const uint32_t j = j0 + NT * e + tid;
-            sl[e] = j < n ? ntl(&a.rec_slot[rb + j]) : 0u;
-            cn[e] = j < n ? ntl(&a.rec_cnt[rb + j]) : 0u;
+            sl[e] = j < n ? a.rec_slot[rb + j] : 0u;
+            cn[e] = j < n ? a.rec_cnt[rb + j] : 0u;
         }
 #pragma unroll
         for (int e = 0; e < K5L_EB; ++e) {
@@ -1741,8 +1739,8 @@ __global__ __launch_bounds__(256, K5S_OCC) void k_score_small(K5Args a) {
         for (int q = 0; q < Q; ++q) {
             const uint32_t j = 64u * q + lane;
             const bool v = j < d.n;
-            r[q] = v ? ntl(&a.rec_slot[d.rb + j]) : 0xFFFFFFFFu;
-            c[q] = v ? ntl(&a.rec_cnt[d.rb + j]) : 0u;
+            r[q] = v ? a.rec_slot[d.rb + j] : 0xFFFFFFFFu;
+            c[q] = v ? a.rec_cnt[d.rb + j] : 0u;
         }
     };
     auto load_idf = [&](const K5SDoc& d, uint32_t (&r)[Q], double (&f)[Q]) {
@@ -1837,8 +1835,8 @@ __global__ __launch_bounds__(256) void k_emit_split(K5Args a) {
 #pragma unroll
             for (int e = 0; e < K5L_EB; ++e) {
                 const uint32_t j = j0 + 256u * e + threadIdx.x;
-                rk[e] = j < j1 ? ntl(&a.rec_slot[rb + j]) : 0u;
-                cn[e] = j < j1 ? ntl(&a.rec_cnt[rb + j]) : 0u;
+                rk[e] = j < j1 ? a.rec_slot[rb + j] : 0u;
+                cn[e] = j < j1 ? a.rec_cnt[rb + j] : 0u;
             }
 #pragma unroll
             for (int e = 0; e < K5L_EB; ++e) {
