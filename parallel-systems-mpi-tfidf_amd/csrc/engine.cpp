@@ -524,7 +524,19 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     mark(ctx, S_PREP);
     /* ---- buffers ---- */
     const uint64_t span = c.hi - c.lo;
-    const uint64_t nchunks = span ? (span + CHUNK_BYTES - 1) / CHUNK_BYTES : 0;
+    /* K1 variant: the slot-keyed kernels (tokcount_st / tokcount_vs) need a 16-byte aligned
+     * corpus base; TFIDF_K1=general selects the general kernel (cross-checks).  The LDS-staged
+     * kernel is the low-cardinality one: with a vocabulary table past K1_ST_MAX_CAP slots
+     * (config 4: ~1e7 terms, nearly every token a new (doc, term) pair) its bucketed LDS count
+     * table runs full and the round-1 kernel is 2.3x faster (c4: 11.5 vs 26.2 ms) */
+    const bool aligned = (((uintptr_t)c.bytes & 15u) == 0);
+    ctx->k1_vs = aligned && (ctx->k1_mode <= 1 || ctx->k1_mode >= 4);
+    if (ctx->k1_vs && ctx->vcap > K1_VS_MAX_CAP) return TFIDF_E_CAPACITY;
+    ctx->k1_win = ctx->k1_vs && ctx->k1_mode == 6 && ctx->vcap <= K1_WIN_MAX_CAP;
+    ctx->k1_lean = ctx->k1_vs && ctx->k1_mode == 5 && ctx->vcap <= K1_ST_MAX_CAP;
+    ctx->k1_st = ctx->k1_vs && (ctx->k1_mode == 0 || ctx->k1_mode == 4) && ctx->vcap <= K1_ST_MAX_CAP;
+    const uint32_t cb = ctx->k1_st ? CHUNK_BYTES_ST : CHUNK_BYTES;
+    const uint64_t nchunks = span ? (span + cb - 1) / cb : 0;
     if (ctx->rec_cap == 0) ctx->rec_cap = span / 6 + 4096;
     if (ctx->part_cap == 0) ctx->part_cap = span / 64 + 4096;
     ENSURE(ctx->chunk_start, (nchunks + 1) * 8);
@@ -548,13 +560,8 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     HIPCHK(hipMemsetAsync(ctx->doc_flags.p, 0, (size_t)N + 1, s));
     ENSURE(ctx->big_list, (size_t)BIG_LIST_CAP * 4);
     if (nchunks)
-        LCHK(launch_plan_chunks(c, nchunks, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(),
+        LCHK(launch_plan_chunks(c, nchunks, cb, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(),
                                 ctx->big_list.as<uint32_t>(), cnt + 6, s));
-    /* K1 variant: the slot-keyed kernel (tokcount_vs.hip) needs a 16-byte aligned corpus
-     * base; TFIDF_K1=general selects the general kernel (cross-checks) */
-    const bool aligned = (((uintptr_t)c.bytes & 15u) == 0);
-    ctx->k1_vs = aligned && (ctx->k1_mode <= 1 || ctx->k1_mode >= 4);
-    if (ctx->k1_vs && ctx->vcap > K1_VS_MAX_CAP) return TFIDF_E_CAPACITY;
     /* ---- K1 ---- */
     mark(ctx, S_TOKCOUNT);
     VocabDev vd{ctx->vkeys.as<uint4>(), ctx->vrep.as<uint64_t>(), ctx->vcap - 1};
@@ -585,13 +592,6 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
         HIPCHK(hipMemsetAsync(ctx->stamps.p, 0, 8 * K1_STAMP_WORDS, s));
         o.stamps = ctx->stamps.as<unsigned long long>();
     }
-    /* the LDS-staged kernel is the low-cardinality one: with a vocabulary table past
-     * K1_ST_MAX_CAP slots (config 4: ~1e7 terms, nearly every token a new (doc, term) pair)
-     * its bucketed LDS count table runs full and the round-1 kernel is 2.3x faster (c4:
-     * 11.5 vs 26.2 ms) */
-    ctx->k1_win = ctx->k1_vs && ctx->k1_mode == 6 && ctx->vcap <= K1_WIN_MAX_CAP;
-    ctx->k1_lean = ctx->k1_vs && ctx->k1_mode == 5 && ctx->vcap <= K1_ST_MAX_CAP;
-    ctx->k1_st = ctx->k1_vs && (ctx->k1_mode == 0 || ctx->k1_mode == 4) && ctx->vcap <= K1_ST_MAX_CAP;
 #ifdef TFIDF_K1_EXPERIMENTAL
     if (nchunks && (ctx->k1_lean || ctx->k1_win)) {
         LeanParams& lp = *ctx->lp_host;

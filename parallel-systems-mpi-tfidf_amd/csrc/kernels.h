@@ -11,7 +11,11 @@
 #define K1_NT        256                 /* threads per tokenize+count workgroup */
 #define K1_WIN       (K1_NT * 16)        /* bytes per window: one 16-byte group per thread */
 #ifndef CHUNK_BYTES
-#define CHUNK_BYTES  16384u              /* nominal chunk (work unit) size */
+#define CHUNK_BYTES  16384u              /* nominal chunk (work unit) size: tokcount_vs / general */
+#endif
+#ifndef CHUNK_BYTES_ST
+#define CHUNK_BYTES_ST 24576u            /* ... and tokcount_st's: its per-chunk set-up, flush and
+                                            barrier wait over 1.5x the bytes (c2 K1 -3 %, c5 -5 %) */
 #endif
 #ifndef DENSE_DOC
 #define DENSE_DOC    (4ull << 20)        /* documents longer than this: dense merge of their partial records */
@@ -82,8 +86,8 @@ struct K1Out {
 #define K1_STAMP_WORDS (K1_NSTAMP + 1 + K1_NCOUNT)
 
 /* K0: chunk boundaries; chunk_start has nchunks+1 entries, chunk_doc nchunks */
-int launch_plan_chunks(const CorpusDev& c, uint64_t nchunks, uint64_t* chunk_start, uint32_t* chunk_doc,
-                       uint32_t* big_list, unsigned long long* big_ctr, hipStream_t s);
+int launch_plan_chunks(const CorpusDev& c, uint64_t nchunks, uint32_t chunk_bytes, uint64_t* chunk_start,
+                       uint32_t* chunk_doc, uint32_t* big_list, unsigned long long* big_ctr, hipStream_t s);
 /* K1: tokenize + per-document term counts for chunks [c0, c1) */
 int launch_tokcount(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc,
                     uint64_t c0, uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s);

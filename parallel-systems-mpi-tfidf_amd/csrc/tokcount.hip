@@ -74,12 +74,12 @@ __device__ __forceinline__ uint4 load16_guarded(const uint8_t* __restrict__ byte
 /* Also lists the documents longer than DENSE_DOC (each registered once, by the first grid
  * point inside it): their partial records are summed in a dense per-document array by
  * the merge stage instead of being sorted (finalize.hip, k_part_dense). */
-__global__ void k_plan_chunks(CorpusDev c, uint64_t nchunks, uint64_t* __restrict__ chunk_start,
+__global__ void k_plan_chunks(CorpusDev c, uint64_t nchunks, uint32_t cb, uint64_t* __restrict__ chunk_start,
                               uint32_t* __restrict__ chunk_doc, uint32_t* __restrict__ big_list,
                               unsigned long long* __restrict__ big_ctr) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i > nchunks) return;
-    uint64_t b = c.lo + i * (uint64_t)CHUNK_BYTES;
+    uint64_t b = c.lo + i * (uint64_t)cb;
     if (i == nchunks || b >= c.hi) {
         chunk_start[i] = c.hi;
         chunk_doc[i] = c.ndocs ? c.ndocs - 1 : 0;
@@ -89,16 +89,17 @@ __global__ void k_plan_chunks(CorpusDev c, uint64_t nchunks, uint64_t* __restric
     uint64_t s0 = c.doc_off[d], s1 = c.doc_off[d + 1];
     chunk_start[i] = (s1 - s0 <= BIG_DOC) ? s0 : b;
     chunk_doc[i] = d;
-    if (big_list && s1 - s0 > DENSE_DOC && (i == 0 || b - CHUNK_BYTES < s0)) {
+    if (big_list && s1 - s0 > DENSE_DOC && (i == 0 || b - cb < s0)) {
         const unsigned long long k = atomicAdd(big_ctr, 1ull);
         if (k < BIG_LIST_CAP) big_list[k] = d;
     }
 }
 
-int launch_plan_chunks(const CorpusDev& c, uint64_t nchunks, uint64_t* chunk_start, uint32_t* chunk_doc,
-                       uint32_t* big_list, unsigned long long* big_ctr, hipStream_t s) {
+int launch_plan_chunks(const CorpusDev& c, uint64_t nchunks, uint32_t chunk_bytes, uint64_t* chunk_start,
+                       uint32_t* chunk_doc, uint32_t* big_list, unsigned long long* big_ctr, hipStream_t s) {
     uint64_t n = nchunks + 1;
-    k_plan_chunks<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(c, nchunks, chunk_start, chunk_doc, big_list, big_ctr);
+    k_plan_chunks<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(c, nchunks, chunk_bytes, chunk_start, chunk_doc, big_list,
+                                                              big_ctr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

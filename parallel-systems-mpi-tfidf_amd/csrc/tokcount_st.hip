@@ -4,7 +4,7 @@
  * tokenising (:141-147), the O(P) strcmp search/append of (word, doc) records (:151-167)
  * and the per-rank word table (:169-188).
  *
- * Work split (as tokcount_vs.hip): a persistent grid takes K0's chunks (~16 KiB of whole
+ * Work split (as tokcount_vs.hip): a persistent grid takes K0's chunks (~24 KiB of whole
  * documents, or a piece of a document longer than BIG_DOC) from a global counter; inside
  * a chunk the four waves of a workgroup run without block barriers, wave w taking the
  * 1 KiB steps w, w+4, ...; (document, term) pairs are counted in one LDS table per
@@ -138,10 +138,13 @@ __device__ __forceinline__ uint32_t compress4(uint32_t m) {   /* bits 7, 15, 23,
  * empty slot proves a key is not further on).  With 4-slot buckets a c2 chunk's ~1000
  * keys in 896 buckets leave the home bucket full for ~2.6 % of new keys, which sends about
  * half of all rounds through bkt_slow (0.2 ms of K1, measured in round 2 with slow keys
- * dropped); 8-slot buckets (two ds_read_b128, K1S_BW=8) make that rare but cost the same in compares
- * (c2 2.255 vs 2.222 ms, c5 2.441 vs 2.432 ms): 4-slot buckets stay. */
+ * dropped); 8-slot buckets (two ds_read_b128) make that rare but cost the same in compares
+ * at 16 KiB chunks (c2 2.255 vs 2.222 ms, c5 2.441 vs 2.432 ms).  With 24 KiB chunks
+ * (CHUNK_BYTES_ST: ~1.5x the keys per group) 8-slot buckets win: c2 K1 2.233 -> 2.161 ms,
+ * c5 2.434 -> 2.315 ms, and no more overflow records than 16 KiB chunks with 4-slot ones
+ * (4-slot buckets at 24 KiB: merge c2 0.10 -> 0.125 ms), profiles/r03_chunk_ab.txt. */
 #ifndef K1S_BW
-#define K1S_BW 4
+#define K1S_BW 8
 #endif
 constexpr uint32_t BW = K1S_BW;
 static_assert(BW == 4 || BW == 8, "bucket width");

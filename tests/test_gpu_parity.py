@@ -84,7 +84,8 @@ def test_long_tokens_and_shared_prefixes(engine):
 
 def test_tokens_across_windows_and_chunks(engine):
     # one big document (> BIG_DOC, split across chunks) whose tokens straddle the 4 KiB
-    # windows and 16 KiB chunk boundaries at every offset
+    # windows and chunk boundaries (24 KiB for tokcount_st, 16 KiB for the other K1
+    # kernels) at every offset
     rng = np.random.default_rng(3)
     parts = []
     n = 0
