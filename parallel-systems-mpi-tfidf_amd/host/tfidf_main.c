@@ -11,7 +11,7 @@
  * one per rank); --stats prints one JSON line of ingest / run / output times to stderr.
  *
  * Parallelism (the reference's `mpirun -np P`, TFIDF.c:82-92,125-130):
- *   --gpus N     GPUs to use (default: every visible GPU), one shard each;
+ *   --gpus N     GPUs to use (default 1; capped at the visible GPUs), one shard each;
  *   --shards K   shards (default: N), dealt to the GPUs round-robin — more shards than
  *                GPUs run through the in-process transport (tests on one GPU).
  * Shards are byte-balanced contiguous ranges of the "docN@" order (tfidf_plan_dir), never
