@@ -618,15 +618,15 @@ __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ r
                                                         const uint32_t* __restrict__ rank_of_slot,
                                                         const uint16_t* __restrict__ rank16, uint32_t V,
                                                         uint64_t slot_cap, uint64_t ranked_from,
-                                                        uint32_t* __restrict__ status,
+                                                        uint32_t* __restrict__ status, uint32_t per,
                                                         uint32_t* __restrict__ part /* [grid][V/2 words] */) {
     extern __shared__ __attribute__((aligned(16))) uint32_t bins[]; /* V/2 words of two u16 counters */
     const uint32_t W = (V + 1) / 2;
     for (uint32_t k = threadIdx.x; k < W; k += DFH_NT) bins[k] = 0;
     __syncthreads();
     if (nrec_extra) nrec += *nrec_extra; /* merged partial records, counted on the device */
-    const uint64_t r0 = (uint64_t)blockIdx.x * DFH_RECS;
-    const uint64_t r1 = r0 + DFH_RECS < nrec ? r0 + DFH_RECS : nrec;
+    const uint64_t r0 = (uint64_t)blockIdx.x * per;
+    const uint64_t r1 = r0 + per < nrec ? r0 + per : nrec;
     for (uint64_t i = r0 + threadIdx.x; i < r1; i += (uint64_t)DFH_B * DFH_NT) {
         uint32_t sl[DFH_B], r[DFH_B];
 #pragma unroll
@@ -812,12 +812,27 @@ int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra
     if (V <= DFH_MAXV) {
         uint32_t nparts = (uint32_t)((nrec_max + DFH_RECS - 1) / DFH_RECS);
         uint32_t W = (V + 1) / 2;
+        /* records per workgroup (<= DFH_RECS): the workgroups fill whole waves of the CUs'
+         * resident slots (c2: 946 x 65535 records = 3.7 waves -> 1024 x 60548, no tail) */
+        static int ncu = 0;
+        if (!ncu) {
+            int dev = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+                ncu = 256;
+        }
+        const uint64_t per_cu = (uint64_t)163840 / ((uint64_t)W * 4) >= 2 ? 2 : 1;   /* 1024-thread workgroups */
+        const uint64_t slots = (uint64_t)ncu * per_cu;
+        const uint64_t full = (nparts + slots - 1) / slots * slots;
+        uint32_t per = (uint32_t)((nrec_max + full - 1) / full);
+        if (per < 8192u) per = 8192u;   /* small inputs: few workgroups (each clears and writes W words) */
+        nparts = (uint32_t)((nrec_max + per - 1) / per);
         size_t m = ar.mark();
         uint32_t* part = (uint32_t*)ar.get((size_t)nparts * W * 4);
         if (!part) return -2;
         if (hipMemsetAsync(df, 0, (size_t)V * 4, s) != hipSuccess) return -1;
         k_df_hist_lds<<<nparts, DFH_NT, (size_t)W * 4, s>>>(rec_slot, nrec, nrec_extra, rank_of_slot, rank16, V, slot_cap,
-                                                             ranked_from, status, part);
+                                                             ranked_from, status, per, part);
         k_df_colsum<<<dim3(grid_for(V), (nparts + DFC_G - 1) / DFC_G), NT, 0, s>>>(part, nparts, V, df);
         ar.release(m);
         return ok();
