@@ -8,8 +8,8 @@ batch: the config-2 corpus (1e5 synthetic Zipfian documents, V = 5e4, ~1 GB) res
 HBM.  Multi-GPU is weak scaling: every rank owns one config-2-sized shard of a corpus of
 N x 1e5 documents (contiguous "docN" strcmp ranges; idf uses the global N).
 
-    python bench.py [--gpus N --steps K --warmup W]
-    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+    python bench.py [--gpus N --steps K --warmup W]      (N > 1: one process, N GPUs, tfidf_group)
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...   (one process per GPU)
 
 Rank 0 prints one JSON line.  `roofline` is priced on the dominant kernel (K1
 tokenize+count), algorithmic bytes per launch = C + 12*P, divided by K1's
@@ -46,16 +46,11 @@ def hip_device_sync():
         raise RuntimeError("hipDeviceSynchronize failed")
 
 
-K1_SOURCES = {"k_tokcount_st": "tokcount_st.hip", "k_tokcount_win": "tokcount_win.hip",
-              "k_tokcount_lean": "tokcount_lean.hip", "k_tokcount_vs": "tokcount_vs.hip", "k_tokcount": "tokcount.hip"}
+K1_SOURCES = {"k_tokcount_st": "tokcount_st.hip", "k_tokcount_vs": "tokcount_vs.hip", "k_tokcount": "tokcount.hip"}
 
 
 def k1_kernel(flags: int) -> str:
     """The tokenize+count kernel the last run used (tfidf_run_info.flags)."""
-    if flags & tfidf_abi.RUN_K1_WIN:
-        return "k_tokcount_win"
-    if flags & tfidf_abi.RUN_K1_LEAN:
-        return "k_tokcount_lean"
     if flags & tfidf_abi.RUN_K1_ST:
         return "k_tokcount_st"
     return "k_tokcount_vs" if flags & tfidf_abi.RUN_K1_VS else "k_tokcount"
@@ -220,6 +215,104 @@ def main_shards(args):
     g.close()
 
 
+def main_group(args):
+    """`--gpus N` without a launcher: ONE process drives N GPUs through tfidf_group (rank r
+    on device r, one host thread per rank, the RCCL clique of ncclCommInitAll over xGMI;
+    group.cpp).  The same engine path as one process per GPU under torch.distributed.run;
+    exits non-zero when fewer than N GPUs are visible instead of measuring fewer."""
+    N = args.gpus
+    have = tfidf_abi.device_count()
+    if have < N:
+        print(f"bench.py: --gpus {N} needs {N} visible GPUs, found {have}", file=sys.stderr)
+        sys.exit(2)
+    g = tfidf_abi.Group(N, devices=list(range(N)))
+    plans, corpora = [], []
+    for r in range(N):
+        p = tfidf_configs.plan(args.config, scale=args.scale, rank=r, nranks=N, weak=not args.strong,
+                               vocab=args.vocab)
+        plans.append(p)
+        corpora.append(g.ranks[r].synth_device(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"],
+                                               p["ndocs_total"]))
+        g.ranks[r].set_timing(True)
+    hip_device_sync_all(N)
+    a0 = g.ranks[0].alloc_counters()
+    tc = time.perf_counter()
+    g.run(corpora)
+    hip_device_sync_all(N)
+    cold_ms = (time.perf_counter() - tc) * 1e3
+    for _ in range(max(0, args.warmup - 1)):
+        g.run(corpora)
+    hip_device_sync_all(N)
+    a1 = g.ranks[0].alloc_counters()
+    steps = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        g.run(corpora)   # returns when every rank's run is done (one host thread per rank, joined)
+        steps.append([e.info() for e in g.ranks])
+    hip_device_sync_all(N)
+    elapsed = time.perf_counter() - t0
+    a2 = g.ranks[0].alloc_counters()
+    infos = steps[-1]
+    C_all = float(sum(i["nbytes"] for i in infos))
+    P_all = float(sum(i["npairs"] for i in infos))
+    T_all = float(sum(i["ntokens"] for i in infos))
+    names = list(infos[0]["stages"].keys())
+    st_max = {k: float(np.mean([max(i["stages"][k] for i in st) for st in steps])) for k in names}
+    xmin = float(np.mean([min(i["stages"].get("exchange", 0.0) for i in st) for st in steps]))
+    k1 = [i["ms_tokcount"] for st in steps for i in st]
+    i0 = infos[0]
+    kern = k1_kernel(int(i0["flags"]))
+    alg0 = i0["nbytes"] + 12.0 * i0["npairs"]
+    k1_r0 = float(np.mean([st[0]["ms_tokcount"] for st in steps]))
+    achieved = alg0 / (k1_r0 * 1e-3) / 1e9
+    traffic, traffic_src = load_traffic(args.config, args.strong, N, kern)
+    ms_step = elapsed / args.steps * 1e3
+    line = {
+        "metric": "corpus GB/s (TF-IDF hot path: tokenize->TF->DF->tf*idf->ordered output)",
+        "value": round(C_all * args.steps / elapsed / 1e9, 4),
+        "unit": "GB/s",
+        "n_gpus": N,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "strong" if args.strong else "weak",
+        "vs_baseline": None,
+        "dtype": "u8/u32 (f64 score)",
+        "data": "synthetic (device-generated Zipfian corpus, csrc/synth.h), resident in HBM",
+        "config": {"workload": f"{args.config}: {sum(len(p['doc_ids']) for p in plans)} docs over {N} GPUs, "
+                               f"V={plans[0]['V']}, {C_all / 1e9:.3f} GB, {int(P_all)} pairs",
+                   "docs_total": int(plans[0]["ndocs_total"]), "corpus_bytes_total": int(C_all),
+                   "parallelism": f"doc-shard x{N}, one process (tfidf_group: RCCL clique, hash-owner DF "
+                                  f"exchange over xGMI)"},
+        "pairs_per_s": round(P_all * args.steps / elapsed, 1),
+        "tokens_per_s": round(T_all * args.steps / elapsed, 1),
+        "launcher": "in-process group (tfidf_group_open -> ncclCommInitAll)",
+        "stage_ms_max_over_ranks_mean": {k: round(v, 4) for k, v in st_max.items()},
+        "exchange_ms": round(st_max.get("exchange", 0.0), 4),
+        "exchange_ms_min_over_ranks": round(xmin, 4),
+        "k1_ms_mean_over_ranks": round(float(np.mean(k1)), 4),
+        "roofline": {"bound": "hbm", "kernel": f"{kern} (K1, rank 0)", "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "traffic_source": traffic_src, "alg_bytes_per_launch": int(alg0),
+                     "k1_avg_ms": round(k1_r0, 4)},
+        "cpu_baseline": None,
+        "device_allocs_in_timed_steps": a2[0] - a1[0],
+        "cold_run_ms": round(cold_ms, 3),
+        "cold_run": {"ms": round(cold_ms, 3), "device_allocs": a1[0] - a0[0]},
+    }
+    print(json.dumps(line), flush=True)
+    g.close()
+
+
+def hip_device_sync_all(n: int):
+    """hipDeviceSynchronize on devices 0..n-1 (the group's ranks)."""
+    hip = C.CDLL("libamdhip64.so.7")
+    for d in range(n):
+        if hip.hipSetDevice(d) != 0 or hip.hipDeviceSynchronize() != 0:
+            raise RuntimeError("hipDeviceSynchronize failed on device %d" % d)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -245,7 +338,14 @@ def main():
     if args.shards >= 2:
         return main_shards(args)
 
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return main_group(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None

@@ -22,7 +22,9 @@
 extern "C" {
 #endif
 
-#define TFIDF_ABI_VERSION 1
+/* 2: tfidf_run_info starts with its own size (set by the caller), the experimental K1 run
+ *    flags are gone */
+#define TFIDF_ABI_VERSION 2
 
 enum tfidf_status {
     TFIDF_OK = 0,
@@ -152,8 +154,12 @@ int tfidf_run(tfidf_ctx* ctx, const tfidf_corpus* corpus);
 int tfidf_fetch(tfidf_ctx* ctx, tfidf_result* out);
 void tfidf_result_free(tfidf_result* r);
 
-/* Counters of the last run (sizes, for roofline accounting). */
+/* Counters of the last run (sizes, for roofline accounting).  The caller sets `size` to
+ * sizeof(tfidf_run_info) as it was compiled; the library writes no byte past it (a
+ * caller built against an older, shorter struct gets its prefix), and sets `size` to the
+ * bytes it wrote.  TFIDF_E_INVAL when size < 16. */
 typedef struct tfidf_run_info {
+    uint64_t size;            /* in: sizeof(tfidf_run_info) of the caller; out: bytes written */
     uint64_t nbytes;          /* C */
     uint64_t ntokens;         /* T */
     uint64_t npairs;          /* P */
@@ -178,8 +184,6 @@ typedef struct tfidf_run_info {
                                  kernel of TFIDF_K1=general or an unaligned corpus leaves it clear) */
 #define TFIDF_RUN_K1_ST   4u  /* ... run as the LDS-staged k_tokcount_st (the default, vocabulary table <= 4M slots);
                                  clear with TFIDF_RUN_K1_VS set: k_tokcount_vs (larger tables) */
-#define TFIDF_RUN_K1_LEAN 16u /* ... run as k_tokcount_lean (experimental build only: TFIDF_K1=lean) */
-#define TFIDF_RUN_K1_WIN  32u /* ... run as the windowed k_tokcount_win (experimental build only: TFIDF_K1=win) */
 int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info);
 /* The same device-allocation counters without a run (process-wide, cumulative). */
 int tfidf_alloc_stats(uint64_t* allocs, uint64_t* bytes);

@@ -106,21 +106,17 @@ struct tfidf_ctx {
     bool timing = true;
     int k1_mode = 0;        /* 0 auto (k_tokcount_st up to K1_ST_MAX_CAP slots, k_tokcount_vs beyond),
                                1 round-1 kernel (TFIDF_K1=vs), 2 general K1 (TFIDF_K1=general),
-                               4 k_tokcount_st at any size <= K1_ST_MAX_CAP (TFIDF_K1=st); the
-                               experimental build only (make experimental, TFIDF_K1_EXPERIMENTAL):
-                               5 lean kernel (TFIDF_K1=lean), 6 windowed kernel (TFIDF_K1=win) —
+                               4 k_tokcount_st at any size <= K1_ST_MAX_CAP (TFIDF_K1=st) —
                                cross-checks and A/B timing */
     bool stamps_on = false; /* env TFIDF_STAMPS=1 with the diagnostic library build */
     int xfail_rank = -1;    /* env TFIDF_TEST_XFAIL_RANK (tests): this rank fails inside the exchange of
                                its first run, right after the key all-gather (the abort path of
                                exchange_df) */
+    int xnomem_rank = -1;   /* env TFIDF_TEST_XNOMEM_RANK (tests): this rank's receive-side allocation
+                               of its first exchange fails (the agreed path: no abort) */
     DevBuf stamps;
     bool k1_vs = false;     /* last run used the slot-keyed kernel (default) */
     bool k1_st = false;     /* ... and of those the LDS-staged tokcount_st (else tokcount_vs) */
-    bool k1_lean = false;   /* ... or k_tokcount_lean (TFIDF_K1=lean) */
-    bool k1_win = false;    /* ... or k_tokcount_win (the default up to K1_WIN_MAX_CAP slots) */
-    LeanParams* lp_host = nullptr;   /* pinned staging of k_tokcount_lean's parameter block */
-    DevBuf lp_dev;
     hipEvent_t ev[S_NSTAGES + 1];
     Arena arena;
     DevBuf arena_buf;
@@ -155,7 +151,6 @@ struct tfidf_ctx {
      * of pageable or synchronous copies (two round trips per run saved) */
     uint64_t* hpin = nullptr;
     DevBuf dense, vslot, skey0, skey1, seq0, seq1, rank_of_slot, slot_of_rank, rank16;
-    DevBuf hot_slot;        /* k_tokcount_lean's hot term ids -> vocabulary slots */
     DevBuf pkey0, pkey1, pseq0, pseq1, phead;
     DevBuf big_list, big_idx, dense_cnt, kcnt, tile_cnt;   /* dense merge of long documents */
     DevBuf df_local, df_global, present, idf_vals;
@@ -261,14 +256,12 @@ int tfidf_open(int device, tfidf_ctx** out) {
     if (km && !strcmp(km, "general")) ctx->k1_mode = 2;
     if (km && !strcmp(km, "vs")) ctx->k1_mode = 1;
     if (km && !strcmp(km, "st")) ctx->k1_mode = 4;
-#ifdef TFIDF_K1_EXPERIMENTAL
-    if (km && !strcmp(km, "lean")) ctx->k1_mode = 5;
-    if (km && !strcmp(km, "win")) ctx->k1_mode = 6;
-#endif
     const char* ks = getenv("TFIDF_STAMPS");
     ctx->stamps_on = ks && ks[0] == '1';
     const char* kx = getenv("TFIDF_TEST_XFAIL_RANK");
     ctx->xfail_rank = kx ? atoi(kx) : -1;
+    const char* kn = getenv("TFIDF_TEST_XNOMEM_RANK");
+    ctx->xnomem_rank = kn ? atoi(kn) : -1;
     /* diagnostics: initial vocabulary capacity (power of two) and the loads it may reach
      * before the run is repeated with a larger table (TFIDF_VLOAD percent below 16M slots,
      * default 12; TFIDF_VLOAD_BIG from 16M slots on, default 45) */
@@ -295,8 +288,6 @@ int tfidf_open(int device, tfidf_ctx** out) {
     if (arena_reset(ctx, 64ull << 20) != 0) { delete ctx; return TFIDF_E_NOMEM; }
     if (ctx->counters.ensure(256) != 0) { delete ctx; return TFIDF_E_NOMEM; }
     if (hipHostMalloc((void**)&ctx->hpin, 256, hipHostMallocDefault) != hipSuccess) { delete ctx; return TFIDF_E_NOMEM; }
-    if (hipHostMalloc((void**)&ctx->lp_host, sizeof(LeanParams), hipHostMallocDefault) != hipSuccess ||
-        ctx->lp_dev.ensure(sizeof(LeanParams)) != 0) { delete ctx; return TFIDF_E_NOMEM; }
     *out = ctx;
     return TFIDF_OK;
 }
@@ -315,7 +306,7 @@ void tfidf_close(tfidf_ctx* ctx) {
                       &ctx->chunk_start, &ctx->chunk_doc, &ctx->vkeys, &ctx->vrep, &ctx->rec_slot, &ctx->rec_cnt,
                       &ctx->part_doc, &ctx->part_slot, &ctx->part_cnt, &ctx->doc_recoff, &ctx->doc_npairs,
                       &ctx->doc_size, &ctx->doc_flags, &ctx->counters, &ctx->dense, &ctx->vslot, &ctx->skey0,
-                      &ctx->skey1, &ctx->seq0, &ctx->seq1, &ctx->rank_of_slot, &ctx->slot_of_rank, &ctx->rank16, &ctx->hot_slot, &ctx->pkey0,
+                      &ctx->skey1, &ctx->seq0, &ctx->seq1, &ctx->rank_of_slot, &ctx->slot_of_rank, &ctx->rank16, &ctx->pkey0,
                       &ctx->pkey1, &ctx->pseq0, &ctx->pseq1, &ctx->phead, &ctx->df_local, &ctx->df_global,
                       &ctx->present, &ctx->idf_vals, &ctx->dkey0, &ctx->dkey1, &ctx->dseq0, &ctx->dseq1,
                       &ctx->npairs_ord, &ctx->out_off, &ctx->doc_meta, &ctx->t_key, &ctx->t_len, &ctx->doc_tbytes,
@@ -327,8 +318,6 @@ void tfidf_close(tfidf_ctx* ctx) {
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i <= S_NSTAGES; ++i) (void)hipEventDestroy(ctx->ev[i]);
     if (ctx->hpin) (void)hipHostFree(ctx->hpin);
-    if (ctx->lp_host) (void)hipHostFree(ctx->lp_host);
-    ctx->lp_dev.release();
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -420,7 +409,10 @@ static int exchange_agree(tfidf_ctx* ctx, int local_rc, uint64_t v, uint64_t* ma
         if (l_ < 0) { HIPCHK(hipGetLastError()); return TFIDF_E_HIP; }      \
     } while (0)
 
-static int exchange_collective(tfidf_ctx* ctx, uint32_t V) {
+/* *agreed = true when the returned failure was decided by all ranks together (the
+ * receive-side allocation agreement): nothing is left half-done in a collective then, and
+ * the transport must not be aborted (tfidf.h: an agreed failure needs no action) */
+static int exchange_collective(tfidf_ctx* ctx, uint32_t V, bool* agreed) {
     hipStream_t s = ctx->stream;
     Xport* xp = ctx->xp;
     const int R = xp->nranks, me = xp->rank;
@@ -460,9 +452,13 @@ static int exchange_collective(tfidf_ctx* ctx, uint32_t V) {
     ens(ctx->x_reply, nrecv * 4 + 4);
     ens(ctx->x_tkey, tcap * 16);
     ens(ctx->x_tdf, tcap * 4);
+    if (ctx->xnomem_rank == me) {   /* tests: an agreed receive-side allocation failure (once) */
+        ctx->xnomem_rank = -1;
+        arc = TFIDF_E_NOMEM;
+    }
     rc = exchange_agree(ctx, arc, 0, nullptr);
     if (rc == 1) rc = TFIDF_E_STATE;
-    if (rc) return rc;
+    if (rc) { *agreed = true; return rc; }
     /* (key, local df) to the owners */
     rc = xp->alltoallv(ctx->x_skey.p, scnt.data(), ctx->x_rkey.p, rcnt.data(), 16, s);
     if (!rc) rc = xp->alltoallv(ctx->x_sdf.p, scnt.data(), ctx->x_rdf.p, rcnt.data(), 4, s);
@@ -505,8 +501,9 @@ static int exchange_df(tfidf_ctx* ctx, int local_rc, uint32_t V) {
     rc = exchange_agree(ctx, arc, 0, nullptr);   /* all allocated, or all fail */
     if (rc == 1) rc = TFIDF_E_STATE;               /* no retry is ever requested here */
     if (rc) return rc;
-    rc = exchange_collective(ctx, V);              /* step 3 */
-    if (rc && rc != TFIDF_E_PEER) ctx->xp->abort();
+    bool agreed = false;
+    rc = exchange_collective(ctx, V, &agreed);     /* step 3 */
+    if (rc && rc != TFIDF_E_PEER && !agreed) ctx->xp->abort();
     return rc;
 }
 
@@ -532,8 +529,6 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     const bool aligned = (((uintptr_t)c.bytes & 15u) == 0);
     ctx->k1_vs = aligned && (ctx->k1_mode <= 1 || ctx->k1_mode >= 4);
     if (ctx->k1_vs && ctx->vcap > K1_VS_MAX_CAP) return TFIDF_E_CAPACITY;
-    ctx->k1_win = ctx->k1_vs && ctx->k1_mode == 6 && ctx->vcap <= K1_WIN_MAX_CAP;
-    ctx->k1_lean = ctx->k1_vs && ctx->k1_mode == 5 && ctx->vcap <= K1_ST_MAX_CAP;
     ctx->k1_st = ctx->k1_vs && (ctx->k1_mode == 0 || ctx->k1_mode == 4) && ctx->vcap <= K1_ST_MAX_CAP;
     const uint32_t cb = ctx->k1_st ? CHUNK_BYTES_ST : CHUNK_BYTES;
     const uint64_t nchunks = span ? (span + cb - 1) / cb : 0;
@@ -584,31 +579,11 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     o.chunk_shard = cnt + 16;
     o.status = (uint32_t*)(cnt + 3);
     o.stamps = nullptr;
-    ENSURE(ctx->hot_slot, (size_t)HOT_SLOTS * 4);
-    o.hot_slot = ctx->hot_slot.as<uint32_t>();
-    o.hot_ctr = (uint32_t*)(cnt + 9);   /* zeroed with the run's counters */
     if (ctx->stamps_on) {
         ENSURE(ctx->stamps, 8 * K1_STAMP_WORDS);
         HIPCHK(hipMemsetAsync(ctx->stamps.p, 0, 8 * K1_STAMP_WORDS, s));
         o.stamps = ctx->stamps.as<unsigned long long>();
     }
-#ifdef TFIDF_K1_EXPERIMENTAL
-    if (nchunks && (ctx->k1_lean || ctx->k1_win)) {
-        LeanParams& lp = *ctx->lp_host;
-        lp.c = c;
-        lp.v = vd;
-        lp.o = o;
-        lp.chunk_start = ctx->chunk_start.as<uint64_t>();
-        lp.chunk_doc = ctx->chunk_doc.as<uint32_t>();
-        lp.c0 = 0;
-        lp.c1 = nchunks;
-        /* pinned source: the copy is stream-ordered before the launch and the block is not
-         * rewritten before the next run's copy (which follows this kernel on the stream) */
-        HIPCHK(hipMemcpyAsync(ctx->lp_dev.p, &lp, sizeof(LeanParams), hipMemcpyHostToDevice, s));
-        if (ctx->k1_win) LCHK(launch_tokcount_win(ctx->lp_dev.as<LeanParams>(), lp, s));
-        else LCHK(launch_tokcount_lean(ctx->lp_dev.as<LeanParams>(), lp, s));
-    } else
-#endif
     if (nchunks && ctx->k1_st)
         LCHK(launch_tokcount_st(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
     else if (nchunks && ctx->k1_vs)
@@ -616,10 +591,6 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     else if (nchunks)
         LCHK(launch_tokcount(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
     mark(ctx, S_VOCAB);
-    /* the lean K1's hot-term marks leave the keys before anything else reads them */
-#ifdef TFIDF_K1_EXPERIMENTAL
-    if (nchunks && ctx->k1_lean) LCHK(launch_hot_unmark(vd.keys, o.hot_slot, o.hot_ctr, s));
-#endif
     /* the vocabulary's used-slot flags and count are enqueued before the host reads K1's
      * counters: one host round trip for both */
     const uint64_t cap = ctx->vcap;
@@ -699,8 +670,8 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     ENSURE(ctx->skey1, (size_t)V * 16 + 16);
     ENSURE(ctx->seq0, (size_t)V * 4 + 4);
     ENSURE(ctx->seq1, (size_t)V * 4 + 4);
-    /* rank maps: one entry per slot, plus one per hot term id (slot cap + id) */
-    ENSURE(ctx->rank_of_slot, (cap + HOT_SLOTS) * 4);
+    /* rank maps: one entry per slot */
+    ENSURE(ctx->rank_of_slot, cap * 4);
     ENSURE(ctx->slot_of_rank, (size_t)V * 4 + 4);
     LCHK(launch_vocab_compact(vd, cap, ctx->dense.as<uint32_t>(), c, ctx->vslot.as<uint32_t>(), ctx->skey0.as<uint4>(),
                               ctx->seq0.as<uint32_t>(), s));
@@ -738,14 +709,9 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     if (st & ST_HAS_LONG)   /* terms of >= 16 bytes exist: order the ones tied on 16 bytes */
         LCHK(launch_vocab_long_fixup(ctx->sorted_skey, ctx->sorted_dense, ctx->vslot.as<uint32_t>(), vd, c, V, ar, s));
     uint16_t* r16 = nullptr;
-    if (V <= 65536u) { ENSURE(ctx->rank16, (cap + HOT_SLOTS) * 2); r16 = ctx->rank16.as<uint16_t>(); }
+    if (V <= 65536u) { ENSURE(ctx->rank16, cap * 2); r16 = ctx->rank16.as<uint16_t>(); }
     LCHK(launch_vocab_rank(ctx->sorted_dense, ctx->vslot.as<uint32_t>(), V, ctx->rank_of_slot.as<uint32_t>(),
                            ctx->slot_of_rank.as<uint32_t>(), r16, s));
-#ifdef TFIDF_K1_EXPERIMENTAL
-    if (nchunks && ctx->k1_lean)
-        LCHK(launch_hot_ranks(ctx->rank_of_slot.as<uint32_t>(), r16, cap, ctx->hot_slot.as<uint32_t>(),
-                              (const uint32_t*)(cnt + 9), s));
-#endif
     /* ---- partial documents ---- */
     mark(ctx, S_MERGE);
     uint64_t R_total = R_main;
@@ -845,7 +811,7 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     /* also rewrites every record's slot as its term rank (K5 then needs no rank gather) */
     LCHK(launch_df_hist(ctx->rec_slot.as<uint32_t>(), R_main, merged_count, R_total,
                         ctx->rank_of_slot.as<uint32_t>(),
-                        V <= 65536u ? ctx->rank16.as<uint16_t>() : nullptr, V, cap + HOT_SLOTS,
+                        V <= 65536u ? ctx->rank16.as<uint16_t>() : nullptr, V, cap,
                         (uint32_t*)(cnt + 3), ctx->df_local.as<uint32_t>(), ar, s));
     ctx->run_V = V;
     ctx->run_cap = cap;
@@ -969,7 +935,7 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
     a.nterms = V;
     a.rank_bits = V > 1 ? 32u - (uint32_t)__builtin_clz(V - 1) : 1u;
     a.rec_total = R_total;
-    a.slot_cap = cap + HOT_SLOTS;
+    a.slot_cap = cap;
     a.status = (uint32_t*)(cnt + 3);
     a.out_term = ctx->out_term.as<uint32_t>();
     a.out_cnt = ctx->out_cnt.as<uint32_t>();
@@ -1168,10 +1134,14 @@ extern "C" int tfidf_alloc_stats(uint64_t* allocs, uint64_t* bytes) {
     return TFIDF_OK;
 }
 
-extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info) {
-    if (!ctx || !info) return TFIDF_E_INVAL;
+extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* out) {
+    tfidf_run_info* info = out;
+    if (!ctx || !info || info->size < 16) return TFIDF_E_INVAL;
     if (!ctx->have_info) return TFIDF_E_STATE;
-    memset(info, 0, sizeof(*info));
+    const size_t want = info->size < sizeof(tfidf_run_info) ? (size_t)info->size : sizeof(tfidf_run_info);
+    tfidf_run_info full;
+    memset(&full, 0, sizeof(full));
+    info = &full;   /* filled whole here, copied out up to the caller's size below */
     info->nbytes = ctx->run_nbytes;   /* no device round trip: the run read the bounds */
     info->ntokens = ctx->ntokens;
     info->npairs = ctx->npairs;
@@ -1185,10 +1155,11 @@ extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info) {
     info->ms_tokcount = ctx->ms_stage[S_TOKCOUNT];
     for (int i = 0; i < S_NSTAGES; ++i) info->ms_stage[i] = ctx->ms_stage[i];
     info->nstages = S_NSTAGES;
-    info->flags = (ctx->k1_vs ? TFIDF_RUN_K1_VS : 0u) | (ctx->k1_st ? TFIDF_RUN_K1_ST : 0u) |
-                  (ctx->k1_lean ? TFIDF_RUN_K1_LEAN : 0u) | (ctx->k1_win ? TFIDF_RUN_K1_WIN : 0u);
+    info->flags = (ctx->k1_vs ? TFIDF_RUN_K1_VS : 0u) | (ctx->k1_st ? TFIDF_RUN_K1_ST : 0u);
     info->device_allocs = g_dev_allocs.load(std::memory_order_relaxed);
     info->device_alloc_bytes = g_dev_alloc_bytes.load(std::memory_order_relaxed);
+    full.size = want;
+    memcpy(out, &full, want);
     return TFIDF_OK;
 }
 

@@ -2005,15 +2005,27 @@ __global__ void k_owner_scatter(const uint4* __restrict__ keys, const uint32_t* 
 /* owner side: find-or-insert of a received key into the owner's table (the claim protocol
  * of the vocabulary's vocab_insert_s: EMPTY -> PENDING by CAS, low word, then the high word
  * published); *claimed when this call inserted it.  The table holds >= 1.5x the received
- * entries, so a probe run ends. */
-__device__ uint32_t owner_insert(uint4* __restrict__ keys, uint64_t mask, uint64_t klo, uint64_t khi, bool* claimed) {
+ * entries, so a probe run ends.  One loop body for every case: a lane that finds a slot
+ * PENDING re-reads it (at the memory side) in its next iteration, so a claiming lane of the
+ * same wave publishes in the same pass of the body instead of waiting behind the spin; the
+ * wait is bounded anyway (ST_VOCAB_SPIN, INVALID_SLOT). */
+__device__ uint32_t owner_insert(uint4* __restrict__ keys, uint64_t mask, uint64_t klo, uint64_t khi, bool* claimed,
+                                 uint32_t* status) {
     uint64_t h = key_hash(klo, khi) & mask;
-    for (uint64_t probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
+    uint32_t spins = 0;
+    bool reread = false;
+    for (uint64_t probe = 0; probe <= mask;) {
         unsigned long long* slot = reinterpret_cast<unsigned long long*>(&keys[h]);
-        const uint4 s = keys[h];
-        uint64_t lo = ((uint64_t)s.y << 32) | s.x, hi = ((uint64_t)s.w << 32) | s.z;
-        if (hi == khi && lo == klo) return (uint32_t)h;
-        if (hi != KEY_EMPTY_HI && hi != KEY_PENDING_HI) continue;
+        uint64_t lo, hi;
+        if (reread) {
+            hi = atomicOr(&slot[1], 0ull);
+            lo = atomicOr(&slot[0], 0ull);
+        } else {
+            const uint4 s = keys[h];
+            lo = ((uint64_t)s.y << 32) | s.x;
+            hi = ((uint64_t)s.w << 32) | s.z;
+        }
+        reread = false;
         if (hi == KEY_EMPTY_HI) {
             const unsigned long long old = atomicCAS(&slot[1], (unsigned long long)KEY_EMPTY_HI,
                                                      (unsigned long long)KEY_PENDING_HI);
@@ -2024,16 +2036,19 @@ __device__ uint32_t owner_insert(uint4* __restrict__ keys, uint64_t mask, uint64
                 *claimed = true;
                 return (uint32_t)h;
             }
-            hi = old;
+            reread = true;                 /* another lane claimed it: look again */
+            continue;
         }
-        while (hi == KEY_PENDING_HI) {
+        if (hi == KEY_PENDING_HI) {
+            if (++spins > (1u << 22)) { atomicOr(status, ST_VOCAB_SPIN); return INVALID_SLOT; }
             __builtin_amdgcn_s_sleep(2);
-            hi = atomicOr(&slot[1], 0ull);
+            reread = true;
+            continue;
         }
-        if (hi == khi) {
-            lo = atomicOr(&slot[0], 0ull);
-            if (lo == klo) return (uint32_t)h;
-        }
+        /* a published hi carries its lo (lo is written first, both in one line) */
+        if (hi == khi && lo == klo) return (uint32_t)h;
+        h = (h + 1) & mask;
+        ++probe;
     }
     return INVALID_SLOT;
 }
@@ -2048,8 +2063,9 @@ __global__ void k_owner_insert(const uint4* __restrict__ rkey, const uint32_t* _
         bool claimed = false;
         if (i < n) {
             const uint4 k = rkey[i];
-            const uint32_t sl = owner_insert(tkey, tmask, ((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z, &claimed);
-            if (sl == INVALID_SLOT) {   /* not reachable at the table's load */
+            const uint32_t sl = owner_insert(tkey, tmask, ((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z, &claimed,
+                                             status);
+            if (sl == INVALID_SLOT) {   /* not reachable at the table's load (or a bounded wait gave up) */
                 atomicOr(status, ST_BOUNDS);
                 rslot[i] = 0u;
             } else {

@@ -22,6 +22,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <memory>
 #include <mutex>
@@ -36,26 +38,43 @@ namespace {
 
 /* ------------------------------------------------------------------ RCCL -- */
 
-/* The communicators of one tfidf_group clique (ncclCommInitAll in one process).  An error
- * on one rank after the agreement aborts EVERY communicator of the clique: a peer already
- * inside an all-gather / all-reduce (or the stream synchronisation after it) is released
- * by its own communicator's abort, not by the failing rank's.  `mu` orders the enqueue of
- * a collective against the abort (no collective is enqueued on an aborted communicator);
- * the synchronisations run outside it, so an abort can happen while a peer waits. */
+/* The communicators of one tfidf_group clique (ncclCommInitAll in one process, one host
+ * thread per rank).  Each rank's communicator has its own lock, held only by that rank's
+ * thread while it enqueues a collective: RCCL connects peers lazily inside those calls and
+ * blocks until the peer ranks make the matching call, so a lock shared by the clique would
+ * deadlock the first collective (rank A inside ncclGroupEnd waiting for B, B waiting for the
+ * lock).  An error on one rank after the agreement aborts every communicator of the clique:
+ * a peer already waiting for a collective's kernels (the stream synchronisation after it) is
+ * released by the abort of its own communicator.  abort_all takes each rank's lock in turn
+ * (bounded wait) so no communicator is freed while its thread is inside an RCCL call; a rank
+ * whose lock it could not take aborts its own communicator when its call returns. */
 struct Clique {
-    std::mutex mu;
     std::vector<ncclComm_t> comms;
-    bool aborted = false;
+    std::vector<std::unique_ptr<std::mutex>> mu;   /* one per rank */
+    std::atomic<bool> aborted{false};
+    explicit Clique(int n) : comms((size_t)n, nullptr) {
+        for (int r = 0; r < n; ++r) mu.emplace_back(new std::mutex());
+    }
     ~Clique() {
         for (ncclComm_t c : comms)
             if (c) (void)ncclCommDestroy(c);
     }
+    /* with mu[r] held */
+    void abort_rank_locked(int r) {
+        if (comms[r]) { (void)ncclCommAbort(comms[r]); comms[r] = nullptr; }
+    }
     void abort_all() {
-        std::lock_guard<std::mutex> lk(mu);
-        if (aborted) return;
-        aborted = true;
-        for (ncclComm_t& c : comms)
-            if (c) { (void)ncclCommAbort(c); c = nullptr; }
+        aborted.store(true);
+        for (size_t r = 0; r < comms.size(); ++r) {
+            for (int t = 0; t < 2000; ++t) {   /* up to ~2 s per rank */
+                if (mu[r]->try_lock()) {
+                    abort_rank_locked((int)r);
+                    mu[r]->unlock();
+                    break;
+                }
+                std::this_thread::sleep_for(std::chrono::milliseconds(1));
+            }
+        }
     }
 };
 
@@ -68,12 +87,20 @@ struct RcclXport final : Xport {
         if (own) (void)ncclCommDestroy(own);
         if (dwords) (void)hipFree(dwords);
     }
-    /* enqueues f(comm) under the clique lock; TFIDF_E_PEER once the clique was aborted */
+    /* enqueues f(comm) under this rank's lock; TFIDF_E_PEER once the clique was aborted */
     template <class F> int enqueue(F&& f) {
         if (clique) {
-            std::lock_guard<std::mutex> lk(clique->mu);
-            if (clique->aborted || !clique->comms[rank]) return TFIDF_E_PEER;
-            return f(clique->comms[rank]) == ncclSuccess ? TFIDF_OK : TFIDF_E_RCCL;
+            std::lock_guard<std::mutex> lk(*clique->mu[rank]);
+            if (clique->aborted.load() || !clique->comms[rank]) {
+                clique->abort_rank_locked(rank);
+                return TFIDF_E_PEER;
+            }
+            const ncclResult_t r = f(clique->comms[rank]);
+            if (clique->aborted.load()) {   /* aborted while this call ran: release our kernels */
+                clique->abort_rank_locked(rank);
+                return TFIDF_E_PEER;
+            }
+            return r == ncclSuccess ? TFIDF_OK : TFIDF_E_RCCL;
         }
         if (!own) return TFIDF_E_STATE;
         return f(own) == ncclSuccess ? TFIDF_OK : TFIDF_E_RCCL;
@@ -81,10 +108,7 @@ struct RcclXport final : Xport {
     /* a synchronisation that an abort of the clique released reports TFIDF_E_PEER */
     int sync(hipStream_t s) {
         const hipError_t e = hipStreamSynchronize(s);
-        if (clique) {
-            std::lock_guard<std::mutex> lk(clique->mu);
-            if (clique->aborted) return TFIDF_E_PEER;
-        }
+        if (clique && clique->aborted.load()) return TFIDF_E_PEER;
         return e == hipSuccess ? TFIDF_OK : TFIDF_E_HIP;
     }
     int words(const uint64_t mine[2], uint64_t* all, hipStream_t s) override {
@@ -286,8 +310,7 @@ int tfidf_group_open(int nranks, const int* devices, uint32_t flags, tfidf_group
         /* one RCCL communicator per GPU of the clique (a 1-rank group gets one too, so the
          * exchange path is the same at every size), owned by the clique so that an error on
          * one rank aborts them all */
-        auto cl = std::make_shared<Clique>();
-        cl->comms.assign((size_t)nranks, nullptr);
+        auto cl = std::make_shared<Clique>(nranks);
         if (ncclCommInitAll(cl->comms.data(), nranks, dev.data()) != ncclSuccess) rc = TFIDF_E_RCCL;
         for (int r = 0; r < nranks && !rc; ++r) {
             RcclXport* x = new RcclXport();

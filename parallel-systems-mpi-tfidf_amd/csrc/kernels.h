@@ -78,8 +78,6 @@ struct K1Out {
     unsigned long long* chunk_shard; /* tokcount_st: 8 sharded chunk counters (zeroed per run) */
     unsigned long long* stamps;  /* diagnostic build only: K1_NSTAMP phase cycle sums, WG count,
                                     then K1_NCOUNT event counters */
-    uint32_t* hot_slot;          /* k_tokcount_lean: vocabulary slot of hot term id (HOT_MAX) */
-    uint32_t* hot_ctr;           /* ... hot ids handed out (zeroed per run; may exceed HOT_MAX) */
 };
 #define K1_NSTAMP 17
 #define K1_NCOUNT 4   /* segments, flushes, tokens taking the full probe, probe iterations */
@@ -105,32 +103,6 @@ int launch_tokcount_vs(const CorpusDev& c, const uint64_t* chunk_start, const ui
 
 #define K1_ST_MAX_CAP (1ull << 22)   /* tokcount_st up to this vocabulary capacity, tokcount_vs beyond */
 
-/* K1 lean (tokcount_lean.hip): the default tokenize+count kernel up to K1_ST_MAX_CAP.  Its
- * rarely used pointers and sizes are read from this block in device memory where they are
- * used (scalar loads), not held in registers; `h` is the same block on the host (the
- * launcher reads the hot fields from it).  Requires c0 == 0, a 16-byte aligned corpus. */
-struct LeanParams {
-    CorpusDev c;
-    VocabDev v;
-    K1Out o;
-    const uint64_t* chunk_start;
-    const uint32_t* chunk_doc;
-    uint64_t c0, c1;
-};
-int launch_tokcount_lean(const LeanParams* dparams, const LeanParams& h, hipStream_t s);
-/* K1 windowed (tokcount_win.hip): block-wide 8 KiB windows, batched vocabulary loads; the
- * same parameter block and contract as k_tokcount_lean without hot terms; vocabulary
- * tables < 2^24 slots */
-int launch_tokcount_win(const LeanParams* dparams, const LeanParams& h, hipStream_t s);
-#define K1_WIN_MAX_CAP (1ull << 22)
-/* after k_tokcount_lean: clear the hot marks from the vocabulary keys (before any other
- * stage reads them) */
-int launch_hot_unmark(uint4* keys, const uint32_t* hot_slot, const uint32_t* hot_ctr, hipStream_t s);
-/* after the vocabulary ranks: rank_of_slot[cap + id] (and rank16) = the rank of hot term id
- * (k_tokcount_lean writes a dense-counted pair's record with slot cap + id) */
-int launch_hot_ranks(uint32_t* rank_of_slot, uint16_t* rank16, uint64_t cap, const uint32_t* hot_slot,
-                     const uint32_t* hot_ctr, hipStream_t s);
-#define HOT_SLOTS 1024u   /* = HOT_MAX (dev_vocab.h): slots cap .. cap + HOT_SLOTS of the rank maps */
 
 /* vocabulary finalisation */
 int launch_vocab_flags(const VocabDev& v, uint64_t cap, uint32_t* flags, hipStream_t s);

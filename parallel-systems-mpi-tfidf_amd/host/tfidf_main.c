@@ -74,6 +74,7 @@ static int run_single(int device, const char* indir, const char* outpath, int de
     if (!rc && debug) rc = debug_jobs(ctx);
     if (rc) { tfidf_close(ctx); return fail(rc); }
     tfidf_run_info ri;
+    ri.size = sizeof(ri);
     double t_out = 0;
     if (stats) { tfidf_last_run_info(ctx, &ri); t_out = wall_ms(); }
     /* lines formatted on the GPU, copied out through pinned buffers (TFIDF.c:245,274-282) */
@@ -174,6 +175,7 @@ static int run_sharded(int ngpus, int nshards, const char* indir, const char* ou
         uint64_t pairs = 0, bytes = 0;
         for (int r = 0; r < nshards; ++r) {
             tfidf_run_info ri;
+            ri.size = sizeof(ri);
             if (tfidf_last_run_info(tfidf_group_ctx(g, r), &ri) == 0) pairs += ri.npairs;
             bytes += plan.shard_bytes[r];
         }

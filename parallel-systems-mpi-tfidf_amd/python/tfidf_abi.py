@@ -22,8 +22,7 @@ TFIDF_CORPUS_DEVICE = 1
 UNIQUE_ID_BYTES = 128
 RUN_K1_VS = 2   # tfidf_run_info.flags (include/tfidf.h): slot-keyed K1 ...
 RUN_K1_ST = 4   # ... run as k_tokcount_st (the default up to 4M vocabulary slots; else k_tokcount_vs)
-RUN_K1_LEAN = 16  # ... run as k_tokcount_lean (experimental library: TFIDF_LIB=exp TFIDF_K1=lean)
-RUN_K1_WIN = 32   # ... run as k_tokcount_win (experimental library: TFIDF_LIB=exp TFIDF_K1=win)
+ABI_VERSION = 2  # TFIDF_ABI_VERSION of include/tfidf.h this binding is written for
 
 # exported symbols declared by include/tfidf.h
 EXPORTS = [
@@ -34,7 +33,7 @@ EXPORTS = [
     "tfidf_format", "tfidf_copy_text", "tfidf_write_output_gpu", "tfidf_format_f64",
     "tfidf_ingest_dir_device", "tfidf_hbm_probe", "tfidf_group_open", "tfidf_group_size", "tfidf_group_ctx",
     "tfidf_group_run", "tfidf_group_write_output", "tfidf_group_close", "tfidf_plan_dir", "tfidf_plan_free",
-    "tfidf_ingest_shard_device", "tfidf_doc_name_order", "tfidf_shard_split",
+    "tfidf_ingest_shard_device", "tfidf_doc_name_order", "tfidf_shard_split", "tfidf_device_count",
 ]
 TFIDF_GROUP_LOCAL = 1
 E_PEER = -11
@@ -61,7 +60,7 @@ class Result(C.Structure):
 
 class RunInfo(C.Structure):
     _fields_ = [
-        ("nbytes", C.c_uint64), ("ntokens", C.c_uint64), ("npairs", C.c_uint64), ("nterms", C.c_uint32),
+        ("size", C.c_uint64), ("nbytes", C.c_uint64), ("ntokens", C.c_uint64), ("npairs", C.c_uint64), ("nterms", C.c_uint32),
         ("nterms_global", C.c_uint32), ("nchunks", C.c_uint64), ("partial_records", C.c_uint64),
         ("ndocs", C.c_uint32), ("vocab_capacity", C.c_uint32), ("ms_total", C.c_double),
         ("ms_tokcount", C.c_double), ("ms_stage", C.c_double * 16), ("nstages", C.c_uint32), ("flags", C.c_uint32),
@@ -134,6 +133,9 @@ def lib() -> C.CDLL:
                                                 C.POINTER(Corpus), C.POINTER(C.c_uint32), C.POINTER(IngestInfo)]
         L.tfidf_doc_name_order.argtypes = [C.c_uint32, C.c_void_p]
         L.tfidf_shard_split.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
+        if L.tfidf_abi_version() != ABI_VERSION:
+            raise RuntimeError(f"{LIB_PATH}: ABI version {L.tfidf_abi_version()}, binding expects {ABI_VERSION} "
+                               f"(stale build: rebuild with __graft_entry__.build())")
         _lib = L
     return _lib
 
@@ -262,8 +264,9 @@ class Engine:
 
     def info(self) -> dict:
         r = RunInfo()
+        r.size = C.sizeof(RunInfo)
         _chk(lib().tfidf_last_run_info(self.h, C.byref(r)), "tfidf_last_run_info")
-        d = {k: getattr(r, k) for k, _ in RunInfo._fields_ if k != "ms_stage"}
+        d = {k: getattr(r, k) for k, _ in RunInfo._fields_ if k not in ("ms_stage", "size")}
         d["stages"] = {lib().tfidf_stage_name(i).decode(): r.ms_stage[i] for i in range(r.nstages)}
         return d
 
@@ -414,6 +417,11 @@ def format_lines(res: dict) -> bytes:
     for d, t, s in zip(res["doc"].tolist(), res["term"].tolist(), res["score"].tolist()):
         parts.append(b"doc%d@" % d + terms[t] + b"\t%.16f\n" % s)
     return b"".join(parts)
+
+
+def device_count() -> int:
+    """Visible HIP devices (tfidf_device_count; 0 without a GPU)."""
+    return int(lib().tfidf_device_count())
 
 
 def comm_unique_id() -> bytes:

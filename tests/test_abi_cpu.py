@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     for name in decl:
         assert hasattr(lib, name), name
     assert set(tfidf_abi.EXPORTS) <= set(decl)
-    assert lib.tfidf_abi_version() == 1
+    assert lib.tfidf_abi_version() == tfidf_abi.ABI_VERSION == 2
 
 
 def test_library_is_gfx950_code_object():

@@ -156,6 +156,23 @@ def test_exchange_failure_after_allgather_aborts_peers(failing, monkeypatch):
         assert b"".join(g.ranks[r].text() for r in range(3)) == ora["output_txt"]
 
 
+@pytest.mark.parametrize("failing", [0, 2])
+def test_exchange_agreed_alloc_failure_keeps_group_usable(failing, monkeypatch):
+    """A receive-side allocation failure inside the exchange is agreed between the ranks
+    (TFIDF_TEST_XNOMEM_RANK): every rank returns an error before the (key, df) all-to-all,
+    the transport is NOT aborted (tfidf.h: an agreed failure needs no action from the
+    caller), and the next run of the same group succeeds with the oracle's output."""
+    shards = _shards("c2", 0.001, 3)
+    monkeypatch.setenv("TFIDF_TEST_XNOMEM_RANK", str(failing))   # read by tfidf_open; fires once
+    with tfidf_abi.Group(3, devices=[0, 0, 0]) as g:
+        with pytest.raises(tfidf_abi.TfidfError) as ei:
+            g.run_host(shards)
+        assert ei.value.rc == -2   # TFIDF_E_NOMEM, the failing rank's own error (the others: E_PEER)
+        g.run_host(shards)
+        ora = _full("c2", 0.001)
+        assert b"".join(g.ranks[r].text() for r in range(3)) == ora["output_txt"]
+
+
 def test_rccl_single_rank_runs_the_exchange():
     """A 1-rank RCCL communicator: exchange_df runs (agreement, the count ncclAllGather, the
     self all-to-all by ncclSend / ncclRecv, the owner aggregation) and the results are
