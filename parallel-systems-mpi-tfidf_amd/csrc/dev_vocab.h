@@ -22,10 +22,13 @@
  * across XCDs, device-scope atomics are).  Every case runs in one loop body: a lane that
  * finds a slot PENDING re-reads it in its next iteration, so a lane of the same wave that
  * holds the claim publishes in the same pass of the body (no lane waits in an inner spin
- * loop that its wave's claimer might be scheduled behind); the wait is bounded. */
+ * loop that its wave's claimer might be scheduled behind); the wait is bounded.
+ * Probing starts at the EVEN slot of the key's hash (home = hash & mask & ~1): the K1
+ * kernels load a key's home pair (two 16-byte slots, one aligned 32-byte piece, never
+ * wrapping) and find every key that sits in its home pair without a dependent load. */
 __device__ __forceinline__ uint32_t vocab_insert_s(uint4* __restrict__ keys, uint64_t* __restrict__ reps, uint64_t mask,
                                                 uint64_t klo, uint64_t khi, uint64_t rep, uint32_t* status) {
-    uint64_t h = key_hash(klo, khi) & mask;
+    uint64_t h = key_hash(klo, khi) & mask & ~1ull;
     uint32_t spins = 0;
     bool reread = false;
     for (uint32_t probe = 0; probe < VOCAB_MAX_PROBE && probe <= mask;) {

@@ -104,10 +104,10 @@ struct tfidf_ctx {
     Xport* xp = nullptr;    /* peers of the DF exchange (RCCL or in-process); owned */
     int rank = 0, nranks = 1;
     bool timing = true;
-    int k1_mode = 0;        /* 0 auto (k_tokcount_st up to K1_ST_MAX_CAP slots, k_tokcount_vs beyond),
+    int k1_mode = 0;        /* 0 auto (k_tokcount_sl up to K1_ST_MAX_CAP slots, k_tokcount_vs beyond),
                                1 round-1 kernel (TFIDF_K1=vs), 2 general K1 (TFIDF_K1=general),
-                               4 k_tokcount_st at any size <= K1_ST_MAX_CAP (TFIDF_K1=st) —
-                               cross-checks and A/B timing */
+                               4 the persistent k_tokcount_st (TFIDF_K1=st), 3 k_tokcount_sl
+                               (TFIDF_K1=sl) — cross-checks and A/B timing */
     bool stamps_on = false; /* env TFIDF_STAMPS=1 with the diagnostic library build */
     int xfail_rank = -1;    /* env TFIDF_TEST_XFAIL_RANK (tests): this rank fails inside the exchange of
                                its first run, right after the key all-gather (the abort path of
@@ -116,7 +116,10 @@ struct tfidf_ctx {
                                of its first exchange fails (the agreed path: no abort) */
     DevBuf stamps;
     bool k1_vs = false;     /* last run used the slot-keyed kernel (default) */
-    bool k1_st = false;     /* ... and of those the LDS-staged tokcount_st (else tokcount_vs) */
+    bool k1_st = false;     /* ... and of those the LDS-staged tokcount_st */
+    bool k1_sl = false;     /* ... or tokcount_sl (else tokcount_vs) */
+    K1Out* k1out_host = nullptr;   /* pinned: tokcount_sl's output block, copied to k1out_dev per run */
+    DevBuf k1out_dev;
     hipEvent_t ev[S_NSTAGES + 1];
     Arena arena;
     DevBuf arena_buf;
@@ -160,8 +163,12 @@ struct tfidf_ctx {
     /* DF exchange (hash owners): this rank's keys by term rank, the send side grouped by
      * owner (key, local df, term rank), the owner side (received keys and df, their table
      * slots, the replies, the aggregation table), the returned global df, the count matrix */
-    DevBuf x_mine, x_skey, x_sdf, x_sidx, x_back, x_cnt;
-    DevBuf x_rkey, x_rdf, x_rslot, x_reply, x_tkey, x_tdf;
+    DevBuf x_mine, x_srec, x_sidx, x_back, x_cnt;
+    DevBuf x_rrec, x_rslot, x_reply, x_tkey, x_tdf;
+    /* dense exchange (small vocabularies): gathered keys, shared positions, the DF vector */
+    DevBuf x_gkeys, x_pos, x_dense;
+    int xchg_mode = 0;      /* env TFIDF_XCHG: 0 auto (dense up to DENSE_XCHG_MAXV terms per rank), 1 owner, 2 dense */
+    bool last_dense = false;   /* the last exchange used the dense form */
     /* sizes the local part of a run hands to the exchange and the stages after it */
     uint32_t run_N = 0, run_V = 0;
     uint64_t run_cap = 0, run_R_total = 0;
@@ -256,10 +263,14 @@ int tfidf_open(int device, tfidf_ctx** out) {
     if (km && !strcmp(km, "general")) ctx->k1_mode = 2;
     if (km && !strcmp(km, "vs")) ctx->k1_mode = 1;
     if (km && !strcmp(km, "st")) ctx->k1_mode = 4;
+    if (km && !strcmp(km, "sl")) ctx->k1_mode = 3;
     const char* ks = getenv("TFIDF_STAMPS");
     ctx->stamps_on = ks && ks[0] == '1';
     const char* kx = getenv("TFIDF_TEST_XFAIL_RANK");
     ctx->xfail_rank = kx ? atoi(kx) : -1;
+    const char* kxm = getenv("TFIDF_XCHG");
+    if (kxm && !strcmp(kxm, "owner")) ctx->xchg_mode = 1;
+    if (kxm && !strcmp(kxm, "dense")) ctx->xchg_mode = 2;
     const char* kn = getenv("TFIDF_TEST_XNOMEM_RANK");
     ctx->xnomem_rank = kn ? atoi(kn) : -1;
     /* diagnostics: initial vocabulary capacity (power of two) and the loads it may reach
@@ -288,6 +299,8 @@ int tfidf_open(int device, tfidf_ctx** out) {
     if (arena_reset(ctx, 64ull << 20) != 0) { delete ctx; return TFIDF_E_NOMEM; }
     if (ctx->counters.ensure(256) != 0) { delete ctx; return TFIDF_E_NOMEM; }
     if (hipHostMalloc((void**)&ctx->hpin, 256, hipHostMallocDefault) != hipSuccess) { delete ctx; return TFIDF_E_NOMEM; }
+    if (hipHostMalloc((void**)&ctx->k1out_host, sizeof(K1Out), hipHostMallocDefault) != hipSuccess ||
+        ctx->k1out_dev.ensure(sizeof(K1Out)) != 0) { delete ctx; return TFIDF_E_NOMEM; }
     *out = ctx;
     return TFIDF_OK;
 }
@@ -311,13 +324,16 @@ void tfidf_close(tfidf_ctx* ctx) {
                       &ctx->present, &ctx->idf_vals, &ctx->dkey0, &ctx->dkey1, &ctx->dseq0, &ctx->dseq1,
                       &ctx->npairs_ord, &ctx->out_off, &ctx->doc_meta, &ctx->t_key, &ctx->t_len, &ctx->doc_tbytes,
                       &ctx->doc_toff, &ctx->text, &ctx->out_term, &ctx->out_cnt,
-                      &ctx->out_score, &ctx->idf_rank, &ctx->large_list, &ctx->split_tasks, &ctx->cls_off, &ctx->x_mine, &ctx->x_skey, &ctx->x_sdf,
-                      &ctx->x_sidx, &ctx->x_back, &ctx->x_cnt, &ctx->x_rkey, &ctx->x_rdf, &ctx->x_rslot, &ctx->x_reply,
+                      &ctx->out_score, &ctx->idf_rank, &ctx->large_list, &ctx->split_tasks, &ctx->cls_off, &ctx->x_mine, &ctx->x_srec,
+                      &ctx->x_sidx, &ctx->x_back, &ctx->x_cnt, &ctx->x_rrec, &ctx->x_rslot, &ctx->x_reply, &ctx->x_gkeys,
+                      &ctx->x_pos, &ctx->x_dense,
                       &ctx->x_tkey, &ctx->x_tdf, &ctx->stamps, &ctx->big_list, &ctx->big_idx, &ctx->dense_cnt, &ctx->kcnt,
                       &ctx->tile_cnt};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i <= S_NSTAGES; ++i) (void)hipEventDestroy(ctx->ev[i]);
     if (ctx->hpin) (void)hipHostFree(ctx->hpin);
+    if (ctx->k1out_host) (void)hipHostFree(ctx->k1out_host);
+    ctx->k1out_dev.release();
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -365,38 +381,49 @@ hipStream_t tfidf_ctx_stream(const tfidf_ctx* ctx) { return ctx->stream; }
 /* ------------------------------------------------------------------------------ */
 
 /* ---- the DF exchange (replaces MPI_Reduce(CustomReduce) + MPI_Bcast, TFIDF.c:209-222,
- * 291-326; SURVEY §8e's hash-owner partitioning).  Every rank enters it once per attempt,
- * also when its local stages failed or asked for a retry, so the ranks always agree:
+ * 291-326).  Every rank enters it once per attempt, also when its local stages failed or
+ * asked for a retry, so the ranks always agree:
  *   1. words(status, V): any error -> every rank returns an error (its own, or
- *      TFIDF_E_PEER); any retry -> every rank returns 1 and repeats the run in step.
- *   2. the send side is sized from this rank's V; words(allocation status) -> all fail
- *      together or none does.
- *   3. every term goes to its owner rank (a hash of its identity key): the ranks all-gather
- *      their per-owner counts, size the receive side (words(allocation status) again),
- *      send (key, local df) to the owners (all-to-all), each owner sums the df of equal
- *      keys in a hash table and sends every entry's global df back (all-to-all); global V
- *      = the owners' distinct keys summed (words).  Per rank that is ~V entries moved and
- *      aggregated — the all-gather union it replaces moved and radix-sorted max V x nranks
- *      keys on every rank (c4 on 8 shards: 91.8 ms exchange, 85 % of the step).  From here
- *      on no stage of the run returns "retry" (the stages after the exchange were checked
- *      against the main arena before step 1, in run_local); an error inside 3 aborts the
- *      transport, releasing the peers. */
+ *      TFIDF_E_PEER); any retry -> every rank returns 1 and repeats the run in step.  Every
+ *      rank learns every rank's V, which sizes everything after it.
+ *   2. one of two forms (the same results; TFIDF_XCHG=owner|dense forces one):
+ *      dense  (every rank's V <= DENSE_XCHG_MAXV: c2, c3, c5) — north_star's form: the
+ *             ranks' term keys are all-gathered (padded to the largest V), every rank numbers
+ *             the distinct keys identically (smallest gathered position), scatters its local
+ *             df into a dense vector over those numbers, and ONE all-reduce (sum) gives every
+ *             rank the global df; global V = the distinct keys.  One words agreement on the
+ *             allocations, one all-gather, one all-reduce.
+ *      owner  (larger V: c4) — SURVEY §8e's hash-owner partitioning: every term goes to an
+ *             owner rank (a hash of its key); the per-owner counts are all-gathered together
+ *             with each rank's allocation status (an allocation failure is agreed there, no
+ *             extra exchange), one all-to-all sends 20-byte (key, local df) records, each owner
+ *             sums equal keys in a hash table and one all-to-all returns the global df of each
+ *             record plus, per sender, the owner's distinct-key count (global V = their sum).
+ *             Per rank ~V entries move; the owner aggregates ~ΣV/R.
+ *   Global V stays on the device and is read with the run's final status (no host round
+ *   trip of its own).  From step 2 on no stage of the run returns "retry" (run_local checked
+ *   the post-exchange stages' scratch before step 1); an error inside a collective sequence
+ *   aborts the transport (releasing the peers), an agreed failure does not. */
 static uint64_t status_word(int rc) { return rc < 0 ? 0x100ull | (uint64_t)(-rc) : (uint64_t)rc; }
 
 static size_t scan_scratch(uint64_t n) { return (size_t)(n / 16) + 8192; }
 
-static int exchange_agree(tfidf_ctx* ctx, int local_rc, uint64_t v, uint64_t* maxv) {
+#define DENSE_XCHG_MAXV (1u << 17)
+
+/* words(status, v) over the ranks: 0 all fine, 1 retry (some rank asked), <0 an error (this
+ * rank's own, else TFIDF_E_PEER); vs (optional) = every rank's v */
+static int exchange_agree(tfidf_ctx* ctx, int local_rc, uint64_t v, std::vector<uint64_t>* vs) {
     Xport* xp = ctx->xp;
     std::vector<uint64_t> all(2 * (size_t)xp->nranks);
     const uint64_t mine[2] = {status_word(local_rc), v};
     const int rc = xp->words(mine, all.data(), ctx->stream);
     if (rc) return rc;
-    uint64_t worst = 0, mv = 1;
+    uint64_t worst = 0;
+    if (vs) vs->assign((size_t)xp->nranks, 0);
     for (int r = 0; r < xp->nranks; ++r) {
         worst = all[2 * r] > worst ? all[2 * r] : worst;
-        mv = all[2 * r + 1] > mv ? all[2 * r + 1] : mv;
+        if (vs) (*vs)[r] = all[2 * r + 1];
     }
-    if (maxv) *maxv = mv;
     if (worst >= 0x100) return local_rc < 0 ? local_rc : TFIDF_E_PEER;
     return worst ? 1 : 0;
 }
@@ -409,100 +436,155 @@ static int exchange_agree(tfidf_ctx* ctx, int local_rc, uint64_t v, uint64_t* ma
         if (l_ < 0) { HIPCHK(hipGetLastError()); return TFIDF_E_HIP; }      \
     } while (0)
 
-/* *agreed = true when the returned failure was decided by all ranks together (the
- * receive-side allocation agreement): nothing is left half-done in a collective then, and
- * the transport must not be aborted (tfidf.h: an agreed failure needs no action) */
-static int exchange_collective(tfidf_ctx* ctx, uint32_t V, bool* agreed) {
+static uint64_t table_cap(uint64_t n) {   /* load <= 2/3: short probe runs */
+    uint64_t t = 1024;
+    while (t < n + n / 2) t *= 2;
+    return t;
+}
+
+/* the hash-owner form (step 2 above); *agreed = true when the returned failure was decided
+ * by all ranks together (nothing half-done in a collective: the transport stays usable) */
+static int exchange_owner(tfidf_ctx* ctx, uint32_t V, const std::vector<uint64_t>& vs, bool* agreed) {
     hipStream_t s = ctx->stream;
     Xport* xp = ctx->xp;
     const int R = xp->nranks, me = xp->rank;
     unsigned long long* cnt = ctx->counters.as<unsigned long long>();
-    uint32_t* ocnt = ctx->x_cnt.as<uint32_t>();   /* [R] per-owner counts, [R] cursors, [R * R] all ranks' */
-    /* this rank's terms by rank, grouped by owner */
-    XCHK(launch_keys_by_rank(ctx->vkeys.as<uint4>(), ctx->slot_of_rank.as<uint32_t>(), V, ctx->x_mine.as<uint4>(), s));
-    XCHK(launch_owner_partition(ctx->x_mine.as<uint4>(), ctx->df_local.as<uint32_t>(), V, (uint32_t)R, ocnt, ocnt + R,
-                                ctx->x_skey.as<uint4>(), ctx->x_sdf.as<uint32_t>(), ctx->x_sidx.as<uint32_t>(), s));
-    int rc = xp->allgather(ocnt, ocnt + 2 * R, (size_t)R * 4, s);
+    uint64_t sumv = 0;
+    for (uint64_t x : vs) sumv += x;
+    /* everything sized here from the agreed V's: the receive side holds at most every
+     * rank's terms; a failure travels as the status word of the count row (below) */
+    int arc = 0;
+    auto ens = [&](DevBuf& b, size_t bytes) { if (!arc && b.ensure(bytes) != 0) arc = TFIDF_E_NOMEM; };
+    ens(ctx->x_mine, (size_t)V * 16 + 16);
+    ens(ctx->x_srec, (size_t)V * 20 + 20);
+    ens(ctx->x_sidx, (size_t)V * 4 + 4);
+    ens(ctx->x_back, ((size_t)V + R) * 4 + 4);
+    ens(ctx->x_rrec, sumv * 20 + 20);
+    ens(ctx->x_rslot, sumv * 4 + 4);
+    ens(ctx->x_reply, (sumv + R) * 4 + 4);
+    ens(ctx->x_tkey, table_cap(sumv) * 16);
+    ens(ctx->x_tdf, table_cap(sumv) * 4);
+    if (ctx->xnomem_rank == me) {   /* tests: an agreed allocation failure (once) */
+        ctx->xnomem_rank = -1;
+        arc = TFIDF_E_NOMEM;
+    }
+    /* x_cnt (sized in run_local): [R + 1] this rank's row (counts per owner + status),
+     * [R (R + 1)] all rows, [R + 1] soff, [R + 1] roff */
+    uint32_t* row = ctx->x_cnt.as<uint32_t>();
+    uint32_t* mat = row + (R + 1);
+    uint32_t* soff = mat + (size_t)R * (R + 1);
+    uint32_t* roff = soff + (R + 1);
+    uint32_t* cur = roff + (R + 1);
+    if (!arc) {
+        XCHK(launch_keys_by_rank(ctx->vkeys.as<uint4>(), ctx->slot_of_rank.as<uint32_t>(), V, ctx->x_mine.as<uint4>(), s));
+        XCHK(launch_owner_partition(ctx->x_mine.as<uint4>(), ctx->df_local.as<uint32_t>(), V, (uint32_t)R, row, cur,
+                                    ctx->x_srec.as<uint32_t>(), ctx->x_sidx.as<uint32_t>(), s));
+    } else {
+        HIPCHK(hipMemsetAsync(row, 0, (size_t)R * 4, s));
+    }
+    ctx->hpin[15] = (uint64_t)(uint32_t)arc;
+    HIPCHK(hipMemcpyAsync(row + R, ctx->hpin + 15, 4, hipMemcpyHostToDevice, s));
+    int rc = xp->allgather(row, mat, (size_t)(R + 1) * 4, s);
     if (rc) return rc;
-    std::vector<uint32_t> m((size_t)R * R);
-    HIPCHK(hipMemcpyAsync(m.data(), ocnt + 2 * R, (size_t)R * R * 4, hipMemcpyDeviceToHost, s));
+    std::vector<uint32_t> m((size_t)R * (R + 1));
+    HIPCHK(hipMemcpyAsync(m.data(), mat, m.size() * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    std::vector<uint64_t> scnt(R), rcnt(R);
+    int peer_fail = 0;
+    for (int p = 0; p < R; ++p)
+        if (m[(size_t)p * (R + 1) + R]) peer_fail = 1;
+    if (peer_fail) { *agreed = true; return arc ? arc : TFIDF_E_PEER; }
+    std::vector<uint64_t> scnt(R), rcnt(R), scnt1(R), rcnt1(R);
     uint64_t nrecv = 0, nsend = 0;
     for (int p = 0; p < R; ++p) {
-        scnt[p] = m[(size_t)me * R + p];
-        rcnt[p] = m[(size_t)p * R + me];
+        scnt[p] = m[(size_t)me * (R + 1) + p];
+        rcnt[p] = m[(size_t)p * (R + 1) + me];
+        scnt1[p] = scnt[p] + 1;   /* the replies carry one trailer word per owner */
+        rcnt1[p] = rcnt[p] + 1;
         nrecv += rcnt[p];
         nsend += scnt[p];
     }
-    if (nsend != V) return TFIDF_E_STATE;
+    if (nsend != V || nrecv > sumv) return TFIDF_E_STATE;
     if (ctx->xfail_rank == me) {   /* tests: a rank-local failure after a collective (once) */
         ctx->xfail_rank = -1;
         fprintf(stderr, "tfidf: rank %d: injected exchange failure (TFIDF_TEST_XFAIL_RANK)\n", me);
         return TFIDF_E_HIP;
     }
-    /* the owner side, sized from the received count; agreed like step 2 */
-    uint64_t tcap = 1024;   /* load <= 2/3: short probe runs, half the clear of a 2x table */
-    while (tcap < nrecv + nrecv / 2) tcap *= 2;
+    XCHK(launch_owner_offsets(mat, (uint32_t)R, (uint32_t)me, soff, roff, s));
+    /* (key, local df) records to the owners */
+    rc = xp->alltoallv(ctx->x_srec.p, scnt.data(), ctx->x_rrec.p, rcnt.data(), 20, s);
+    if (rc) return rc;
+    /* the owner: df summed per distinct key, every received record answered in order */
+    unsigned long long* used = cnt + 10;
+    XCHK(launch_owner_aggregate(ctx->x_rrec.as<uint32_t>(), nrecv, roff, (uint32_t)R, ctx->x_tkey.as<uint4>(),
+                                table_cap(nrecv), ctx->x_tdf.as<uint32_t>(), ctx->x_rslot.as<uint32_t>(),
+                                ctx->x_reply.as<uint32_t>(), used, (uint32_t*)(cnt + 3), s));
+    rc = xp->alltoallv(ctx->x_reply.p, rcnt1.data(), ctx->x_back.p, scnt1.data(), 4, s);
+    if (rc) return rc;
+    XCHK(launch_owner_back(ctx->x_back.as<uint32_t>(), soff, (uint32_t)R, ctx->x_sidx.as<uint32_t>(), V,
+                           ctx->df_global.as<uint32_t>(), (uint32_t*)(cnt + 12), s));
+    return 0;
+}
+
+/* the dense form (step 2 above) */
+static int exchange_dense(tfidf_ctx* ctx, uint32_t V, const std::vector<uint64_t>& vs, bool* agreed) {
+    hipStream_t s = ctx->stream;
+    Xport* xp = ctx->xp;
+    const int R = xp->nranks, me = xp->rank;
+    unsigned long long* cnt = ctx->counters.as<unsigned long long>();
+    uint64_t maxv = 1, sumv = 0;
+    for (uint64_t x : vs) { maxv = x > maxv ? x : maxv; sumv += x; }
+    const uint64_t n = (uint64_t)R * maxv;   /* gathered positions */
     int arc = 0;
     auto ens = [&](DevBuf& b, size_t bytes) { if (!arc && b.ensure(bytes) != 0) arc = TFIDF_E_NOMEM; };
-    ens(ctx->x_rkey, nrecv * 16 + 16);
-    ens(ctx->x_rdf, nrecv * 4 + 4);
-    ens(ctx->x_rslot, nrecv * 4 + 4);
-    ens(ctx->x_reply, nrecv * 4 + 4);
-    ens(ctx->x_tkey, tcap * 16);
-    ens(ctx->x_tdf, tcap * 4);
-    if (ctx->xnomem_rank == me) {   /* tests: an agreed receive-side allocation failure (once) */
+    ens(ctx->x_mine, maxv * 16 + 16);
+    ens(ctx->x_gkeys, n * 16 + 16);
+    ens(ctx->x_tkey, table_cap(sumv) * 16);
+    ens(ctx->x_tdf, table_cap(sumv) * 4);   /* the shared positions of the table's keys */
+    ens(ctx->x_pos, (size_t)V * 4 + 4);
+    ens(ctx->x_dense, n * 4 + 4);
+    if (ctx->xnomem_rank == me) {   /* tests: an agreed allocation failure (once) */
         ctx->xnomem_rank = -1;
         arc = TFIDF_E_NOMEM;
     }
-    rc = exchange_agree(ctx, arc, 0, nullptr);
+    int rc = exchange_agree(ctx, arc, 0, nullptr);
     if (rc == 1) rc = TFIDF_E_STATE;
     if (rc) { *agreed = true; return rc; }
-    /* (key, local df) to the owners */
-    rc = xp->alltoallv(ctx->x_skey.p, scnt.data(), ctx->x_rkey.p, rcnt.data(), 16, s);
-    if (!rc) rc = xp->alltoallv(ctx->x_sdf.p, scnt.data(), ctx->x_rdf.p, rcnt.data(), 4, s);
+    if (ctx->xfail_rank == me) {   /* tests: a rank-local failure after a collective (once) */
+        ctx->xfail_rank = -1;
+        fprintf(stderr, "tfidf: rank %d: injected exchange failure (TFIDF_TEST_XFAIL_RANK)\n", me);
+        return TFIDF_E_HIP;
+    }
+    uint4* mine = ctx->x_mine.as<uint4>();
+    HIPCHK(hipMemsetAsync(mine, 0xEE, maxv * 16, s));   /* padding: EMPTY keys */
+    XCHK(launch_keys_by_rank(ctx->vkeys.as<uint4>(), ctx->slot_of_rank.as<uint32_t>(), V, mine, s));
+    rc = xp->allgather(mine, ctx->x_gkeys.p, maxv * 16, s);
     if (rc) return rc;
-    /* the owner: df summed per distinct key, every received entry answered in order */
-    unsigned long long* used = cnt + 10;
-    XCHK(launch_owner_aggregate(ctx->x_rkey.as<uint4>(), ctx->x_rdf.as<uint32_t>(), nrecv, ctx->x_tkey.as<uint4>(), tcap,
-                                ctx->x_tdf.as<uint32_t>(), ctx->x_rslot.as<uint32_t>(), ctx->x_reply.as<uint32_t>(), used,
-                                (uint32_t*)(cnt + 3), s));
-    rc = xp->alltoallv(ctx->x_reply.p, rcnt.data(), ctx->x_back.p, scnt.data(), 4, s);
+    const uint64_t tcap = table_cap(sumv);
+    uint32_t* status = (uint32_t*)(cnt + 3);
+    XCHK(launch_dense_ids(ctx->x_gkeys.as<uint4>(), n, ctx->x_tkey.as<uint4>(), ctx->x_tdf.as<uint32_t>(), tcap, cnt + 10,
+                          status, s));
+    HIPCHK(hipMemsetAsync(ctx->x_dense.p, 0, n * 4, s));
+    XCHK(launch_dense_scatter(mine, ctx->df_local.as<uint32_t>(), V, ctx->x_tkey.as<uint4>(), tcap,
+                              ctx->x_tdf.as<uint32_t>(), ctx->x_pos.as<uint32_t>(), ctx->x_dense.as<uint32_t>(), status,
+                              s));
+    rc = xp->allreduce_u32(ctx->x_dense.as<uint32_t>(), n, s);
     if (rc) return rc;
-    XCHK(launch_owner_back(ctx->x_back.as<uint32_t>(), ctx->x_sidx.as<uint32_t>(), V, ctx->df_global.as<uint32_t>(), s));
-    /* global V: the owners' distinct keys */
-    ctx->hpin[10] = 0;
-    HIPCHK(hipMemcpyAsync(ctx->hpin + 10, used, 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    std::vector<uint64_t> all(2 * (size_t)R);
-    const uint64_t mine[2] = {ctx->hpin[10], 0};
-    rc = xp->words(mine, all.data(), s);
-    if (rc) return rc;
-    uint64_t vg = 0;
-    for (int p = 0; p < R; ++p) vg += all[2 * (size_t)p];
-    ctx->Vg = (uint32_t)vg;
+    XCHK(launch_dense_gather(ctx->x_dense.as<uint32_t>(), ctx->x_pos.as<uint32_t>(), V, ctx->df_global.as<uint32_t>(), s));
+    /* global V = the distinct keys (the same on every rank) */
+    HIPCHK(hipMemcpyAsync(cnt + 12, cnt + 10, 4, hipMemcpyDeviceToDevice, s));
     return 0;
 }
 
 static int exchange_df(tfidf_ctx* ctx, int local_rc, uint32_t V) {
-    int rc = exchange_agree(ctx, local_rc, V, nullptr);   /* step 1 */
+    std::vector<uint64_t> vs;
+    int rc = exchange_agree(ctx, local_rc, V, &vs);   /* step 1 */
     if (rc) return rc;
-    /* step 2: the send side */
-    const int R = ctx->xp->nranks;
-    int arc = 0;
-    auto ens = [&](DevBuf& b, size_t bytes) { if (!arc && b.ensure(bytes) != 0) arc = TFIDF_E_NOMEM; };
-    ens(ctx->x_mine, (size_t)V * 16 + 16);
-    ens(ctx->x_skey, (size_t)V * 16 + 16);
-    ens(ctx->x_sdf, (size_t)V * 4 + 4);
-    ens(ctx->x_sidx, (size_t)V * 4 + 4);
-    ens(ctx->x_back, (size_t)V * 4 + 4);
-    ens(ctx->x_cnt, ((size_t)2 * R + (size_t)R * R) * 4);
-    rc = exchange_agree(ctx, arc, 0, nullptr);   /* all allocated, or all fail */
-    if (rc == 1) rc = TFIDF_E_STATE;               /* no retry is ever requested here */
-    if (rc) return rc;
+    uint64_t maxv = 0;
+    for (uint64_t x : vs) maxv = x > maxv ? x : maxv;
+    const bool dense = ctx->xchg_mode == 2 || (ctx->xchg_mode == 0 && maxv <= DENSE_XCHG_MAXV);
+    ctx->last_dense = dense;
     bool agreed = false;
-    rc = exchange_collective(ctx, V, &agreed);     /* step 3 */
+    rc = dense ? exchange_dense(ctx, V, vs, &agreed) : exchange_owner(ctx, V, vs, &agreed);
     if (rc && rc != TFIDF_E_PEER && !agreed) ctx->xp->abort();
     return rc;
 }
@@ -520,6 +602,10 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     ctx->run_V = 0;
     mark(ctx, S_PREP);
     /* ---- buffers ---- */
+    if (ctx->xp) {   /* the exchange's count rows (sized before its agreement: see exchange_owner) */
+        const size_t R = (size_t)ctx->nranks;
+        ENSURE(ctx->x_cnt, ((R + 1) * (R + 4)) * 4);
+    }
     const uint64_t span = c.hi - c.lo;
     /* K1 variant: the slot-keyed kernels (tokcount_st / tokcount_vs) need a 16-byte aligned
      * corpus base; TFIDF_K1=general selects the general kernel (cross-checks).  The LDS-staged
@@ -527,10 +613,11 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
      * (config 4: ~1e7 terms, nearly every token a new (doc, term) pair) its bucketed LDS count
      * table runs full and the round-1 kernel is 2.3x faster (c4: 11.5 vs 26.2 ms) */
     const bool aligned = (((uintptr_t)c.bytes & 15u) == 0);
-    ctx->k1_vs = aligned && (ctx->k1_mode <= 1 || ctx->k1_mode >= 4);
+    ctx->k1_vs = aligned && ctx->k1_mode != 2;
     if (ctx->k1_vs && ctx->vcap > K1_VS_MAX_CAP) return TFIDF_E_CAPACITY;
-    ctx->k1_st = ctx->k1_vs && (ctx->k1_mode == 0 || ctx->k1_mode == 4) && ctx->vcap <= K1_ST_MAX_CAP;
-    const uint32_t cb = ctx->k1_st ? CHUNK_BYTES_ST : CHUNK_BYTES;
+    ctx->k1_st = ctx->k1_vs && ctx->k1_mode == 4 && ctx->vcap <= K1_ST_MAX_CAP;
+    ctx->k1_sl = ctx->k1_vs && (ctx->k1_mode == 0 || ctx->k1_mode == 3) && ctx->vcap <= K1_ST_MAX_CAP;
+    const uint32_t cb = (ctx->k1_st || ctx->k1_sl) ? CHUNK_BYTES_ST : CHUNK_BYTES;
     const uint64_t nchunks = span ? (span + cb - 1) / cb : 0;
     if (ctx->rec_cap == 0) ctx->rec_cap = span / 6 + 4096;
     if (ctx->part_cap == 0) ctx->part_cap = span / 64 + 4096;
@@ -580,11 +667,18 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     o.status = (uint32_t*)(cnt + 3);
     o.stamps = nullptr;
     if (ctx->stamps_on) {
-        ENSURE(ctx->stamps, 8 * K1_STAMP_WORDS);
-        HIPCHK(hipMemsetAsync(ctx->stamps.p, 0, 8 * K1_STAMP_WORDS, s));
+        ENSURE(ctx->stamps, 8 * K1_DEBUG_WORDS);
+        HIPCHK(hipMemsetAsync(ctx->stamps.p, 0, 8 * K1_DEBUG_WORDS, s));
         o.stamps = ctx->stamps.as<unsigned long long>();
     }
-    if (nchunks && ctx->k1_st)
+    if (nchunks && ctx->k1_sl) {
+        /* pinned source: the copy is stream-ordered before the launch, and the block is not
+         * rewritten before the next run (every run synchronises with the host after K1) */
+        *ctx->k1out_host = o;
+        HIPCHK(hipMemcpyAsync(ctx->k1out_dev.p, ctx->k1out_host, sizeof(K1Out), hipMemcpyHostToDevice, s));
+        LCHK(launch_tokcount_sl(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd,
+                                ctx->k1out_dev.as<K1Out>(), s));
+    } else if (nchunks && ctx->k1_st)
         LCHK(launch_tokcount_st(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
     else if (nchunks && ctx->k1_vs)
         LCHK(launch_tokcount_vs(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
@@ -943,12 +1037,15 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
     XCHK(launch_score_order(a, ar, s, ctx->stream2, ctx->ev_fork, ctx->ev_order));
     mark(ctx, S_NSTAGES);
     ctx->hpin[10] = 0;
+    ctx->hpin[14] = 0;
     HIPCHK(hipMemcpyAsync(ctx->hpin + 10, cnt + 3, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(ctx->hpin + 11, ctx->out_off.as<uint64_t>() + N, 8, hipMemcpyDeviceToHost, s));
+    if (ctx->xp) HIPCHK(hipMemcpyAsync(ctx->hpin + 14, cnt + 12, 4, hipMemcpyDeviceToHost, s));   /* global V */
     HIPCHK(hipStreamSynchronize(s));
     const uint32_t st_end = (uint32_t)ctx->hpin[10];
     const uint64_t P = ctx->hpin[11];
     ctx->npairs = P;
+    if (ctx->xp) ctx->Vg = (uint32_t)ctx->hpin[14];
     if (st_end & ST_BOUNDS) {
         fprintf(stderr, "tfidf: internal bounds check tripped (status 0x%x)\n", st_end);
         return TFIDF_E_STATE;
@@ -1076,7 +1173,7 @@ extern "C" int tfidf_run(tfidf_ctx* ctx, const tfidf_corpus* in) {
 extern "C" int tfidf_debug_k1_stamps(tfidf_ctx* ctx, uint64_t* out, int n) {
     if (!ctx || !out || n <= 0) return TFIDF_E_INVAL;
     if (!ctx->stamps_on || !ctx->stamps.p) return TFIDF_E_STATE;
-    int m = n < K1_STAMP_WORDS ? n : K1_STAMP_WORDS;
+    int m = n < K1_DEBUG_WORDS ? n : K1_DEBUG_WORDS;
     HIPCHK(hipMemcpy(out, ctx->stamps.p, 8 * (size_t)m, hipMemcpyDeviceToHost));
     return m;
 }
@@ -1155,7 +1252,7 @@ extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* out) {
     info->ms_tokcount = ctx->ms_stage[S_TOKCOUNT];
     for (int i = 0; i < S_NSTAGES; ++i) info->ms_stage[i] = ctx->ms_stage[i];
     info->nstages = S_NSTAGES;
-    info->flags = (ctx->k1_vs ? TFIDF_RUN_K1_VS : 0u) | (ctx->k1_st ? TFIDF_RUN_K1_ST : 0u);
+    info->flags = (ctx->k1_vs ? TFIDF_RUN_K1_VS : 0u) | (ctx->k1_st ? TFIDF_RUN_K1_ST : 0u) | (ctx->k1_sl ? TFIDF_RUN_K1_SL : 0u);
     info->device_allocs = g_dev_allocs.load(std::memory_order_relaxed);
     info->device_alloc_bytes = g_dev_alloc_bytes.load(std::memory_order_relaxed);
     full.size = want;

@@ -1968,11 +1968,12 @@ __global__ void k_owner_count(const uint4* __restrict__ keys, uint32_t V, uint32
     for (uint32_t o = threadIdx.x; o < R; o += blockDim.x)
         if (h[o]) atomicAdd(&cnt[o], h[o]);
 }
-/* the send buffer grouped by owner (order inside an owner's segment is free: the replies
- * come back in send order and send_idx maps them to term ranks).  cur[o] starts at 0. */
+/* The send buffer grouped by owner as 20-byte records (the 16-byte key and the local df:
+ * one all-to-all instead of two); order inside an owner's segment is free (the replies come
+ * back in send order, sidx maps them to term ranks).  cur[o] starts at 0. */
 __global__ void k_owner_scatter(const uint4* __restrict__ keys, const uint32_t* __restrict__ df, uint32_t V, uint32_t R,
-                                const uint32_t* __restrict__ cnt, uint32_t* __restrict__ cur, uint4* __restrict__ skey,
-                                uint32_t* __restrict__ sdf, uint32_t* __restrict__ sidx) {
+                                const uint32_t* __restrict__ cnt, uint32_t* __restrict__ cur, uint32_t* __restrict__ srec,
+                                uint32_t* __restrict__ sidx) {
     __shared__ uint32_t h[XO_MAXR], base[XO_MAXR], seg[XO_MAXR];
     /* segment starts: an exclusive scan of cnt (R <= 1024, serial per 256 entries is cheap) */
     if (threadIdx.x == 0) {
@@ -1997,8 +1998,9 @@ __global__ void k_owner_scatter(const uint4* __restrict__ keys, const uint32_t* 
         const uint32_t r = r0 + q * blockDim.x + threadIdx.x;
         if (own[q] == 0xFFFFFFFFu) continue;
         const uint32_t p = base[own[q]] + pos[q];
-        skey[p] = keys[r];
-        sdf[p] = df[r];
+        const uint4 k = keys[r];
+        uint32_t* d = srec + 5ull * p;
+        d[0] = k.x; d[1] = k.y; d[2] = k.z; d[3] = k.w; d[4] = df[r];
         sidx[p] = r;
     }
 }
@@ -2052,24 +2054,43 @@ __device__ uint32_t owner_insert(uint4* __restrict__ keys, uint64_t mask, uint64
     }
     return INVALID_SLOT;
 }
-/* every received key into the owner's table, its df added; rslot[i] = the entry's slot,
+/* find-only probe of a table filled by owner_insert (every key looked up is in it) */
+__device__ uint32_t owner_find(const uint4* __restrict__ keys, uint64_t mask, uint64_t klo, uint64_t khi) {
+    uint64_t h = key_hash(klo, khi) & mask;
+    for (uint64_t probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
+        const uint4 s = keys[h];
+        const uint64_t lo = ((uint64_t)s.y << 32) | s.x, hi = ((uint64_t)s.w << 32) | s.z;
+        if (hi == khi && lo == klo) return (uint32_t)h;
+        if (hi == KEY_EMPTY_HI) break;
+    }
+    return INVALID_SLOT;
+}
+/* the segment of a position: last p with off[p] <= i (off: R + 1 prefix offsets) */
+__device__ __forceinline__ uint32_t seg_of(const uint32_t* __restrict__ off, uint32_t R, uint64_t i) {
+    uint32_t lo = 0, hi = R;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (off[mid] <= i) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+/* every received record into the owner's table, its df added; rslot[i] = the record's slot,
  * *used += distinct keys (one claim each) */
-__global__ void k_owner_insert(const uint4* __restrict__ rkey, const uint32_t* __restrict__ rdf, uint64_t n,
-                               uint4* __restrict__ tkey, uint64_t tmask, uint32_t* __restrict__ tdf,
-                               uint32_t* __restrict__ rslot, unsigned long long* __restrict__ used,
-                               uint32_t* __restrict__ status) {
+__global__ void k_owner_insert(const uint32_t* __restrict__ rrec, uint64_t n, uint4* __restrict__ tkey, uint64_t tmask,
+                               uint32_t* __restrict__ tdf, uint32_t* __restrict__ rslot,
+                               unsigned long long* __restrict__ used, uint32_t* __restrict__ status) {
     for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < n; i0 += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t i = i0 + threadIdx.x;
         bool claimed = false;
         if (i < n) {
-            const uint4 k = rkey[i];
-            const uint32_t sl = owner_insert(tkey, tmask, ((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z, &claimed,
-                                             status);
+            const uint32_t* r = rrec + 5 * i;
+            const uint32_t sl = owner_insert(tkey, tmask, ((uint64_t)r[1] << 32) | r[0], ((uint64_t)r[3] << 32) | r[2],
+                                             &claimed, status);
             if (sl == INVALID_SLOT) {   /* not reachable at the table's load (or a bounded wait gave up) */
                 atomicOr(status, ST_BOUNDS);
                 rslot[i] = 0u;
             } else {
-                atomicAdd(&tdf[sl], rdf[i]);
+                atomicAdd(&tdf[sl], r[4]);
                 rslot[i] = sl;
             }
         }
@@ -2077,45 +2098,163 @@ __global__ void k_owner_insert(const uint4* __restrict__ rkey, const uint32_t* _
         if ((threadIdx.x & 63) == 0 && c) atomicAdd(used, (unsigned long long)c);
     }
 }
-/* distinct keys the owner holds (its share of the global V) and the replies */
-__global__ void k_owner_reply(const uint32_t* __restrict__ rslot, uint64_t n, const uint32_t* __restrict__ tdf,
+/* The replies, one segment per sender p: the summed df of each of its records in the order
+ * received, then one trailer word = this owner's distinct keys (its share of the global V),
+ * so every sender learns global V from the same all-to-all (reply[roff[p] + p + i]). */
+__global__ void k_owner_reply(const uint32_t* __restrict__ rslot, uint64_t n, const uint32_t* __restrict__ roff, uint32_t R,
+                              const uint32_t* __restrict__ tdf, const unsigned long long* __restrict__ used,
                               uint32_t* __restrict__ reply) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) reply[i] = tdf[rslot[i]];
+    if (i < n) reply[i + seg_of(roff, R, i)] = tdf[rslot[i]];
+    if (i < R) reply[(uint64_t)roff[i + 1] + i] = (uint32_t)*used;
 }
-/* sender side: the global df of each sent term back at its rank */
-__global__ void k_owner_back(const uint32_t* __restrict__ back, const uint32_t* __restrict__ sidx, uint32_t V,
-                             uint32_t* __restrict__ df_global) {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p < V) df_global[sidx[p]] = back[p];
+/* sender side: the global df of each sent term back at its rank; global V = the owners'
+ * trailers summed (back[soff[p] + p + i], trailer of owner p at soff[p + 1] + p) */
+__global__ void k_owner_back(const uint32_t* __restrict__ back, const uint32_t* __restrict__ soff, uint32_t R,
+                             const uint32_t* __restrict__ sidx, uint32_t V, uint32_t* __restrict__ df_global,
+                             uint32_t* __restrict__ vg) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < V) df_global[sidx[j]] = back[j + seg_of(soff, R, j)];
+    if (blockIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t p = threadIdx.x; p < R; p += blockDim.x) t += back[(uint64_t)soff[p + 1] + p];
+        t = wave_sum(t);
+        __shared__ uint32_t ws[NT / 64];
+        if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = t;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t a = 0;
+            for (int w = 0; w < NT / 64; ++w) a += ws[w];
+            *vg = a;
+        }
+    }
+}
+/* prefix offsets of this rank's send (soff: its row of the all-gathered count matrix) and
+ * receive (roff: its column) segments; m holds R rows of R counts + 1 status word */
+__global__ void k_owner_offsets(const uint32_t* __restrict__ m, uint32_t R, uint32_t me, uint32_t* __restrict__ soff,
+                                uint32_t* __restrict__ roff) {
+    if (threadIdx.x == 0) {
+        uint32_t a = 0, b = 0;
+        for (uint32_t p = 0; p < R; ++p) {
+            soff[p] = a;
+            roff[p] = b;
+            a += m[(uint64_t)me * (R + 1) + p];
+            b += m[(uint64_t)p * (R + 1) + me];
+        }
+        soff[R] = a;
+        roff[R] = b;
+    }
 }
 int launch_owner_partition(const uint4* keys, const uint32_t* df, uint32_t V, uint32_t R, uint32_t* cnt, uint32_t* cur,
-                           uint4* skey, uint32_t* sdf, uint32_t* sidx, hipStream_t s) {
+                           uint32_t* srec, uint32_t* sidx, hipStream_t s) {
     if (R < 1 || R > XO_MAXR) return -3;
     if (hipMemsetAsync(cnt, 0, (size_t)R * 4, s) != hipSuccess || hipMemsetAsync(cur, 0, (size_t)R * 4, s) != hipSuccess)
         return -1;
     if (!V) return 0;
     const uint32_t nb = (V + NT * 8 - 1) / (NT * 8);
     k_owner_count<<<nb < 1024 ? nb : 1024, NT, 0, s>>>(keys, V, R, cnt);
-    k_owner_scatter<<<nb, NT, 0, s>>>(keys, df, V, R, cnt, cur, skey, sdf, sidx);
+    k_owner_scatter<<<nb, NT, 0, s>>>(keys, df, V, R, cnt, cur, srec, sidx);
     return ok();
 }
-int launch_owner_aggregate(const uint4* rkey, const uint32_t* rdf, uint64_t n, uint4* tkey, uint64_t tcap, uint32_t* tdf,
-                           uint32_t* rslot, uint32_t* reply, unsigned long long* used, uint32_t* status, hipStream_t s) {
+int launch_owner_offsets(const uint32_t* m, uint32_t R, uint32_t me, uint32_t* soff, uint32_t* roff, hipStream_t s) {
+    k_owner_offsets<<<1, 64, 0, s>>>(m, R, me, soff, roff);
+    return ok();
+}
+int launch_owner_aggregate(const uint32_t* rrec, uint64_t n, const uint32_t* roff, uint32_t R, uint4* tkey, uint64_t tcap,
+                           uint32_t* tdf, uint32_t* rslot, uint32_t* reply, unsigned long long* used, uint32_t* status,
+                           hipStream_t s) {
     if (hipMemsetAsync(tkey, 0xEE, tcap * 16, s) != hipSuccess || hipMemsetAsync(tdf, 0, tcap * 4, s) != hipSuccess ||
         hipMemsetAsync(used, 0, 8, s) != hipSuccess)
         return -1;
     if (n) {
         const uint64_t nb = (n + NT - 1) / NT;
-        k_owner_insert<<<(unsigned)(nb < 8192 ? nb : 8192), NT, 0, s>>>(rkey, rdf, n, tkey, tcap - 1, tdf, rslot, used,
-                                                                        status);
-        k_owner_reply<<<grid_for(n), NT, 0, s>>>(rslot, n, tdf, reply);
+        k_owner_insert<<<(unsigned)(nb < 8192 ? nb : 8192), NT, 0, s>>>(rrec, n, tkey, tcap - 1, tdf, rslot, used, status);
+    }
+    const uint64_t m = n > R ? n : R;
+    k_owner_reply<<<grid_for(m), NT, 0, s>>>(rslot, n, roff, R, tdf, used, reply);
+    return ok();
+}
+int launch_owner_back(const uint32_t* back, const uint32_t* soff, uint32_t R, const uint32_t* sidx, uint32_t V,
+                      uint32_t* df_global, uint32_t* vg, hipStream_t s) {
+    k_owner_back<<<grid_for(V > 1 ? V : 1), NT, 0, s>>>(back, soff, R, sidx, V, df_global, vg);
+    return ok();
+}
+
+/* ---- the dense DF exchange (north_star's form: per-rank DF vectors over one shared
+ * vocabulary, summed by an all-reduce).  Every rank all-gathers the ranks' term keys
+ * (each rank's list padded to the largest V with EMPTY keys), inserts them all into a table
+ * and numbers each distinct key by the smallest position it has in the gathered list: the
+ * same numbering on every rank with no further exchange.  Each rank scatters its local df
+ * into a dense vector over those positions, the vectors are all-reduced (sum), and each rank
+ * reads back its terms' global df; global V = the table's distinct keys. */
+__global__ void k_dense_insert(const uint4* __restrict__ gkeys, uint64_t n, uint4* __restrict__ tkey, uint64_t tmask,
+                               uint32_t* __restrict__ tpos, unsigned long long* __restrict__ used,
+                               uint32_t* __restrict__ status) {
+    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < n; i0 += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = i0 + threadIdx.x;
+        bool claimed = false;
+        if (i < n) {
+            const uint4 k = gkeys[i];
+            const uint64_t hi = ((uint64_t)k.w << 32) | k.z;
+            if (hi != KEY_EMPTY_HI) {   /* padding */
+                const uint32_t sl = owner_insert(tkey, tmask, ((uint64_t)k.y << 32) | k.x, hi, &claimed, status);
+                if (sl == INVALID_SLOT) atomicOr(status, ST_BOUNDS);
+                else atomicMin(&tpos[sl], (uint32_t)i);
+            }
+        }
+        const uint32_t c = (uint32_t)__popcll(__ballot(claimed));
+        if ((threadIdx.x & 63) == 0 && c) atomicAdd(used, (unsigned long long)c);
+    }
+}
+__global__ void k_dense_scatter(const uint4* __restrict__ mine, const uint32_t* __restrict__ df, uint32_t V,
+                                const uint4* __restrict__ tkey, uint64_t tmask, const uint32_t* __restrict__ tpos,
+                                uint32_t* __restrict__ pos, uint32_t* __restrict__ dense, uint32_t* __restrict__ status) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= V) return;
+    const uint4 k = mine[r];
+    const uint32_t sl = owner_find(tkey, tmask, ((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z);
+    if (sl == INVALID_SLOT) { atomicOr(status, ST_BOUNDS); pos[r] = 0; return; }
+    const uint32_t p = tpos[sl];
+    pos[r] = p;
+    dense[p] = df[r];   /* one term per position: the keys of a rank are distinct */
+}
+__global__ void k_dense_gather(const uint32_t* __restrict__ dense, const uint32_t* __restrict__ pos, uint32_t V,
+                               uint32_t* __restrict__ df_global) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < V) df_global[r] = dense[pos[r]];
+}
+__global__ void k_sum_rows_u32(const uint32_t* __restrict__ rows, uint32_t nrows, uint64_t n, uint32_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t t = 0;
+    for (uint32_t r = 0; r < nrows; ++r) t += rows[(uint64_t)r * n + i];
+    out[i] = t;
+}
+int launch_sum_rows_u32(const uint32_t* rows, uint32_t nrows, uint64_t n, uint32_t* out, hipStream_t s) {
+    if (!n) return 0;
+    k_sum_rows_u32<<<grid_for(n), NT, 0, s>>>(rows, nrows, n, out);
+    return ok();
+}
+int launch_dense_ids(const uint4* gkeys, uint64_t n, uint4* tkey, uint32_t* tpos, uint64_t tcap,
+                     unsigned long long* used, uint32_t* status, hipStream_t s) {
+    if (hipMemsetAsync(tkey, 0xEE, tcap * 16, s) != hipSuccess || hipMemsetAsync(tpos, 0xFF, tcap * 4, s) != hipSuccess ||
+        hipMemsetAsync(used, 0, 8, s) != hipSuccess)
+        return -1;
+    if (n) {
+        const uint64_t nb = (n + NT - 1) / NT;
+        k_dense_insert<<<(unsigned)(nb < 8192 ? nb : 8192), NT, 0, s>>>(gkeys, n, tkey, tcap - 1, tpos, used, status);
     }
     return ok();
 }
-int launch_owner_back(const uint32_t* back, const uint32_t* sidx, uint32_t V, uint32_t* df_global, hipStream_t s) {
+int launch_dense_scatter(const uint4* mine, const uint32_t* df, uint32_t V, const uint4* tkey, uint64_t tcap,
+                         const uint32_t* tpos, uint32_t* pos, uint32_t* dense, uint32_t* status, hipStream_t s) {
     if (!V) return 0;
-    k_owner_back<<<grid_for(V), NT, 0, s>>>(back, sidx, V, df_global);
+    k_dense_scatter<<<grid_for(V), NT, 0, s>>>(mine, df, V, tkey, tcap - 1, tpos, pos, dense, status);
+    return ok();
+}
+int launch_dense_gather(const uint32_t* dense, const uint32_t* pos, uint32_t V, uint32_t* df_global, hipStream_t s) {
+    if (!V) return 0;
+    k_dense_gather<<<grid_for(V), NT, 0, s>>>(dense, pos, V, df_global);
     return ok();
 }
 

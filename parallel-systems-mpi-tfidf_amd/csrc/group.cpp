@@ -139,6 +139,9 @@ struct RcclXport final : Xport {
             return r != ncclSuccess ? r : e;
         });
     }
+    int allreduce_u32(uint32_t* buf, size_t n, hipStream_t s) override {
+        return enqueue([&](ncclComm_t c) { return ncclAllReduce(buf, buf, n, ncclUint32, ncclSum, c, s); });
+    }
     void abort() override {
         if (clique) clique->abort_all();
         else if (own) { (void)ncclCommAbort(own); own = nullptr; }
@@ -245,6 +248,41 @@ struct LocalXport final : Xport {
         if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = TFIDF_E_HIP;
         if (rc) { abort(); return rc; }
         if (!hub->barrier()) return TFIDF_E_PEER;   /* no send buffer is reused before all copied */
+        return TFIDF_OK;
+    }
+    /* every rank copies all ranks' vectors into its staging area (after a barrier: all are
+     * complete), then (after a second barrier: nobody overwrites a vector still being read)
+     * sums them into its own */
+    uint32_t* stage = nullptr;
+    size_t stage_n = 0;
+    ~LocalXport() override {
+        if (stage) (void)hipFree(stage);
+    }
+    int allreduce_u32(uint32_t* buf, size_t n, hipStream_t s) override {
+        if (!n) return hub->barrier() && hub->barrier() && hub->barrier() ? TFIDF_OK : TFIDF_E_PEER;
+        if (stage_n < n * (size_t)nranks) {
+            if (stage) (void)hipFree(stage);
+            stage = nullptr;
+            stage_n = 0;
+            if (tfidf_dev_malloc((void**)&stage, n * (size_t)nranks * 4) != hipSuccess) { abort(); return TFIDF_E_NOMEM; }
+            stage_n = n * (size_t)nranks;
+        }
+        if (hipStreamSynchronize(s) != hipSuccess) { abort(); return TFIDF_E_HIP; }
+        hub->ptr[rank] = buf;
+        if (!hub->barrier()) return TFIDF_E_PEER;
+        int rc = TFIDF_OK;
+        for (int r = 0; r < nranks && !rc; ++r) {
+            const hipError_t e = hub->dev[r] == device
+                ? hipMemcpyAsync(stage + (size_t)r * n, hub->ptr[r], n * 4, hipMemcpyDeviceToDevice, s)
+                : hipMemcpyPeerAsync(stage + (size_t)r * n, device, hub->ptr[r], hub->dev[r], n * 4, s);
+            if (e != hipSuccess) rc = TFIDF_E_HIP;
+        }
+        if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = TFIDF_E_HIP;
+        if (rc) { abort(); return rc; }
+        if (!hub->barrier()) return TFIDF_E_PEER;   /* every vector read before any is overwritten */
+        if (launch_sum_rows_u32(stage, (uint32_t)nranks, n, buf, s)) { abort(); return TFIDF_E_HIP; }
+        if (hipStreamSynchronize(s) != hipSuccess) { abort(); return TFIDF_E_HIP; }
+        if (!hub->barrier()) return TFIDF_E_PEER;
         return TFIDF_OK;
     }
     void abort() override { hub->poison(); }

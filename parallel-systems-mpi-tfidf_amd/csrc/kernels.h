@@ -82,6 +82,7 @@ struct K1Out {
 #define K1_NSTAMP 17
 #define K1_NCOUNT 4   /* segments, flushes, tokens taking the full probe, probe iterations */
 #define K1_STAMP_WORDS (K1_NSTAMP + 1 + K1_NCOUNT)
+#define K1_DEBUG_WORDS 16384   /* diagnostic builds: the stamps buffer's size in u64 words */
 
 /* K0: chunk boundaries; chunk_start has nchunks+1 entries, chunk_doc nchunks */
 int launch_plan_chunks(const CorpusDev& c, uint64_t nchunks, uint32_t chunk_bytes, uint64_t* chunk_start,
@@ -102,6 +103,11 @@ int launch_tokcount_vs(const CorpusDev& c, const uint64_t* chunk_start, const ui
 #define K1_VS_MAX_CAP (1ull << 28)
 
 #define K1_ST_MAX_CAP (1ull << 22)   /* tokcount_st up to this vocabulary capacity, tokcount_vs beyond */
+/* K1 default (tokcount_sl.hip): one workgroup per chunk, straight-line rounds; the output
+ * block is read from device memory (o_dev: a K1Out the engine copies there per run).
+ * 16-byte aligned corpus base; -3 when the vocabulary exceeds K1_ST_MAX_CAP slots */
+int launch_tokcount_sl(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc, uint64_t c0,
+                       uint64_t c1, const VocabDev& v, const K1Out* o_dev, hipStream_t s);
 
 
 /* vocabulary finalisation */
@@ -190,14 +196,30 @@ int launch_score_order(const K5Args& a, Arena& ar, hipStream_t s, hipStream_t s2
 
 /* multi-GPU vocabulary agreement */
 int launch_keys_by_rank(const uint4* vkeys, const uint32_t* slot_of_rank, uint32_t V, uint4* out, hipStream_t s);
-/* hash-owner DF exchange: partition this rank's terms by owner (cnt[R] = terms per owner;
- * cur[R] scratch), aggregate the received entries on the owner (table of tcap = 2^k >= 1.5 n slots;
- * *used = distinct keys), write the returned global df at the term ranks */
+/* hash-owner DF exchange: partition this rank's terms by owner into 20-byte (key, df)
+ * records (cnt[R] = terms per owner, cur[R] scratch); the send/receive segment offsets from
+ * the all-gathered count matrix m (R rows of R counts + 1 status word); aggregate the
+ * received records on the owner (table of tcap = 2^k >= 1.5 n slots; *used = distinct keys)
+ * and reply per sender (segment + one trailer word = *used); write the returned global df at
+ * the term ranks and global V (the trailers summed) to *vg */
 int launch_owner_partition(const uint4* keys, const uint32_t* df, uint32_t V, uint32_t R, uint32_t* cnt, uint32_t* cur,
-                           uint4* skey, uint32_t* sdf, uint32_t* sidx, hipStream_t s);
-int launch_owner_aggregate(const uint4* rkey, const uint32_t* rdf, uint64_t n, uint4* tkey, uint64_t tcap, uint32_t* tdf,
-                           uint32_t* rslot, uint32_t* reply, unsigned long long* used, uint32_t* status, hipStream_t s);
-int launch_owner_back(const uint32_t* back, const uint32_t* sidx, uint32_t V, uint32_t* df_global, hipStream_t s);
+                           uint32_t* srec, uint32_t* sidx, hipStream_t s);
+int launch_owner_offsets(const uint32_t* m, uint32_t R, uint32_t me, uint32_t* soff, uint32_t* roff, hipStream_t s);
+int launch_owner_aggregate(const uint32_t* rrec, uint64_t n, const uint32_t* roff, uint32_t R, uint4* tkey, uint64_t tcap,
+                           uint32_t* tdf, uint32_t* rslot, uint32_t* reply, unsigned long long* used, uint32_t* status,
+                           hipStream_t s);
+int launch_owner_back(const uint32_t* back, const uint32_t* soff, uint32_t R, const uint32_t* sidx, uint32_t V,
+                      uint32_t* df_global, uint32_t* vg, hipStream_t s);
+/* out[i] = sum of rows[r * n + i] over r < nrows (the in-process transport's all-reduce) */
+int launch_sum_rows_u32(const uint32_t* rows, uint32_t nrows, uint64_t n, uint32_t* out, hipStream_t s);
+/* dense DF exchange (small vocabularies): gathered keys -> shared positions (tpos[slot] =
+ * smallest gathered position of the key, *used = distinct keys), this rank's df scattered
+ * over them (pos[r] = position of term rank r), and read back after the all-reduce */
+int launch_dense_ids(const uint4* gkeys, uint64_t n, uint4* tkey, uint32_t* tpos, uint64_t tcap,
+                     unsigned long long* used, uint32_t* status, hipStream_t s);
+int launch_dense_scatter(const uint4* mine, const uint32_t* df, uint32_t V, const uint4* tkey, uint64_t tcap,
+                         const uint32_t* tpos, uint32_t* pos, uint32_t* dense, uint32_t* status, hipStream_t s);
+int launch_dense_gather(const uint32_t* dense, const uint32_t* pos, uint32_t V, uint32_t* df_global, hipStream_t s);
 
 /* synthetic corpus generation on the device */
 struct SynSpecDev;

@@ -795,8 +795,8 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_st(CorpusDev c, cons
                             q.k2 = __builtin_amdgcn_perm(0x09090909u, raw.z, sl.z);
                             q.k3 = __builtin_amdgcn_perm(0x09090909u, raw.w, sl.w);
                             q.hv = q.kind == 1u ? (uint32_t)(key_hash(((uint64_t)q.k1 << 32) | q.k0,
-                                                                      ((uint64_t)q.k3 << 32) | q.k2) & v.mask)
-                                                : 0u;
+                                                                      ((uint64_t)q.k3 << 32) | q.k2) & v.mask & ~1ull)
+                                                : 0u;   /* even home slot (dev_vocab.h) */
                             /* the home slot and the next one: a key displaced by one slot
                              * (linear probing) resolves without a dependent load */
                             q.s4 = gload(v.keys + q.hv);

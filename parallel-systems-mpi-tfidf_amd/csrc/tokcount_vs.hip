@@ -575,7 +575,7 @@ __global__ __launch_bounds__(NT, K1_WAVES_PER_SIMD) void k_tokcount_vs(CorpusDev
                                 uint32_t rel = wr;
                                 for (uint32_t k = wr + 1; k < kend; ++k) rel += uni64(S.gdoc[k]) <= q.ap ? 1u : 0u;
                                 q.rel = rel;
-                                q.hv = q.kind == 1u ? (uint32_t)(key_hash(q.klo, q.khi) & v.mask) : 0u;
+                                q.hv = q.kind == 1u ? (uint32_t)(key_hash(q.klo, q.khi) & v.mask & ~1ull) : 0u;   /* even home (dev_vocab.h) */
                                 /* the home slot and the next one: a key displaced by one slot
                                  * (linear probing) still resolves without a dependent load */
                                 q.s4 = v.keys[q.hv];

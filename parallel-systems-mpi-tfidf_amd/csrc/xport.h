@@ -5,7 +5,7 @@
  * (TFIDF.c:209-222,291-326) between OS processes.  Here a context (one GPU shard) talks
  * to its peers through an Xport:
  *
- *   RcclXport   ncclAllGather / grouped ncclSend-ncclRecv over xGMI: one
+ *   RcclXport   ncclAllGather / ncclAllReduce / grouped ncclSend-ncclRecv over xGMI: one
  *               communicator rank per GPU,
  *               either one process per GPU (tfidf_comm_init, torch.distributed launch) or
  *               one process driving every GPU (tfidf_group_open, ncclCommInitAll).
@@ -41,6 +41,8 @@ struct Xport {
      * (rcnt[p] must equal peer p's scnt[rank]) */
     virtual int alltoallv(const void* send, const uint64_t* scnt, void* recv, const uint64_t* rcnt, size_t eb,
                           hipStream_t s) = 0;
+    /* device all-reduce (sum) of n u32 in place: the dense DF exchange's one collective */
+    virtual int allreduce_u32(uint32_t* buf, size_t n, hipStream_t s) = 0;
     /* a rank failed between collectives: release the peers (they return errors) */
     virtual void abort() = 0;
     virtual const char* name() const = 0;

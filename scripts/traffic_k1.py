@@ -20,7 +20,7 @@ import statistics
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SOURCES = {"k_tokcount_st": "tokcount_st.hip", "k_tokcount_vs": "tokcount_vs.hip", "k_tokcount": "tokcount.hip"}
+SOURCES = {"k_tokcount_sl": "tokcount_sl.hip", "k_tokcount_st": "tokcount_st.hip", "k_tokcount_vs": "tokcount_vs.hip", "k_tokcount": "tokcount.hip"}
 
 
 def k1_source_sha(kernel) -> str:
@@ -30,7 +30,7 @@ def k1_source_sha(kernel) -> str:
 
 def kernel_of(name):
     """k_tokcount_st / k_tokcount_vs / k_tokcount from a demangled kernel name"""
-    for k in ("k_tokcount_st", "k_tokcount_vs"):
+    for k in ("k_tokcount_sl", "k_tokcount_st", "k_tokcount_vs"):
         if k in name:
             return k
     return "k_tokcount" if "k_tokcount(" in name else None

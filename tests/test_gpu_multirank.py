@@ -66,9 +66,13 @@ def _run_group(shards, K, **kw):
     return texts, res, infos
 
 
+@pytest.mark.parametrize("xchg", ["dense", "owner"])
 @pytest.mark.parametrize("cfg,scale,K", [("c2", 0.003, 2), ("c2", 0.003, 3), ("c5", 0.0005, 2), ("c5", 0.0005, 3),
                                          ("c4", 0.001, 2), ("c2", 0.003, 5)])
-def test_group_shards_equal_single_rank_oracle(cfg, scale, K):
+def test_group_shards_equal_single_rank_oracle(cfg, scale, K, xchg, monkeypatch):
+    """Both forms of the DF exchange (engine.cpp): the dense all-reduce over shared
+    positions (the default up to 2^17 terms per rank) and the hash-owner all-to-all."""
+    monkeypatch.setenv("TFIDF_XCHG", xchg)   # read by tfidf_open
     shards = _shards(cfg, scale, K)
     ora = _full(cfg, scale)
     texts, res, infos = _run_group(shards, K)
@@ -137,8 +141,9 @@ def test_group_error_releases_peers():
         g.run_host(_shards("c2", 0.001, 2))
 
 
+@pytest.mark.parametrize("xchg", ["dense", "owner"])
 @pytest.mark.parametrize("failing", [0, 1, 2])
-def test_exchange_failure_after_allgather_aborts_peers(failing, monkeypatch):
+def test_exchange_failure_after_allgather_aborts_peers(failing, xchg, monkeypatch):
     """A rank-local failure INSIDE the exchange (after the per-owner count all-gather, past
     the agreement: TFIDF_TEST_XFAIL_RANK) aborts the transport; the peers, already on their
     way into the next collective, return TFIDF_E_PEER instead of waiting, the group reports the
@@ -146,6 +151,7 @@ def test_exchange_failure_after_allgather_aborts_peers(failing, monkeypatch):
     hub is reset).  The same engine path (exchange_df -> Xport::abort) aborts every RCCL
     communicator of a clique."""
     shards = _shards("c2", 0.001, 3)
+    monkeypatch.setenv("TFIDF_XCHG", xchg)
     monkeypatch.setenv("TFIDF_TEST_XFAIL_RANK", str(failing))   # read by tfidf_open; fires once
     with tfidf_abi.Group(3, devices=[0, 0, 0]) as g:
         with pytest.raises(tfidf_abi.TfidfError) as ei:
@@ -156,13 +162,15 @@ def test_exchange_failure_after_allgather_aborts_peers(failing, monkeypatch):
         assert b"".join(g.ranks[r].text() for r in range(3)) == ora["output_txt"]
 
 
+@pytest.mark.parametrize("xchg", ["dense", "owner"])
 @pytest.mark.parametrize("failing", [0, 2])
-def test_exchange_agreed_alloc_failure_keeps_group_usable(failing, monkeypatch):
+def test_exchange_agreed_alloc_failure_keeps_group_usable(failing, xchg, monkeypatch):
     """A receive-side allocation failure inside the exchange is agreed between the ranks
     (TFIDF_TEST_XNOMEM_RANK): every rank returns an error before the (key, df) all-to-all,
     the transport is NOT aborted (tfidf.h: an agreed failure needs no action from the
     caller), and the next run of the same group succeeds with the oracle's output."""
     shards = _shards("c2", 0.001, 3)
+    monkeypatch.setenv("TFIDF_XCHG", xchg)
     monkeypatch.setenv("TFIDF_TEST_XNOMEM_RANK", str(failing))   # read by tfidf_open; fires once
     with tfidf_abi.Group(3, devices=[0, 0, 0]) as g:
         with pytest.raises(tfidf_abi.TfidfError) as ei:
@@ -173,10 +181,12 @@ def test_exchange_agreed_alloc_failure_keeps_group_usable(failing, monkeypatch):
         assert b"".join(g.ranks[r].text() for r in range(3)) == ora["output_txt"]
 
 
-def test_rccl_single_rank_runs_the_exchange():
-    """A 1-rank RCCL communicator: exchange_df runs (agreement, the count ncclAllGather, the
-    self all-to-all by ncclSend / ncclRecv, the owner aggregation) and the results are
-    unchanged."""
+@pytest.mark.parametrize("xchg", ["dense", "owner"])
+def test_rccl_single_rank_runs_the_exchange(xchg, monkeypatch):
+    """A 1-rank RCCL communicator: exchange_df runs (agreement; dense: the key ncclAllGather
+    and the DF ncclAllReduce; owner: the count ncclAllGather, the self all-to-alls by
+    ncclSend / ncclRecv, the owner aggregation) and the results are unchanged."""
+    monkeypatch.setenv("TFIDF_XCHG", xchg)
     p = tfidf_configs.plan("c2", scale=0.002)
     data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
     with tfidf_abi.Engine(0) as e:

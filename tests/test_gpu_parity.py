@@ -234,13 +234,13 @@ def test_full_config_properties(cfg):
 
 @pytest.mark.parametrize("cfg,scale", [("c2", 0.002), ("c5", 0.0005), ("c4", 0.001)])
 def test_k1_variants_agree(cfg, scale):
-    """The default K1 (k_tokcount_st up to 4M vocabulary slots, k_tokcount_vs beyond), the
-    round-1 slot-keyed K1 (TFIDF_K1=vs) and the general K1 (unaligned corpora) give identical
-    results, equal to the oracle."""
+    """The default K1 (k_tokcount_sl up to 4M vocabulary slots, k_tokcount_vs beyond), the
+    persistent LDS-staged K1 (TFIDF_K1=st), the round-1 slot-keyed K1 (TFIDF_K1=vs) and the
+    general K1 (unaligned corpora) give identical results, equal to the oracle."""
     p = tfidf_configs.plan(cfg, scale=scale)
     data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
     outs = []
-    modes = [("auto", 2), ("st", 2), ("vs", 2), ("general", 0)]
+    modes = [("auto", 2), ("sl", 2), ("st", 2), ("vs", 2), ("general", 0)]
     for mode, flag in modes:
         os.environ["TFIDF_K1"] = mode
         try:
@@ -248,7 +248,9 @@ def test_k1_variants_agree(cfg, scale):
                 e.run_host(data, off, p["doc_ids"], p["ndocs_total"])
                 f = e.info()["flags"]
                 assert (f & 3) == flag
-                if mode in ("auto", "st") and cfg != "c4":
+                if mode in ("auto", "sl") and cfg != "c4":
+                    assert f & tfidf_abi.RUN_K1_SL
+                if mode == "st" and cfg != "c4":
                     assert f & tfidf_abi.RUN_K1_ST
                 outs.append(e.fetch())
         finally:
