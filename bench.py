@@ -410,16 +410,22 @@ def main():
     # GPU %.16f formatting of the last step's lines, then the pinned D2H + write path
     emit = None
     if not args.no_emit:
+        # 1) the CLI's path: formatting in document groups overlapped with the pinned D2H
+        #    (first call: also pins the context's staging ring); 2) the text again (already
+        #    formatted, ring warm): the D2H rate alone
         t1 = time.perf_counter()
+        eng.write_output("/dev/null")
+        t_fw = time.perf_counter() - t1
         n = eng.format_bytes()
-        t_fmt = time.perf_counter() - t1
         t2 = time.perf_counter()
         eng.write_output("/dev/null")
         t_wr = time.perf_counter() - t2
-        emit = {"text_bytes": int(n), "format_ms": round(t_fmt * 1e3, 3),
-                "format_GBps": round(n / t_fmt / 1e9, 2) if t_fmt > 0 else None,
-                "d2h_write_devnull_ms": round(t_wr * 1e3, 3),
-                "note": "GPU formatting (wall, incl. the size sync) and pinned D2H to /dev/null; not in value"}
+        emit = {"text_bytes": int(n), "format_d2h_overlapped_ms": round(t_fw * 1e3, 3),
+                "d2h_devnull_ms": round(t_wr * 1e3, 3),
+                "d2h_GBps": round(n / t_wr / 1e9, 2) if t_wr > 0 else None,
+                "note": "GPU %.16f formatting in 8 document groups overlapped with the D2H through a "
+                        "4 x 32 MB pinned ring (first call, incl. pinning the ring), then the D2H alone; "
+                        "written to /dev/null; not in value"}
 
     if dist is not None:
         import torch

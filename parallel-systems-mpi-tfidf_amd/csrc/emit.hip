@@ -147,7 +147,7 @@ struct EmitArgs {
     const uint4* tkey;
     const uint32_t* tlen;
     const uint8_t* corpus;     /* long terms' bytes */
-    uint32_t ndocs;
+    uint32_t doc0, ndocs;      /* the output positions [doc0, ndocs) this launch covers */
     uint64_t* doc_bytes;       /* pass 1: text bytes per output position */
     const uint64_t* doc_text;  /* pass 2: text offset per output position */
     uint8_t* text;
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(NT) void k_doc_text_write(EmitArgs a) {
     const uint32_t lane = threadIdx.x & 63;
     uint8_t* sg = stage[threadIdx.x >> 6];
     const uint32_t stride = gridDim.x * (NT / 64);
-    for (uint32_t i = blockIdx.x * (NT / 64) + (threadIdx.x >> 6); i < a.ndocs; i += stride) {
+    for (uint32_t i = a.doc0 + blockIdx.x * (NT / 64) + (threadIdx.x >> 6); i < a.ndocs; i += stride) {
         const uint64_t p0 = a.out_off[i], p1 = a.out_off[i + 1];
         const uint32_t id = doc_id_of(a, i), nid = ndig32(id);
         uint64_t pre_lo, pre_hi;
@@ -363,17 +363,19 @@ static unsigned emit_grid(uint32_t ndocs) {
 
 int launch_emit_bytes(const EmitLaunch& e, uint64_t* doc_bytes, hipStream_t s) {
     if (!e.ndocs) return 0;
-    EmitArgs a{e.order, e.doc_ids, e.out_off, e.term, e.score, e.tkey, e.tlen, e.corpus, e.ndocs,
+    EmitArgs a{e.order, e.doc_ids, e.out_off, e.term, e.score, e.tkey, e.tlen, e.corpus, 0u, e.ndocs,
                doc_bytes, nullptr, nullptr, e.status};
     k_doc_text_bytes<<<emit_grid(e.ndocs), NT, 0, s>>>(a);
     return ok();
 }
 
-int launch_emit_write(const EmitLaunch& e, const uint64_t* doc_text, uint8_t* text, hipStream_t s) {
-    if (!e.ndocs) return 0;
-    EmitArgs a{e.order, e.doc_ids, e.out_off, e.term, e.score, e.tkey, e.tlen, e.corpus, e.ndocs,
+int launch_emit_write(const EmitLaunch& e, const uint64_t* doc_text, uint8_t* text, hipStream_t s, uint32_t d0,
+                      uint32_t d1) {
+    if (d1 > e.ndocs) d1 = e.ndocs;
+    if (d0 >= d1) return 0;
+    EmitArgs a{e.order, e.doc_ids, e.out_off, e.term, e.score, e.tkey, e.tlen, e.corpus, d0, d1,
                nullptr, doc_text, text, e.status};
-    k_doc_text_write<<<emit_grid(e.ndocs), NT, 0, s>>>(a);
+    k_doc_text_write<<<emit_grid(d1 - d0), NT, 0, s>>>(a);
     return ok();
 }
 

@@ -175,6 +175,12 @@ struct tfidf_ctx {
     const uint32_t* run_merged = nullptr;
     /* output text (emit.hip) */
     DevBuf t_key, t_len, doc_tbytes, doc_toff, text;
+#define WR_NBUF 4
+#define WR_BUF (32ull << 20)
+#define WR_GROUPS 8
+    uint8_t* wr_buf[WR_NBUF] = {nullptr, nullptr, nullptr, nullptr};   /* pinned output staging ring */
+    hipEvent_t wr_ev[WR_NBUF] = {};
+    hipEvent_t wr_fmt[WR_GROUPS] = {};
     uint64_t text_bytes = 0;
     bool text_valid = false;
     uint32_t* sorted_dense = nullptr; /* points into seq0/seq1 */
@@ -313,6 +319,12 @@ void tfidf_close(tfidf_ctx* ctx) {
     if (ctx->stream2) { (void)hipStreamSynchronize(ctx->stream2); (void)hipStreamDestroy(ctx->stream2); }
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_order) (void)hipEventDestroy(ctx->ev_order);
+    for (int i = 0; i < WR_NBUF; ++i) {
+        if (ctx->wr_buf[i]) (void)hipHostFree(ctx->wr_buf[i]);
+        if (ctx->wr_ev[i]) (void)hipEventDestroy(ctx->wr_ev[i]);
+    }
+    for (int i = 0; i < WR_GROUPS; ++i)
+        if (ctx->wr_fmt[i]) (void)hipEventDestroy(ctx->wr_fmt[i]);
     ctx->arena2_buf.release();
     DevBuf* bufs[] = {&ctx->arena_buf, &ctx->in_bytes, &ctx->in_off, &ctx->in_ids, &ctx->syn_bytes, &ctx->syn_off,
                       &ctx->syn_ids, &ctx->syn_ntok, &ctx->syn_blkfirst, &ctx->syn_blkbytes, &ctx->syn_cdf,
@@ -1446,10 +1458,9 @@ extern "C" int tfidf_synth_device(tfidf_ctx* ctx, uint64_t seed, uint32_t V, uin
  * the "docN@word\t%.16f\n" lines (TFIDF.c:245,281) formatted in HBM
  * by emit.hip (exact round-half-even %.16f), then copied out / written to output.txt
  * (TFIDF.c:274-282). */
-extern "C" int tfidf_format(tfidf_ctx* ctx, uint64_t* nbytes) {
-    if (!ctx || !nbytes) return TFIDF_E_INVAL;
-    if (!ctx->have_result) return TFIDF_E_STATE;
-    if (ctx->text_valid) { *nbytes = ctx->text_bytes; return TFIDF_OK; }
+/* the length pass: term metadata, bytes per output position, their scan (doc_toff) and
+ * the text buffer sized to the total (one synchronisation for the total) */
+static int format_prepare(tfidf_ctx* ctx, EmitLaunch& e, uint64_t& total) {
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     const uint32_t N = ctx->ndocs, V = ctx->V;
@@ -1463,31 +1474,51 @@ extern "C" int tfidf_format(tfidf_ctx* ctx, uint64_t* nbytes) {
     if (launch_term_meta(ctx->vkeys.as<uint4>(), ctx->vrep.as<uint64_t>(), ctx->slot_of_rank.as<uint32_t>(), V,
                          ctx->t_key.as<uint4>(), ctx->t_len.as<uint32_t>(), s))
         return TFIDF_E_HIP;
-    EmitLaunch e{ctx->order, ctx->dev_ids, ctx->out_off.as<uint64_t>(), ctx->out_term.as<uint32_t>(),
-                 ctx->out_score.as<double>(), ctx->t_key.as<uint4>(), ctx->t_len.as<uint32_t>(), ctx->dev_bytes, N,
-                 status};
-    uint64_t total = 0;
+    e = EmitLaunch{ctx->order, ctx->dev_ids, ctx->out_off.as<uint64_t>(), ctx->out_term.as<uint32_t>(),
+                   ctx->out_score.as<double>(), ctx->t_key.as<uint4>(), ctx->t_len.as<uint32_t>(), ctx->dev_bytes, N,
+                   status};
+    total = 0;
     if (N) {
         if (launch_emit_bytes(e, ctx->doc_tbytes.as<uint64_t>(), s)) return TFIDF_E_HIP;
         ctx->arena.used = 0;
         if (scan_excl_u64(ctx->doc_tbytes.as<uint64_t>(), ctx->doc_toff.as<uint64_t>(), N, ctx->arena, s))
             return TFIDF_E_HIP;
-        HIPCHK(hipMemcpyAsync(&total, ctx->doc_toff.as<uint64_t>() + N, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(&ctx->hpin[20], ctx->doc_toff.as<uint64_t>() + N, 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
+        total = ctx->hpin[20];
     }
     ENSURE(ctx->text, total + 64);
-    if (total && launch_emit_write(e, ctx->doc_toff.as<uint64_t>(), ctx->text.as<uint8_t>(), s)) return TFIDF_E_HIP;
-    uint32_t st = 0;
-    HIPCHK(hipMemcpyAsync(&st, status, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    if (st & ST_BOUNDS) {
+    return TFIDF_OK;
+}
+
+/* the formatter's status after its launches (the stream is synchronised by the caller) */
+static int format_finish(tfidf_ctx* ctx, uint64_t total) {
+    uint32_t* status = (uint32_t*)(ctx->counters.as<unsigned long long>() + 3);
+    ctx->hpin[21] = 0;
+    HIPCHK(hipMemcpyAsync(&ctx->hpin[21], status, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if ((uint32_t)ctx->hpin[21] & ST_BOUNDS) {
         fprintf(stderr, "tfidf: score outside the %%.16f formatter's range\n");
         return TFIDF_E_STATE;
     }
     ctx->text_bytes = total;
     ctx->text_valid = true;
-    *nbytes = total;
     return TFIDF_OK;
+}
+
+extern "C" int tfidf_format(tfidf_ctx* ctx, uint64_t* nbytes) {
+    if (!ctx || !nbytes) return TFIDF_E_INVAL;
+    if (!ctx->have_result) return TFIDF_E_STATE;
+    if (ctx->text_valid) { *nbytes = ctx->text_bytes; return TFIDF_OK; }
+    EmitLaunch e{};
+    uint64_t total = 0;
+    int rc = format_prepare(ctx, e, total);
+    if (rc) return rc;
+    if (total && launch_emit_write(e, ctx->doc_toff.as<uint64_t>(), ctx->text.as<uint8_t>(), ctx->stream))
+        return TFIDF_E_HIP;
+    rc = format_finish(ctx, total);
+    if (!rc) *nbytes = total;
+    return rc;
 }
 
 extern "C" int tfidf_copy_text(tfidf_ctx* ctx, uint64_t off, void* dst, uint64_t n) {
@@ -1500,48 +1531,85 @@ extern "C" int tfidf_copy_text(tfidf_ctx* ctx, uint64_t off, void* dst, uint64_t
     return TFIDF_OK;
 }
 
-extern "C" int tfidf_write_output_gpu(tfidf_ctx* ctx, const char* path, int append) {
-    if (!ctx || !path) return TFIDF_E_INVAL;
-    uint64_t total = 0;
-    int rc = tfidf_format(ctx, &total);
-    if (rc) return rc;
-    FILE* f = fopen(path, append ? "ab" : "wb");
-    if (!f) return TFIDF_E_OUTPUT;
-    /* two pinned staging buffers: the copy of block k+1 overlaps the write of block k */
-    const uint64_t B = 64ull << 20;
-    uint8_t* hb[2] = {nullptr, nullptr};
-    hipEvent_t ev[2];
-    bool ok = true;
-    for (int i = 0; i < 2; ++i) {
-        if (hipHostMalloc((void**)&hb[i], B, hipHostMallocDefault) != hipSuccess) ok = false;
-        if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) ok = false;
-    }
-    hipStream_t s = ctx->stream;
-    const uint8_t* src = ctx->text.as<uint8_t>();
-    uint64_t nblk = (total + B - 1) / B;
-    for (uint64_t k = 0; ok && k < nblk && k < 2; ++k) {
-        const uint64_t n = (k + 1) * B <= total ? B : total - k * B;
-        if (hipMemcpyAsync(hb[k & 1], src + k * B, n, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipEventRecord(ev[k & 1], s) != hipSuccess) ok = false;
-    }
-    for (uint64_t k = 0; ok && k < nblk; ++k) {
-        const uint64_t n = (k + 1) * B <= total ? B : total - k * B;
-        if (hipEventSynchronize(ev[k & 1]) != hipSuccess) { ok = false; break; }
-        if (fwrite(hb[k & 1], 1, n, f) != n) { rc = TFIDF_E_OUTPUT; ok = false; break; }
-        const uint64_t k2 = k + 2;
-        if (k2 < nblk) {
-            const uint64_t n2 = (k2 + 1) * B <= total ? B : total - k2 * B;
-            if (hipMemcpyAsync(hb[k2 & 1], src + k2 * B, n2, hipMemcpyDeviceToHost, s) != hipSuccess ||
-                hipEventRecord(ev[k2 & 1], s) != hipSuccess) ok = false;
+/* output.txt (TFIDF.c:274-282): the text leaves HBM through a ring of WR_NBUF pinned
+ * staging buffers owned by the context (allocated on first use and kept: pinning 128 MB
+ * costs tens of ms per call).  The copies run on stream2 while the host writes the
+ * buffers already copied; when the text is not yet formatted, the formatter runs in
+ * WR_GROUPS document groups on the main stream and each copy waits only for the group
+ * that holds its last byte, so formatting of group g+1 overlaps the copy of group g. */
+static int wr_ring_init(tfidf_ctx* ctx) {
+    if (ctx->wr_buf[0]) return TFIDF_OK;
+    for (int i = 0; i < WR_NBUF; ++i) {
+        if (hipHostMalloc((void**)&ctx->wr_buf[i], WR_BUF, hipHostMallocDefault) != hipSuccess) {
+            ctx->wr_buf[i] = nullptr;
+            for (int j = 0; j < i; ++j) { (void)hipHostFree(ctx->wr_buf[j]); ctx->wr_buf[j] = nullptr; }
+            return TFIDF_E_NOMEM;
         }
     }
-    (void)hipStreamSynchronize(s);
-    for (int i = 0; i < 2; ++i) {
-        if (hb[i]) (void)hipHostFree(hb[i]);
-        (void)hipEventDestroy(ev[i]);
+    for (int i = 0; i < WR_NBUF; ++i) HIPCHK(hipEventCreateWithFlags(&ctx->wr_ev[i], hipEventDisableTiming));
+    for (int i = 0; i < WR_GROUPS; ++i) HIPCHK(hipEventCreateWithFlags(&ctx->wr_fmt[i], hipEventDisableTiming));
+    return TFIDF_OK;
+}
+
+extern "C" int tfidf_write_output_gpu(tfidf_ctx* ctx, const char* path, int append) {
+    if (!ctx || !path) return TFIDF_E_INVAL;
+    if (!ctx->have_result) return TFIDF_E_STATE;
+    HIPCHK(hipSetDevice(ctx->device));
+    int rc = wr_ring_init(ctx);
+    if (rc) return rc;
+    hipStream_t s = ctx->stream, cs = ctx->stream2;
+    const uint32_t N = ctx->ndocs;
+    uint64_t total = ctx->text_bytes;
+    /* group g covers output positions [gd[g], gd[g+1]) and text bytes [gb[g], gb[g+1]) */
+    uint64_t gb[WR_GROUPS + 1];
+    int ng = 0;
+    const bool fmt = !ctx->text_valid;
+    if (fmt) {
+        EmitLaunch e{};
+        rc = format_prepare(ctx, e, total);
+        if (rc) return rc;
+        ng = N ? (N < WR_GROUPS ? (int)N : WR_GROUPS) : 0;
+        std::vector<uint64_t> toff((size_t)N + 1);
+        if (N) HIPCHK(hipMemcpy(toff.data(), ctx->doc_toff.p, ((size_t)N + 1) * 8, hipMemcpyDeviceToHost));
+        for (int g = 0; g < ng; ++g) {
+            const uint32_t d0 = (uint32_t)((uint64_t)N * g / ng), d1 = (uint32_t)((uint64_t)N * (g + 1) / ng);
+            gb[g] = toff[d0];
+            gb[g + 1] = toff[d1];
+            if (launch_emit_write(e, ctx->doc_toff.as<uint64_t>(), ctx->text.as<uint8_t>(), s, d0, d1))
+                return TFIDF_E_HIP;
+            HIPCHK(hipEventRecord(ctx->wr_fmt[g], s));
+        }
     }
+    FILE* f = fopen(path, append ? "ab" : "wb");
+    if (!f) { (void)hipStreamSynchronize(s); return TFIDF_E_OUTPUT; }
+    const uint8_t* src = ctx->text.as<uint8_t>();
+    const uint64_t nblk = (total + WR_BUF - 1) / WR_BUF;
+    int gwait = 0;   /* groups the copy stream already waits for */
+    bool ok = true;
+    auto issue = [&](uint64_t k) {
+        const uint64_t b0 = k * WR_BUF, n = b0 + WR_BUF <= total ? WR_BUF : total - b0;
+        while (fmt && gwait < ng && gb[gwait] < b0 + n) {   /* every group holding a byte of this block */
+            if (hipStreamWaitEvent(cs, ctx->wr_fmt[gwait], 0) != hipSuccess) ok = false;
+            ++gwait;
+        }
+        if (hipMemcpyAsync(ctx->wr_buf[k % WR_NBUF], src + b0, n, hipMemcpyDeviceToHost, cs) != hipSuccess ||
+            hipEventRecord(ctx->wr_ev[k % WR_NBUF], cs) != hipSuccess)
+            ok = false;
+    };
+    for (uint64_t k = 0; ok && k < nblk && k < WR_NBUF; ++k) issue(k);
+    for (uint64_t k = 0; ok && k < nblk; ++k) {
+        const uint64_t b0 = k * WR_BUF, n = b0 + WR_BUF <= total ? WR_BUF : total - b0;
+        if (hipEventSynchronize(ctx->wr_ev[k % WR_NBUF]) != hipSuccess) { ok = false; break; }
+        if (fwrite(ctx->wr_buf[k % WR_NBUF], 1, n, f) != n) { rc = TFIDF_E_OUTPUT; ok = false; break; }
+        if (k + WR_NBUF < nblk) issue(k + WR_NBUF);
+    }
+    (void)hipStreamSynchronize(cs);
     if (fclose(f) != 0 && !rc) rc = TFIDF_E_OUTPUT;
     if (!ok && !rc) rc = TFIDF_E_HIP;
+    if (fmt) {
+        const int r2 = format_finish(ctx, total);   /* synchronises the main stream */
+        if (!rc) rc = r2;
+    }
     return rc;
 }
 

@@ -245,7 +245,9 @@ struct EmitLaunch {
 int launch_term_meta(const uint4* vkeys, const uint64_t* vrep, const uint32_t* slot_of_rank, uint32_t V,
                      uint4* tkey, uint32_t* tlen, hipStream_t s);
 int launch_emit_bytes(const EmitLaunch& e, uint64_t* doc_bytes, hipStream_t s);
-int launch_emit_write(const EmitLaunch& e, const uint64_t* doc_text, uint8_t* text, hipStream_t s);
+/* formats the output positions [d0, d1) (default: all) */
+int launch_emit_write(const EmitLaunch& e, const uint64_t* doc_text, uint8_t* text, hipStream_t s, uint32_t d0 = 0,
+                      uint32_t d1 = 0xFFFFFFFFu);
 int launch_format_f64(const double* v, uint64_t n, uint8_t* out, uint32_t* status, hipStream_t s);
 
 #endif

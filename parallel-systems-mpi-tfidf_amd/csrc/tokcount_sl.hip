@@ -262,7 +262,12 @@ __device__ __forceinline__ uint32_t wave_agg_add_rtn(uint32_t* ctr, uint32_t idx
  * documents crossing the chunk, over K5's in-LDS sort size or with overflow records: the
  * partial stream) — any number of documents: per-document counts by wave-aggregated LDS
  * adds, a block scan, every entry written at its document's base + its rank. */
-__device__ __noinline__ void sl_flush(SlShared& S, const K1Out* o, uint32_t gd0, uint32_t ng, uint32_t sb) {
+#ifdef SL_INLINE_FLUSH
+#define SL_FLUSH_ATTR __forceinline__
+#else
+#define SL_FLUSH_ATTR __noinline__
+#endif
+__device__ SL_FLUSH_ATTR void sl_flush(SlShared& S, const K1Out* o, uint32_t gd0, uint32_t ng, uint32_t sb) {
     const int tid = threadIdx.x;
     lds_barrier();
     if (tid < GCAP) { S.f.dcnt[tid] = 0; S.f.drun[tid] = 0; }
@@ -332,7 +337,7 @@ __device__ __noinline__ void sl_flush(SlShared& S, const K1Out* o, uint32_t gd0,
 /* The flush of a group of at most FEW documents (most chunks hold one or two): per-thread
  * 16-bit document counters and one block scan, no LDS atomics.  Same output as sl_flush. */
 constexpr uint32_t FEW = 8;
-__device__ __noinline__ void sl_flush_few(SlShared& S, const K1Out* o, uint32_t gd0, uint32_t ng, uint32_t sb) {
+__device__ SL_FLUSH_ATTR void sl_flush_few(SlShared& S, const K1Out* o, uint32_t gd0, uint32_t ng, uint32_t sb) {
     const int tid = threadIdx.x;
     const int lane = tid & 63, w = tid >> 6;
     lds_barrier();
@@ -503,8 +508,14 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
      * (the chunk starts inside or at the start of its first document), so neither waits for
      * the other or for the clear. */
     const uint32_t ng0 = (dlast + 1 - dfirst) < gcap ? (dlast + 1 - dfirst) : gcap;
+#ifdef SL_NOEARLY
+    const uint64_t dpre = 0;
+    uint4 pf = make_uint4(0, 0, 0, 0);
+    (void)ng0;
+#else
     const uint64_t dpre = (uint32_t)tid <= ng0 ? c.doc_off[dfirst + tid] : 0ull;
     uint4 pf = bload16<2>(crs, wid * WSTEP + 16 * lane - 16 + shift);
+#endif
     /* table + selectors (once per workgroup) */
     if (!clean) {
         uint4* t = reinterpret_cast<uint4*>(S.TK);
@@ -521,7 +532,11 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
     for (uint32_t gd0 = dfirst; gd0 <= dlast; gd0 += gcap) {
         const uint32_t ng = (dlast + 1 - gd0) < gcap ? (dlast + 1 - gd0) : gcap;
         for (uint32_t k = tid; k <= ng; k += NT) {
+#ifdef SL_NOEARLY
+            const uint64_t d = c.doc_off[gd0 + k];
+#else
             const uint64_t d = (gd0 == dfirst && k == (uint32_t)tid) ? dpre : c.doc_off[gd0 + k];
+#endif
             S.gdoc[k] = d < b0 ? -64 : (d - b0 > (uint64_t)span + 64 ? span + 64 : (int32_t)(d - b0));
         }
         if (tid < GCAP) { S.dsz[tid] = 0; S.dpart[tid] = 0; }
@@ -547,6 +562,16 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
         uint32_t wclaims = 0;          /* this wave's LDS table claims (wave-uniform) */
 
         /* resolve + count one round */
+        /* pend takes acc's token and issues its vocabulary loads */
+        auto promote = [&](Round& p, const Round& a) {
+            p.k0 = a.k0; p.k1 = a.k1; p.k2 = a.k2; p.k3 = a.k3;
+            p.h = a.h; p.rel = a.rel; p.kind = a.kind; p.ap = a.ap;
+#ifdef SL_DEBUG
+            p.ent = a.ent;
+#endif
+            p.s0 = bload16<0>(vrs, (int32_t)(p.h << 4));
+            p.s1 = bload16<0>(vrs, (int32_t)(p.h << 4) + 16);
+        };
         auto finish = [&](const Round& r) {
             /* whole-key compares without short-circuit branches */
             const bool h0 = ((r.s0.x ^ r.k0) | (r.s0.y ^ r.k1) | (r.s0.z ^ r.k2) | (r.s0.w ^ r.k3)) == 0u;
@@ -593,10 +618,16 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
             const bool claim = key != 0u && !found && n < BW && !over;
             const uint32_t idx = BW * b + (found ? j : (n & (BW - 1u)));
             /* only a new key waits for an LDS round trip (its CAS); a match adds at once */
+#ifdef SL_CAS_ALL
+            const uint32_t old = atomicCAS(&S.TK[idx], hit ? key : (claim ? 0u : 0x7FFFFFFFu), key);
+            const bool ok = hit || (claim && (old == 0u || old == key));
+            atomicAdd(&S.TC[idx], ok ? 1u : 0u);
+#else
             uint32_t old = key;
             if (claim) old = atomicCAS(&S.TK[idx], 0u, key);
             const bool ok = hit || (claim && (old == 0u || old == key));
             if (ok) atomicAdd(&S.TC[idx], 1u);
+#endif
             const bool claimed = claim && old == 0u;
             const bool slow = key != 0u && !ok;
             uint32_t claims = claimed ? 1u : 0u;
@@ -610,7 +641,11 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
             const int32_t bs = gs & ~15;
             const int32_t nsteps = (ge - bs + WSTEP - 1) / WSTEP;
             const bool inner_all = bs >= lo_rel + 16 && bs + nsteps * WSTEP + 16 <= hi_rel;
+#ifdef SL_NOEARLY
+            pf = bload16<2>(crs, bs + wid * WSTEP + 16 * lane - 16 + shift);
+#else
             if (gd0 != dfirst || bs != 0) pf = bload16<2>(crs, bs + wid * WSTEP + 16 * lane - 16 + shift);
+#endif
             uint32_t wr = 0;                    /* wave-uniform: document containing the step start */
             int32_t wcur = g0, wnext = ng > 1 ? __builtin_amdgcn_readfirstlane(S.gdoc[1]) : gn;
             for (int32_t s = wid; s < nsteps; s += NWAVE) {
@@ -729,20 +764,21 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
                             acc.k3 = __builtin_amdgcn_perm(0x09090909u, raw.w, sl.w);
                             acc.h = (uint32_t)key_hash(((uint64_t)acc.k1 << 32) | acc.k0, ((uint64_t)acc.k3 << 32) | acc.k2) &
                                     (uint32_t)v.mask & ~1u;
-                            acc.s0 = bload16<0>(vrs, (int32_t)(acc.h << 4));
-                            acc.s1 = bload16<0>(vrs, (int32_t)(acc.h << 4) + 16);
                         }
                         t += m;
                         fill += m;
                         if (fill == 64u) {
+                            /* count the previous round, then send this one's vocabulary loads
+                             * straight into the registers that round just released: a loaded
+                             * value is never copied (a copy would wait for the load at once) */
                             finish(pend);
-                            pend = acc;
+                            promote(pend, acc);
                             acc.kind = 0u;
                             fill = 0u;
                         }
                     }
 #ifdef SL_NOCARRY
-                    if (fill) { finish(pend); pend = acc; acc.kind = 0u; fill = 0u; }
+                    if (fill) { finish(pend); promote(pend, acc); acc.kind = 0u; fill = 0u; }
 #endif
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
@@ -752,7 +788,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
         }
         if (fill) {   /* the group's last, partial round */
             finish(pend);
-            pend = acc;
+            promote(pend, acc);
         }
         finish(pend);   /* drain */
         if (ng <= FEW) sl_flush_few(S, o, gd0, ng, sb);

@@ -368,6 +368,24 @@ def test_gpu_text_c2_slice_vs_oracle(engine):
     assert engine.text() == ora["output_txt"]
 
 
+def test_gpu_output_file_grouped_format(engine, tmp_path):
+    """tfidf_write_output_gpu on an unformatted result formats in document groups whose
+    copies overlap the next group's formatting (groups share 16-byte chunks at their
+    boundaries): the file equals the oracle's output.txt, several 32 MB staging blocks
+    deep, and a second write of the now formatted text equals it too."""
+    p = tfidf_configs.plan("c2", scale=0.02)          # ~19 MB corpus -> ~45 MB of text
+    data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
+    engine.run_host(data, off, p["doc_ids"], p["ndocs_total"])
+    path = str(tmp_path / "out.txt")
+    engine.write_output(path)
+    got = open(path, "rb").read()
+    ora = oracle_py.run(data, off, p["doc_ids"], p["ndocs_total"])
+    assert len(got) > (32 << 20)
+    assert got == ora["output_txt"]
+    engine.write_output(path)
+    assert open(path, "rb").read() == got
+
+
 def test_dense_merge_long_documents(engine):
     """Documents longer than DENSE_DOC (4 MiB) take the dense merge (partial records summed
     per document over term ranks, emitted in rank order); a 180 KB document (split across
