@@ -416,13 +416,17 @@ def main():
         t1 = time.perf_counter()
         eng.write_output("/dev/null")
         t_fw = time.perf_counter() - t1
+        oi1 = eng.output_info()
         n = eng.format_bytes()
         t2 = time.perf_counter()
         eng.write_output("/dev/null")
         t_wr = time.perf_counter() - t2
+        oi2 = eng.output_info()
         emit = {"text_bytes": int(n), "format_d2h_overlapped_ms": round(t_fw * 1e3, 3),
                 "d2h_devnull_ms": round(t_wr * 1e3, 3),
                 "d2h_GBps": round(n / t_wr / 1e9, 2) if t_wr > 0 else None,
+                "first_call": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in oi1.items()},
+                "second_call": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in oi2.items()},
                 "note": "GPU %.16f formatting in 8 document groups overlapped with the D2H through a "
                         "4 x 32 MB pinned ring (first call, incl. pinning the ring), then the D2H alone; "
                         "written to /dev/null; not in value"}

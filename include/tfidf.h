@@ -211,10 +211,25 @@ int tfidf_hbm_probe(tfidf_ctx* ctx, uint64_t nbytes, int iters, double* read_gbp
 int tfidf_format(tfidf_ctx* ctx, uint64_t* nbytes);
 /* Copies bytes [off, off + n) of the formatted text to host memory. */
 int tfidf_copy_text(tfidf_ctx* ctx, uint64_t off, void* dst, uint64_t n);
-/* tfidf_format + D2H through two pinned buffers + fwrite to `path` (TFIDF.c:274-282);
- * append != 0 appends (a shard after the previous ones).  TFIDF_E_OUTPUT when the file
+/* tfidf_format + D2H + write to `path` (TFIDF.c:274-282); append != 0 appends (a shard
+ * after the previous ones).  An unformatted result is formatted in document groups whose
+ * D2H copies overlap the next group's formatting; the copies go through the context's
+ * ring of pinned 32 MB buffers (kept across calls) and a regular file is written by
+ * several threads at their blocks' offsets (pwrite).  TFIDF_E_OUTPUT when the file
  * cannot be opened or written. */
 int tfidf_write_output_gpu(tfidf_ctx* ctx, const char* path, int append);
+/* Timings of the last tfidf_write_output_gpu (the caller sets `size` = sizeof). */
+typedef struct tfidf_output_info {
+    uint64_t size;
+    uint64_t text_bytes;      /* bytes written */
+    uint32_t writers;         /* host writer threads (1: not a regular file) */
+    uint32_t formatted;       /* 1: this call formatted the text (0: it was already) */
+    double   ms_prepare;      /* length pass + text size (0 when already formatted) */
+    double   ms_d2h_busy;     /* host wall time from the first copy issued to the last copy done */
+    double   ms_write;        /* summed host time inside write/pwrite (over writer threads) */
+    double   ms_total;        /* the whole call */
+} tfidf_output_info;
+int tfidf_last_output_info(const tfidf_ctx* ctx, tfidf_output_info* info);
 /* The device %.16f formatter on n host doubles: out = n 32-byte slots, NUL-padded.
  * TFIDF_E_INVAL for values outside [0, 2^63/10^16) (scores are < 23). */
 int tfidf_format_f64(tfidf_ctx* ctx, const double* vals, uint64_t n, char* out);

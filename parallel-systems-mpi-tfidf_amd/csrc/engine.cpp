@@ -21,8 +21,16 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
 #include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/tfidf.h"
@@ -181,6 +189,8 @@ struct tfidf_ctx {
     uint8_t* wr_buf[WR_NBUF] = {nullptr, nullptr, nullptr, nullptr};   /* pinned output staging ring */
     hipEvent_t wr_ev[WR_NBUF] = {};
     hipEvent_t wr_fmt[WR_GROUPS] = {};
+#define WR_WRITERS 4
+    tfidf_output_info out_info{};
     uint64_t text_bytes = 0;
     bool text_valid = false;
     uint32_t* sorted_dense = nullptr; /* points into seq0/seq1 */
@@ -1551,16 +1561,25 @@ static int wr_ring_init(tfidf_ctx* ctx) {
     return TFIDF_OK;
 }
 
+static double now_ms() {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e3 + t.tv_nsec * 1e-6;
+}
+
 extern "C" int tfidf_write_output_gpu(tfidf_ctx* ctx, const char* path, int append) {
     if (!ctx || !path) return TFIDF_E_INVAL;
     if (!ctx->have_result) return TFIDF_E_STATE;
+    const double t0 = now_ms();
+    tfidf_output_info oi{};
+    oi.size = sizeof(oi);
     HIPCHK(hipSetDevice(ctx->device));
     int rc = wr_ring_init(ctx);
     if (rc) return rc;
     hipStream_t s = ctx->stream, cs = ctx->stream2;
     const uint32_t N = ctx->ndocs;
     uint64_t total = ctx->text_bytes;
-    /* group g covers output positions [gd[g], gd[g+1]) and text bytes [gb[g], gb[g+1]) */
+    /* group g covers output positions [N g / ng, N (g+1) / ng) and text bytes [gb[g], gb[g+1]) */
     uint64_t gb[WR_GROUPS + 1];
     int ng = 0;
     const bool fmt = !ctx->text_valid;
@@ -1579,38 +1598,121 @@ extern "C" int tfidf_write_output_gpu(tfidf_ctx* ctx, const char* path, int appe
                 return TFIDF_E_HIP;
             HIPCHK(hipEventRecord(ctx->wr_fmt[g], s));
         }
+        oi.formatted = 1;
     }
-    FILE* f = fopen(path, append ? "ab" : "wb");
-    if (!f) { (void)hipStreamSynchronize(s); return TFIDF_E_OUTPUT; }
+    const double t_prep = now_ms();
+    oi.ms_prepare = fmt ? t_prep - t0 : 0.0;
+    const int fd = open(path, O_WRONLY | O_CREAT | (append ? 0 : O_TRUNC), 0644);
+    if (fd < 0) { (void)hipStreamSynchronize(s); return TFIDF_E_OUTPUT; }
+    struct stat fst;
+    const bool regular = fstat(fd, &fst) == 0 && S_ISREG(fst.st_mode);
+    /* a regular file: blocks written at their offsets by WR_WRITERS threads (page-cache
+     * copies in parallel); anything else (a pipe, /dev/null): one thread, in order */
+    const uint64_t base = append && regular ? (uint64_t)fst.st_size : 0;
+    if (!regular && append) (void)lseek(fd, 0, SEEK_END);
     const uint8_t* src = ctx->text.as<uint8_t>();
     const uint64_t nblk = (total + WR_BUF - 1) / WR_BUF;
-    int gwait = 0;   /* groups the copy stream already waits for */
-    bool ok = true;
-    auto issue = [&](uint64_t k) {
-        const uint64_t b0 = k * WR_BUF, n = b0 + WR_BUF <= total ? WR_BUF : total - b0;
-        while (fmt && gwait < ng && gb[gwait] < b0 + n) {   /* every group holding a byte of this block */
-            if (hipStreamWaitEvent(cs, ctx->wr_fmt[gwait], 0) != hipSuccess) ok = false;
-            ++gwait;
+    const int nw = regular ? (nblk < (uint64_t)WR_WRITERS ? (int)(nblk ? nblk : 1) : WR_WRITERS) : 1;
+    oi.writers = (uint32_t)nw;
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t issued = 0;             /* blocks whose copies were sent */
+    uint64_t freed[WR_NBUF] = {0};   /* per ring buffer: blocks it has finished (written) */
+    bool failed = false;
+    int wrc = TFIDF_OK;
+    double t_last_copy = t_prep, write_ms = 0.0;
+    auto blk_n = [&](uint64_t k) { return (k + 1) * WR_BUF <= total ? WR_BUF : total - k * WR_BUF; };
+    /* writer w takes blocks k = w, w + nw, ...: waits for the copy, writes, frees the buffer */
+    auto writer = [&](int w) {
+        double my_write = 0.0, my_last = 0.0;
+        for (uint64_t k = (uint64_t)w; k < nblk; k += (uint64_t)nw) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return issued > k || failed; });
+                if (failed) break;
+            }
+            const int b = (int)(k % WR_NBUF);
+            bool ok = hipEventSynchronize(ctx->wr_ev[b]) == hipSuccess;
+            const double tc = now_ms();
+            my_last = tc > my_last ? tc : my_last;
+            const uint64_t n = blk_n(k);
+            uint64_t done = 0;
+            while (ok && done < n) {
+                const ssize_t r = regular ? pwrite(fd, ctx->wr_buf[b] + done, n - done, (off_t)(base + k * WR_BUF + done))
+                                          : write(fd, ctx->wr_buf[b] + done, n - done);
+                if (r <= 0) { ok = false; break; }
+                done += (uint64_t)r;
+            }
+            my_write += now_ms() - tc;
+            std::lock_guard<std::mutex> lk(mu);
+            if (!ok) {
+                failed = true;
+                if (!wrc) wrc = done < n ? TFIDF_E_OUTPUT : TFIDF_E_HIP;
+            }
+            freed[b] = k + 1;
+            cv.notify_all();
+            if (failed) break;
         }
-        if (hipMemcpyAsync(ctx->wr_buf[k % WR_NBUF], src + b0, n, hipMemcpyDeviceToHost, cs) != hipSuccess ||
-            hipEventRecord(ctx->wr_ev[k % WR_NBUF], cs) != hipSuccess)
-            ok = false;
+        std::lock_guard<std::mutex> lk(mu);
+        write_ms += my_write;
+        if (my_last > t_last_copy) t_last_copy = my_last;
     };
-    for (uint64_t k = 0; ok && k < nblk && k < WR_NBUF; ++k) issue(k);
-    for (uint64_t k = 0; ok && k < nblk; ++k) {
-        const uint64_t b0 = k * WR_BUF, n = b0 + WR_BUF <= total ? WR_BUF : total - b0;
-        if (hipEventSynchronize(ctx->wr_ev[k % WR_NBUF]) != hipSuccess) { ok = false; break; }
-        if (fwrite(ctx->wr_buf[k % WR_NBUF], 1, n, f) != n) { rc = TFIDF_E_OUTPUT; ok = false; break; }
-        if (k + WR_NBUF < nblk) issue(k + WR_NBUF);
-    }
+    std::vector<std::thread> th;
+    for (int w = 1; w < nw; ++w) th.emplace_back(writer, w);
+    /* issue: block k reuses ring buffer k % WR_NBUF once block k - WR_NBUF is written; its
+     * copy waits (on the copy stream) for every format group holding one of its bytes */
+    std::thread issuer([&] {
+        (void)hipSetDevice(ctx->device);
+        int gwait = 0;
+        for (uint64_t k = 0; k < nblk; ++k) {
+            const int b = (int)(k % WR_NBUF);
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return k < WR_NBUF || freed[b] >= k - WR_NBUF + 1 || failed; });
+                if (failed) return;
+            }
+            const uint64_t b0 = k * WR_BUF, n = blk_n(k);
+            bool ok = true;
+            while (fmt && gwait < ng && gb[gwait] < b0 + n) {
+                if (hipStreamWaitEvent(cs, ctx->wr_fmt[gwait], 0) != hipSuccess) ok = false;
+                ++gwait;
+            }
+            if (ok && (hipMemcpyAsync(ctx->wr_buf[b], src + b0, n, hipMemcpyDeviceToHost, cs) != hipSuccess ||
+                       hipEventRecord(ctx->wr_ev[b], cs) != hipSuccess))
+                ok = false;
+            std::lock_guard<std::mutex> lk(mu);
+            if (!ok) { failed = true; if (!wrc) wrc = TFIDF_E_HIP; }
+            else issued = k + 1;
+            cv.notify_all();
+            if (failed) return;
+        }
+    });
+    (void)hipSetDevice(ctx->device);
+    writer(0);
+    issuer.join();
+    for (auto& t : th) t.join();
     (void)hipStreamSynchronize(cs);
-    if (fclose(f) != 0 && !rc) rc = TFIDF_E_OUTPUT;
-    if (!ok && !rc) rc = TFIDF_E_HIP;
+    if (close(fd) != 0 && !wrc) wrc = TFIDF_E_OUTPUT;
+    rc = wrc;
     if (fmt) {
         const int r2 = format_finish(ctx, total);   /* synchronises the main stream */
         if (!rc) rc = r2;
     }
+    oi.text_bytes = total;
+    oi.ms_d2h_busy = nblk ? t_last_copy - t_prep : 0.0;
+    oi.ms_write = write_ms;
+    oi.ms_total = now_ms() - t0;
+    ctx->out_info = oi;
     return rc;
+}
+
+extern "C" int tfidf_last_output_info(const tfidf_ctx* ctx, tfidf_output_info* info) {
+    if (!ctx || !info || info->size < sizeof(uint64_t)) return TFIDF_E_INVAL;
+    const uint64_t n = info->size < sizeof(tfidf_output_info) ? info->size : sizeof(tfidf_output_info);
+    tfidf_output_info o = ctx->out_info;
+    o.size = n;
+    memcpy(info, &o, (size_t)n);
+    return TFIDF_OK;
 }
 
 extern "C" int tfidf_format_f64(tfidf_ctx* ctx, const double* vals, uint64_t n, char* out) {

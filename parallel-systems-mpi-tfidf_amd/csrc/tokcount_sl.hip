@@ -82,6 +82,7 @@ struct SlShared {
     uint8_t dfull[GCAP];                /* document lies wholly inside the chunk */
     uint32_t wsum[NWAVE];
     unsigned long long rec_base, part_base;
+    unsigned long long next_chunk;      /* persistent form: the workgroup's next chunk (claimed ahead) */
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -476,14 +477,27 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
     unsigned long long tokens_w = 0;
     bool clean = false;             /* the LDS table is clear (every flush clears what it emits) */
 #ifdef SL_PERSIST
-    for (uint64_t chunk = c0 + blockIdx.x; chunk < c1; chunk += gridDim.x) {
+    /* chunks are claimed from a global counter (their sizes vary: a static share leaves a
+     * tail of the slowest workgroups); the next claim is sent when a chunk starts, so its
+     * round trip is hidden behind the chunk */
+    if (tid == 0) S.next_chunk = c0 + atomicAdd(o->chunk_ctr, 1ull);
+    lds_barrier();
+    unsigned long long claim = 0;
+    for (uint64_t chunk = (uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S.next_chunk) |
+                          ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S.next_chunk >> 32)) << 32);
+         chunk < c1;) {
+    if (tid == 0) claim = c0 + atomicAdd(o->chunk_ctr, 1ull);
 #else
     do {            /* one chunk per workgroup (`continue` leaves) */
     const uint64_t chunk = c0 + blockIdx.x;
 #endif
     const uint64_t cs = chunk_start[chunk], ce = chunk_start[chunk + 1];
     const uint32_t dfirst = chunk_doc[chunk], dlast = chunk_doc[chunk + 1];
+#ifdef SL_PERSIST
+    if (cs < ce) {
+#else
     if (cs >= ce) continue;   /* an empty chunk (a shard shorter than the chunk grid) */
+#endif
 
     /* chunk base and the corpus buffer: byte at chunk-relative p is at buffer offset p + shift */
     const uint64_t b0 = cs & ~(uint64_t)15;
@@ -804,6 +818,11 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
         if (gd0 + gcap < gd0) break;   /* overflow guard */
     }
 #ifdef SL_PERSIST
+    }   /* cs < ce */
+    if (tid == 0) S.next_chunk = claim;
+    lds_barrier();
+    chunk = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S.next_chunk) |
+            ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S.next_chunk >> 32)) << 32);
     }   /* chunk */
 #else
     } while (0);

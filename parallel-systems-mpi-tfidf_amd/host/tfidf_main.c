@@ -81,14 +81,21 @@ static int run_single(int device, const char* indir, const char* outpath, int de
     rc = tfidf_write_output_gpu(ctx, outpath, 0);
     if (rc == TFIDF_E_OUTPUT) printf("Error Opening File: %s\n", outpath);
     else if (rc) { tfidf_close(ctx); return fail(rc); }
-    if (stats)
+    if (stats) {
+        const double out_ms = wall_ms() - t_out;
+        tfidf_output_info oi;
+        memset(&oi, 0, sizeof(oi));
+        oi.size = sizeof(oi);
+        (void)tfidf_last_output_info(ctx, &oi);
         fprintf(stderr,
                 "{\"docs\": %u, \"corpus_bytes\": %llu, \"shards\": 1, \"ingest_threads\": %u, \"ingest_scan_ms\": %.3f, "
                 "\"ingest_read_h2d_ms\": %.3f, \"ingest_GBps\": %.3f, \"run_device_ms\": %.3f, \"pairs\": %llu, "
-                "\"output_ms\": %.3f}\n",
+                "\"output_ms\": %.3f, \"output_bytes\": %llu, \"output_format_prepare_ms\": %.3f, "
+                "\"output_d2h_busy_ms\": %.3f, \"output_write_thread_ms\": %.3f, \"output_writers\": %u}\n",
                 ii.ndocs, (unsigned long long)ii.nbytes, ii.threads, ii.ms_scan, ii.ms_read,
                 ii.ms_total > 0 ? ii.nbytes / ii.ms_total / 1e6 : 0.0, ri.ms_total, (unsigned long long)ri.npairs,
-                wall_ms() - t_out);
+                out_ms, (unsigned long long)oi.text_bytes, oi.ms_prepare, oi.ms_d2h_busy, oi.ms_write, oi.writers);
+    }
     tfidf_close(ctx);
     return 0;
 }

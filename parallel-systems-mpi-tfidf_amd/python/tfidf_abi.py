@@ -35,6 +35,7 @@ EXPORTS = [
     "tfidf_ingest_dir_device", "tfidf_hbm_probe", "tfidf_group_open", "tfidf_group_size", "tfidf_group_ctx",
     "tfidf_group_run", "tfidf_group_write_output", "tfidf_group_close", "tfidf_plan_dir", "tfidf_plan_free",
     "tfidf_ingest_shard_device", "tfidf_doc_name_order", "tfidf_shard_split", "tfidf_device_count",
+    "tfidf_last_output_info",
 ]
 TFIDF_GROUP_LOCAL = 1
 E_PEER = -11
@@ -66,6 +67,13 @@ class RunInfo(C.Structure):
         ("ndocs", C.c_uint32), ("vocab_capacity", C.c_uint32), ("ms_total", C.c_double),
         ("ms_tokcount", C.c_double), ("ms_stage", C.c_double * 16), ("nstages", C.c_uint32), ("flags", C.c_uint32),
         ("device_allocs", C.c_uint64), ("device_alloc_bytes", C.c_uint64),
+    ]
+
+
+class OutputInfo(C.Structure):
+    _fields_ = [
+        ("size", C.c_uint64), ("text_bytes", C.c_uint64), ("writers", C.c_uint32), ("formatted", C.c_uint32),
+        ("ms_prepare", C.c_double), ("ms_d2h_busy", C.c_double), ("ms_write", C.c_double), ("ms_total", C.c_double),
     ]
 
 
@@ -111,6 +119,7 @@ def lib() -> C.CDLL:
         L.tfidf_format.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         L.tfidf_copy_text.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64]
         L.tfidf_write_output_gpu.argtypes = [C.c_void_p, C.c_char_p, C.c_int]
+        L.tfidf_last_output_info.argtypes = [C.c_void_p, C.POINTER(OutputInfo)]
         L.tfidf_format_f64.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
         L.tfidf_synth_host.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.c_uint32, C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p]
@@ -288,6 +297,13 @@ class Engine:
 
     def write_output(self, path: str, append: bool = False):
         _chk(lib().tfidf_write_output_gpu(self.h, path.encode(), 1 if append else 0), "tfidf_write_output_gpu")
+
+    def output_info(self) -> dict:
+        """Timings of the last write_output (tfidf_last_output_info)."""
+        o = OutputInfo()
+        o.size = C.sizeof(OutputInfo)
+        _chk(lib().tfidf_last_output_info(self.h, C.byref(o)), "tfidf_last_output_info")
+        return {k: getattr(o, k) for k, _ in OutputInfo._fields_ if k != "size"}
 
     def format_f64(self, vals) -> list:
         """The device %.16f formatter on host doubles (tests)."""
