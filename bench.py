@@ -206,6 +206,7 @@ def main_shards(args):
         "exchange_ms": round(st_max.get("exchange", 0.0), 4),
         "exchange_ms_min_over_ranks": round(xmin, 4),
         "exchange_frac_of_step": round(st_max.get("exchange", 0.0) / (elapsed / args.steps * 1e3), 4),
+        "exchange_mode": "dense all-reduce" if infos[0]["flags"] & tfidf_abi.RUN_XCHG_DENSE else "hash-owner all-to-all",
         "nterms_global": int(infos[0]["nterms_global"]),
         "nterms_per_rank": [int(i["nterms"]) for i in infos],
         "device_allocs_in_timed_steps": a1[0] - a0[0],
@@ -286,14 +287,15 @@ def main_group(args):
         "config": {"workload": f"{args.config}: {sum(len(p['doc_ids']) for p in plans)} docs over {N} GPUs, "
                                f"V={plans[0]['V']}, {C_all / 1e9:.3f} GB, {int(P_all)} pairs",
                    "docs_total": int(plans[0]["ndocs_total"]), "corpus_bytes_total": int(C_all),
-                   "parallelism": f"doc-shard x{N}, one process (tfidf_group: RCCL clique, hash-owner DF "
-                                  f"exchange over xGMI)"},
+                   "parallelism": f"doc-shard x{N}, one process (tfidf_group: RCCL clique, DF exchange over "
+                                  f"xGMI)"},
         "pairs_per_s": round(P_all * args.steps / elapsed, 1),
         "tokens_per_s": round(T_all * args.steps / elapsed, 1),
         "launcher": "in-process group (tfidf_group_open -> ncclCommInitAll)",
         "stage_ms_max_over_ranks_mean": {k: round(v, 4) for k, v in st_max.items()},
         "exchange_ms": round(st_max.get("exchange", 0.0), 4),
         "exchange_ms_min_over_ranks": round(xmin, 4),
+        "exchange_mode": "dense all-reduce" if i0["flags"] & tfidf_abi.RUN_XCHG_DENSE else "hash-owner all-to-all",
         "k1_ms_mean_over_ranks": round(float(np.mean(k1)), 4),
         "roofline": {"bound": "hbm", "kernel": f"{kern} (K1, rank 0)", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -183,8 +183,10 @@ typedef struct tfidf_run_info {
 #define TFIDF_RUN_K1_VS   2u  /* slot-keyed tokenize+count kernel (the default path; the general
                                  kernel of TFIDF_K1=general or an unaligned corpus leaves it clear) */
 #define TFIDF_RUN_K1_ST   4u  /* ... run as the LDS-staged persistent k_tokcount_st (TFIDF_K1=st) */
-#define TFIDF_RUN_K1_SL   8u  /* ... run as k_tokcount_sl, one workgroup per chunk (the default, vocabulary
-                                 table <= 4M slots); neither ST nor SL with VS set: k_tokcount_vs (larger tables) */
+#define TFIDF_RUN_K1_SL   8u  /* ... run as k_tokcount_sl (the default, vocabulary table <= 4M slots);
+                                 neither ST nor SL with VS set: k_tokcount_vs (larger tables) */
+#define TFIDF_RUN_XCHG_DENSE 16u  /* multi-rank: the DF exchange used the dense all-reduce form
+                                     (else the hash-owner all-to-all; single rank: no exchange) */
 int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info);
 /* The same device-allocation counters without a run (process-wide, cumulative). */
 int tfidf_alloc_stats(uint64_t* allocs, uint64_t* bytes);

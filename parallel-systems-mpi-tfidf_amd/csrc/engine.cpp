@@ -1274,7 +1274,8 @@ extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* out) {
     info->ms_tokcount = ctx->ms_stage[S_TOKCOUNT];
     for (int i = 0; i < S_NSTAGES; ++i) info->ms_stage[i] = ctx->ms_stage[i];
     info->nstages = S_NSTAGES;
-    info->flags = (ctx->k1_vs ? TFIDF_RUN_K1_VS : 0u) | (ctx->k1_st ? TFIDF_RUN_K1_ST : 0u) | (ctx->k1_sl ? TFIDF_RUN_K1_SL : 0u);
+    info->flags = (ctx->k1_vs ? TFIDF_RUN_K1_VS : 0u) | (ctx->k1_st ? TFIDF_RUN_K1_ST : 0u) | (ctx->k1_sl ? TFIDF_RUN_K1_SL : 0u) |
+                  (ctx->xp && ctx->last_dense ? TFIDF_RUN_XCHG_DENSE : 0u);
     info->device_allocs = g_dev_allocs.load(std::memory_order_relaxed);
     info->device_alloc_bytes = g_dev_alloc_bytes.load(std::memory_order_relaxed);
     full.size = want;

@@ -606,17 +606,18 @@ constexpr uint32_t DFH_MAXV = 65536;
 
 /* LDS-privatised DF histogram: 1024 threads (16 waves, the 100 KB bin array allows one
  * workgroup per CU).  Each thread owns 64 records of the workgroup's range and keeps
- * DFH_B of them in flight at once (slot loads, then rank gathers, then LDS adds): the
- * loop is latency-bound, so the number of dependent round trips is what matters. */
+ * DFH_B of them in flight at once (slot loads, then rank lookups, then LDS adds): the
+ * loop is latency-bound, so the number of dependent round trips is what matters.  The
+ * slot -> rank lookups go through a 16 KB direct-mapped LDS cache first (the frequent
+ * terms recur in every document of the workgroup's range); only its misses send a
+ * random L2 request into the 2-byte map (c2 DF 0.385 -> 0.344 ms, profiles/r04_k1_ab_c2.txt). */
 constexpr int DFH_NT = 1024;
 #ifndef DFH_B_N
 #define DFH_B_N 16
 #endif
 constexpr int DFH_B = DFH_B_N;
-#ifdef DFH_CACHE
 constexpr uint32_t DFH_CK = 2048;          /* LDS slot -> rank cache entries (16 KB) */
 __device__ __forceinline__ uint32_t dfh_cslot(uint32_t slot) { return (slot * 0x9E3779B1u) >> (32 - 11); }
-#endif
 __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ rec_slot, uint64_t nrec,
                                                         const uint32_t* __restrict__ nrec_extra,
                                                         const uint32_t* __restrict__ rank_of_slot,
@@ -627,14 +628,12 @@ __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ r
     extern __shared__ __attribute__((aligned(16))) uint32_t bins[]; /* V/2 words of two u16 counters */
     const uint32_t W = (V + 1) / 2;
     for (uint32_t k = threadIdx.x; k < W; k += DFH_NT) bins[k] = 0;
-#ifdef DFH_CACHE
     /* a direct-mapped LDS cache of slot -> rank behind the bins (one 64-bit word per entry:
      * (slot + 1) << 32 | rank, written and read whole): a workgroup's records repeat the
      * corpus's frequent terms in every document, so most rank lookups hit here instead of
      * sending a random L2 request */
     unsigned long long* cache = reinterpret_cast<unsigned long long*>(bins + ((W + 1) & ~1u));
     for (uint32_t k = threadIdx.x; k < DFH_CK; k += DFH_NT) cache[k] = 0ull;
-#endif
     __syncthreads();
     if (nrec_extra) nrec += *nrec_extra; /* merged partial records, counted on the device */
     const uint64_t r0 = (uint64_t)blockIdx.x * per;
@@ -646,9 +645,7 @@ __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ r
             const uint64_t k = i + (uint64_t)q * DFH_NT;
             sl[q] = k < r1 ? __builtin_nontemporal_load(&rec_slot[k]) : 0xFFFFFFFFu;
         }
-#ifdef DFH_CACHE
         uint32_t miss = 0;   /* bit q: record q's rank came from global memory */
-#endif
 #pragma unroll
         for (int q = 0; q < DFH_B; ++q) {
             const bool ranked = i + (uint64_t)q * DFH_NT >= ranked_from;   /* merged records hold ranks */
@@ -656,23 +653,15 @@ __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ r
                 atomicOr(status, ST_BOUNDS);
                 sl[q] = 0xFFFFFFFFu;
             }
-#ifdef DFH_CACHE
             if (sl[q] == 0xFFFFFFFFu || ranked) { r[q] = ranked ? sl[q] : 0u; continue; }
             const unsigned long long e = cache[dfh_cslot(sl[q])];
             if ((uint32_t)(e >> 32) == sl[q] + 1u) { r[q] = (uint32_t)e; continue; }
             miss |= 1u << q;
             r[q] = rank16 ? (uint32_t)rank16[sl[q]] : rank_of_slot[sl[q]];
-#else
-            /* V <= 65536: the 2-byte map (half the footprint of the 4-byte one: more of
-             * these random gathers hit L2) */
-            r[q] = sl[q] == 0xFFFFFFFFu ? 0u : ranked ? sl[q] : rank16 ? (uint32_t)rank16[sl[q]] : rank_of_slot[sl[q]];
-#endif
         }
-#ifdef DFH_CACHE
 #pragma unroll
         for (int q = 0; q < DFH_B; ++q)
             if ((miss >> q) & 1u) cache[dfh_cslot(sl[q])] = ((unsigned long long)(sl[q] + 1u) << 32) | r[q];
-#endif
 #pragma unroll
         for (int q = 0; q < DFH_B; ++q) {
             if (sl[q] == 0xFFFFFFFFu) continue;
@@ -849,11 +838,7 @@ int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra
                 hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
                 ncu = 256;
         }
-#ifdef DFH_CACHE
         const uint64_t wg_lds = (uint64_t)((W + 1) & ~1u) * 4 + (uint64_t)DFH_CK * 8;
-#else
-        const uint64_t wg_lds = (uint64_t)W * 4;
-#endif
         const uint64_t per_cu = (uint64_t)163840 / wg_lds >= 2 ? 2 : 1;   /* 1024-thread workgroups */
         const uint64_t slots = (uint64_t)ncu * per_cu;
         const uint64_t full = (nparts + slots - 1) / slots * slots;
@@ -864,11 +849,7 @@ int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra
         uint32_t* part = (uint32_t*)ar.get((size_t)nparts * W * 4);
         if (!part) return -2;
         if (hipMemsetAsync(df, 0, (size_t)V * 4, s) != hipSuccess) return -1;
-#ifdef DFH_CACHE
         const size_t lds = (size_t)((W + 1) & ~1u) * 4 + (size_t)DFH_CK * 8;
-#else
-        const size_t lds = (size_t)W * 4;
-#endif
         k_df_hist_lds<<<nparts, DFH_NT, lds, s>>>(rec_slot, nrec, nrec_extra, rank_of_slot, rank16, V, slot_cap,
                                                              ranked_from, status, per, part);
         k_df_colsum<<<dim3(grid_for(V), (nparts + DFC_G - 1) / DFC_G), NT, 0, s>>>(part, nparts, V, df);

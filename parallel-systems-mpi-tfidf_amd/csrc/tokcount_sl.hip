@@ -1,14 +1,16 @@
 /*
- * tokcount_sl.hip — K1: fused tokenize + per-document term counting, one workgroup per
- * chunk, straight-line token rounds.  Replaces the reference's per-rank hot loop
+ * tokcount_sl.hip — K1: fused tokenize + per-document term counting, persistent
+ * workgroups claiming chunks, straight-line token rounds.  Replaces the reference's per-rank hot loop
  * TFIDF.c:130-196: the two fscanf("%s") passes (:141-147), the O(P) strcmp search/append
  * of (word, doc) records (:151-167) and the per-rank word table (:169-188).
  *
  * The kernel is written for instruction issue, which is what bounds this stage on gfx950
  * (the LDS-staged kernel it replaces issued ~480 VALU + ~210 SALU
  * wave-instructions per 64 tokens, a third of them spill and exec-mask traffic):
- *   - one workgroup per K0 chunk (the hardware dispatcher is the scheduler): no claim
- *     loop, no cross-chunk prefetch state, nothing 64-bit live across the loops;
+ *   - four workgroups per CU stay resident and claim K0 chunks from a global counter, the
+ *     next claim sent when a chunk starts (chunk sizes vary: one workgroup per chunk
+ *     measured 2.90 ms on c2 for the per-workgroup set-up, a static share 2.46 for its tail,
+ *     the claim loop 1.94-1.97; profiles/r04_k1_ab_c2.txt);
  *   - corpus and vocabulary reads are buffer loads with 32-bit offsets from a per-chunk
  *     (corpus) or per-launch (vocabulary) resource: out-of-range lanes read zero instead of
  *     being clamped, and a probe's two slots are one address with offsets 0 and 16;
@@ -16,7 +18,8 @@
  *   - the vocabulary pair: terms are inserted from an even home slot (dev_vocab.h), so the
  *     two slots a round loads never wrap;
  *   - a round is a straight line for the common case (both vocabulary slots compared, the
- *     LDS bucket read, matched or claimed); the rare cases (vocabulary miss, a term of 16
+ *     LDS bucket read, one CAS and one add per lane whatever the outcome: branching on the
+ *     outcome measured 0.16 ms slower on c2); the rare cases (vocabulary miss, a term of 16
  *     bytes or more, a full bucket or a lost claim, overflow mode) run in out-of-line
  *     functions behind one wave-uniform test each;
  *   - docSize is counted per step in the walk (one scalar LDS add when the step lies in one
@@ -263,12 +266,7 @@ __device__ __forceinline__ uint32_t wave_agg_add_rtn(uint32_t* ctr, uint32_t idx
  * documents crossing the chunk, over K5's in-LDS sort size or with overflow records: the
  * partial stream) — any number of documents: per-document counts by wave-aggregated LDS
  * adds, a block scan, every entry written at its document's base + its rank. */
-#ifdef SL_INLINE_FLUSH
-#define SL_FLUSH_ATTR __forceinline__
-#else
-#define SL_FLUSH_ATTR __noinline__
-#endif
-__device__ SL_FLUSH_ATTR void sl_flush(SlShared& S, const K1Out* o, uint32_t gd0, uint32_t ng, uint32_t sb) {
+__device__ __forceinline__ void sl_flush(SlShared& S, const K1Out* o, uint32_t gd0, uint32_t ng, uint32_t sb) {
     const int tid = threadIdx.x;
     lds_barrier();
     if (tid < GCAP) { S.f.dcnt[tid] = 0; S.f.drun[tid] = 0; }
@@ -338,7 +336,7 @@ __device__ SL_FLUSH_ATTR void sl_flush(SlShared& S, const K1Out* o, uint32_t gd0
 /* The flush of a group of at most FEW documents (most chunks hold one or two): per-thread
  * 16-bit document counters and one block scan, no LDS atomics.  Same output as sl_flush. */
 constexpr uint32_t FEW = 8;
-__device__ SL_FLUSH_ATTR void sl_flush_few(SlShared& S, const K1Out* o, uint32_t gd0, uint32_t ng, uint32_t sb) {
+__device__ __forceinline__ void sl_flush_few(SlShared& S, const K1Out* o, uint32_t gd0, uint32_t ng, uint32_t sb) {
     const int tid = threadIdx.x;
     const int lane = tid & 63, w = tid >> 6;
     lds_barrier();
@@ -476,7 +474,6 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);   /* wave-uniform: scalar step loop */
     unsigned long long tokens_w = 0;
     bool clean = false;             /* the LDS table is clear (every flush clears what it emits) */
-#ifdef SL_PERSIST
     /* chunks are claimed from a global counter (their sizes vary: a static share leaves a
      * tail of the slowest workgroups); the next claim is sent when a chunk starts, so its
      * round trip is hidden behind the chunk */
@@ -487,17 +484,9 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
                           ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S.next_chunk >> 32)) << 32);
          chunk < c1;) {
     if (tid == 0) claim = c0 + atomicAdd(o->chunk_ctr, 1ull);
-#else
-    do {            /* one chunk per workgroup (`continue` leaves) */
-    const uint64_t chunk = c0 + blockIdx.x;
-#endif
     const uint64_t cs = chunk_start[chunk], ce = chunk_start[chunk + 1];
     const uint32_t dfirst = chunk_doc[chunk], dlast = chunk_doc[chunk + 1];
-#ifdef SL_PERSIST
     if (cs < ce) {
-#else
-    if (cs >= ce) continue;   /* an empty chunk (a shard shorter than the chunk grid) */
-#endif
 
     /* chunk base and the corpus buffer: byte at chunk-relative p is at buffer offset p + shift */
     const uint64_t b0 = cs & ~(uint64_t)15;
@@ -522,14 +511,8 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
      * (the chunk starts inside or at the start of its first document), so neither waits for
      * the other or for the clear. */
     const uint32_t ng0 = (dlast + 1 - dfirst) < gcap ? (dlast + 1 - dfirst) : gcap;
-#ifdef SL_NOEARLY
-    const uint64_t dpre = 0;
-    uint4 pf = make_uint4(0, 0, 0, 0);
-    (void)ng0;
-#else
     const uint64_t dpre = (uint32_t)tid <= ng0 ? c.doc_off[dfirst + tid] : 0ull;
     uint4 pf = bload16<2>(crs, wid * WSTEP + 16 * lane - 16 + shift);
-#endif
     /* table + selectors (once per workgroup) */
     if (!clean) {
         uint4* t = reinterpret_cast<uint4*>(S.TK);
@@ -546,11 +529,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
     for (uint32_t gd0 = dfirst; gd0 <= dlast; gd0 += gcap) {
         const uint32_t ng = (dlast + 1 - gd0) < gcap ? (dlast + 1 - gd0) : gcap;
         for (uint32_t k = tid; k <= ng; k += NT) {
-#ifdef SL_NOEARLY
-            const uint64_t d = c.doc_off[gd0 + k];
-#else
             const uint64_t d = (gd0 == dfirst && k == (uint32_t)tid) ? dpre : c.doc_off[gd0 + k];
-#endif
             S.gdoc[k] = d < b0 ? -64 : (d - b0 > (uint64_t)span + 64 ? span + 64 : (int32_t)(d - b0));
         }
         if (tid < GCAP) { S.dsz[tid] = 0; S.dpart[tid] = 0; }
@@ -632,16 +611,9 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
             const bool claim = key != 0u && !found && n < BW && !over;
             const uint32_t idx = BW * b + (found ? j : (n & (BW - 1u)));
             /* only a new key waits for an LDS round trip (its CAS); a match adds at once */
-#ifdef SL_CAS_ALL
             const uint32_t old = atomicCAS(&S.TK[idx], hit ? key : (claim ? 0u : 0x7FFFFFFFu), key);
             const bool ok = hit || (claim && (old == 0u || old == key));
             atomicAdd(&S.TC[idx], ok ? 1u : 0u);
-#else
-            uint32_t old = key;
-            if (claim) old = atomicCAS(&S.TK[idx], 0u, key);
-            const bool ok = hit || (claim && (old == 0u || old == key));
-            if (ok) atomicAdd(&S.TC[idx], 1u);
-#endif
             const bool claimed = claim && old == 0u;
             const bool slow = key != 0u && !ok;
             uint32_t claims = claimed ? 1u : 0u;
@@ -655,11 +627,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
             const int32_t bs = gs & ~15;
             const int32_t nsteps = (ge - bs + WSTEP - 1) / WSTEP;
             const bool inner_all = bs >= lo_rel + 16 && bs + nsteps * WSTEP + 16 <= hi_rel;
-#ifdef SL_NOEARLY
-            pf = bload16<2>(crs, bs + wid * WSTEP + 16 * lane - 16 + shift);
-#else
             if (gd0 != dfirst || bs != 0) pf = bload16<2>(crs, bs + wid * WSTEP + 16 * lane - 16 + shift);
-#endif
             uint32_t wr = 0;                    /* wave-uniform: document containing the step start */
             int32_t wcur = g0, wnext = ng > 1 ? __builtin_amdgcn_readfirstlane(S.gdoc[1]) : gn;
             for (int32_t s = wid; s < nsteps; s += NWAVE) {
@@ -669,12 +637,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
                 pf = bload16<2>(crs, gpos + NWAVE * WSTEP + shift);   /* next step (harmless past ge) */
                 reinterpret_cast<uint4*>(stage)[lane] = cur;
                 uint32_t lt9 = 0;
-#ifdef SL_OLDWS
-                uint32_t ws = ws_mask16_swar(cur);
-                lt9 = zero_bits(cur.x) | zero_bits(cur.y) | zero_bits(cur.z) | zero_bits(cur.w);
-#else
                 uint32_t ws = ws_mask16_dot(cur, lt9);
-#endif
                 if (!inner_all) ws |= outside16(gpos, lo_rel, hi_rel);
                 /* document starts in the window [sbp - 16, sbp + WSTEP + 16), the document
                  * of each lane's first byte; most steps hold none */
@@ -710,30 +673,6 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
                 tokens_w += ntok;
                 if (!multi && lane == 0) atomicAdd(&S.dsz[wr], ntok);   /* the whole step is in document wr */
                 for (uint32_t tb = 0; tb < ntok; tb += TLW) {
-#ifdef SL_ENT2
-                    {
-                        /* the k-th start of every lane per pass, all lanes in step (a wave-uniform
-                         * loop over the largest start count: no per-lane loop control) */
-                        uint32_t sm = starts, idx = incl - nmine - tb;
-                        while (__ballot(sm != 0u) != 0ull) {
-                            const bool act = sm != 0u;
-                            const uint32_t i = (uint32_t)__builtin_ctz(sm | 0x10000u);
-                            sm &= sm - 1u;
-                            const uint32_t e = ((stop32 >> i) & ~1u) | (nul32 >> i);
-                            const uint32_t len = (uint32_t)__builtin_ctz(e | 0x80000000u);   /* >= 31: none */
-                            uint32_t rel = base;
-                            if (multi) {
-                                if (act && (ds & ((2u << i) - 1u)))
-                                    while (rel + 1 < ng && S.gdoc[rel + 1] <= gpos + (int32_t)i) ++rel;
-                            }
-                            if (act && idx < (uint32_t)TLW) {
-                                tl[idx] = ((uint32_t)lane << 4 | i) | ((len < 16u ? len : LEN_LONG) << 10) | (rel << 16);
-                                if (multi) atomicAdd(&S.dsz[rel], 1u);
-                            }
-                            idx += act ? 1u : 0u;
-                        }
-                    }
-#else
                     {
                         uint32_t sm = starts, idx = incl - nmine;
                         while (sm) {
@@ -751,7 +690,6 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
                             ++idx;
                         }
                     }
-#endif
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -791,9 +729,6 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
                             fill = 0u;
                         }
                     }
-#ifdef SL_NOCARRY
-                    if (fill) { finish(pend); promote(pend, acc); acc.kind = 0u; fill = 0u; }
-#endif
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -817,16 +752,12 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
         lds_barrier();
         if (gd0 + gcap < gd0) break;   /* overflow guard */
     }
-#ifdef SL_PERSIST
     }   /* cs < ce */
     if (tid == 0) S.next_chunk = claim;
     lds_barrier();
     chunk = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S.next_chunk) |
             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S.next_chunk >> 32)) << 32);
     }   /* chunk */
-#else
-    } while (0);
-#endif
     if (lane == 0 && tokens_w) atomicAdd(o->ntokens, tokens_w);
 }
 
@@ -838,7 +769,6 @@ int launch_tokcount_sl(const CorpusDev& c, const uint64_t* chunk_start, const ui
     static_assert(TB % NT == 0 && TB % BW == 0, "table rows");
     const uint32_t sbits = (uint32_t)__builtin_popcountll(v.mask);
     const uint32_t gcap = (1u << (31u - sbits)) >= (uint32_t)GCAP ? (uint32_t)GCAP : (1u << (31u - sbits));
-#ifdef SL_PERSIST
     static int ncu = 0;
     if (!ncu) {
         int dev = 0;
@@ -849,11 +779,5 @@ int launch_tokcount_sl(const CorpusDev& c, const uint64_t* chunk_start, const ui
     const uint64_t wgs = (uint64_t)ncu * WG_PER_CU;
     const uint64_t grid = (c1 - c0) < wgs ? (c1 - c0) : wgs;
     k_tokcount_sl<<<(unsigned)grid, NT, 0, s>>>(c, chunk_start, chunk_doc, c0, c1, v, o_dev, sbits, gcap);
-#else
-    for (uint64_t a = c0; a < c1; a += 0x7FFFFFFFull) {   /* gridDim.x < 2^31 */
-        const uint64_t n = (c1 - a) < 0x7FFFFFFFull ? (c1 - a) : 0x7FFFFFFFull;
-        k_tokcount_sl<<<(unsigned)n, NT, 0, s>>>(c, chunk_start, chunk_doc, a, a + n, v, o_dev, sbits, gcap);
-    }
-#endif
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
