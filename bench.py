@@ -430,7 +430,7 @@ def main():
                 "first_call": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in oi1.items()},
                 "second_call": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in oi2.items()},
                 "note": "GPU %.16f formatting in 8 document groups overlapped with the D2H through a "
-                        "4 x 32 MB pinned ring (first call, incl. pinning the ring), then the D2H alone; "
+                        "8 x 16 MB pinned ring (first call, incl. pinning the ring), then the D2H alone; "
                         "written to /dev/null; not in value"}
 
     if dist is not None:

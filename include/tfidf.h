@@ -216,7 +216,7 @@ int tfidf_copy_text(tfidf_ctx* ctx, uint64_t off, void* dst, uint64_t n);
 /* tfidf_format + D2H + write to `path` (TFIDF.c:274-282); append != 0 appends (a shard
  * after the previous ones).  An unformatted result is formatted in document groups whose
  * D2H copies overlap the next group's formatting; the copies go through the context's
- * ring of pinned 32 MB buffers (kept across calls) and a regular file is written by
+ * ring of pinned 16 MB buffers (kept across calls) and a regular file is written by
  * several threads at their blocks' offsets (pwrite).  TFIDF_E_OUTPUT when the file
  * cannot be opened or written. */
 int tfidf_write_output_gpu(tfidf_ctx* ctx, const char* path, int append);

@@ -183,13 +183,13 @@ struct tfidf_ctx {
     const uint32_t* run_merged = nullptr;
     /* output text (emit.hip) */
     DevBuf t_key, t_len, doc_tbytes, doc_toff, text;
-#define WR_NBUF 4
-#define WR_BUF (32ull << 20)
+#define WR_NBUF 8
+#define WR_BUF (16ull << 20)
 #define WR_GROUPS 8
-    uint8_t* wr_buf[WR_NBUF] = {nullptr, nullptr, nullptr, nullptr};   /* pinned output staging ring */
+    uint8_t* wr_buf[WR_NBUF] = {};   /* pinned output staging ring */
     hipEvent_t wr_ev[WR_NBUF] = {};
     hipEvent_t wr_fmt[WR_GROUPS] = {};
-#define WR_WRITERS 4
+#define WR_WRITERS 8   /* page-cache writes run ~3 GB/s per thread (profiles/r04_cli_c2.json) */
     tfidf_output_info out_info{};
     uint64_t text_bytes = 0;
     bool text_valid = false;
@@ -1543,8 +1543,8 @@ extern "C" int tfidf_copy_text(tfidf_ctx* ctx, uint64_t off, void* dst, uint64_t
 }
 
 /* output.txt (TFIDF.c:274-282): the text leaves HBM through a ring of WR_NBUF pinned
- * staging buffers owned by the context (allocated on first use and kept: pinning 128 MB
- * costs tens of ms per call).  The copies run on stream2 while the host writes the
+ * 16 MB staging buffers owned by the context (allocated on first use and kept: pinning
+ * 128 MB costs ~20 ms per call).  The copies run on stream2 while the host writes the
  * buffers already copied; when the text is not yet formatted, the formatter runs in
  * WR_GROUPS document groups on the main stream and each copy waits only for the group
  * that holds its last byte, so formatting of group g+1 overlaps the copy of group g. */

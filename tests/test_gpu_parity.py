@@ -371,7 +371,7 @@ def test_gpu_text_c2_slice_vs_oracle(engine):
 def test_gpu_output_file_grouped_format(engine, tmp_path):
     """tfidf_write_output_gpu on an unformatted result formats in document groups whose
     copies overlap the next group's formatting (groups share 16-byte chunks at their
-    boundaries): the file equals the oracle's output.txt, several 32 MB staging blocks
+    boundaries): the file equals the oracle's output.txt, several 16 MB staging blocks
     deep, and a second write of the now formatted text equals it too."""
     p = tfidf_configs.plan("c2", scale=0.02)          # ~19 MB corpus -> ~45 MB of text
     data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
