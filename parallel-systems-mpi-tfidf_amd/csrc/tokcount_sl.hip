@@ -26,7 +26,8 @@
  *     document), the LDS table's fill per wave in a scalar register.
  *
  * Work inside a chunk: the four waves run without block barriers, wave w taking the
- * 992-byte steps w, w+4, ...; each lane classifies 16 bytes (SWAR C-locale isspace,
+ * 992-byte step w first and then the next unclaimed one from an LDS counter (a static
+ * w, w+4, ... share left the other waves waiting at the flush for the slowest); each lane classifies 16 bytes (SWAR C-locale isspace,
  * TFIDF.c:142,147, and NUL: strcmp stops there, :152,172), the lane owning a token start
  * writes a 32-bit token entry (stage offset | term length | document in group), and the
  * wave resolves its entries in rounds of 64 (one token per lane): one unaligned
@@ -60,7 +61,10 @@ constexpr int GCAP = 256;               /* documents per group at most */
 constexpr int TLW = 192;                /* token entries per wave and pass */
 constexpr uint32_t LEN_LONG = 31u;
 constexpr uint32_t SLOT_BITS = 22;      /* vocabulary slots < 2^22 (K1_ST_MAX_CAP) */
-constexpr int PMAX = 16;                /* LDS buckets probed before a key becomes a partial record */
+constexpr int PMAX = 16;
+#ifdef SL_STAMPS
+constexpr int SL_NPH = 9;               /* diagnostic phases (SL_STAMPS) */
+#endif                /* LDS buckets probed before a key becomes a partial record */
 
 struct SlShared {
     uint32_t TK[TB];                    /* key32 = 1 << 31 | doc-in-group << sb | slot (0: empty) */
@@ -86,6 +90,7 @@ struct SlShared {
     uint32_t wsum[NWAVE];
     unsigned long long rec_base, part_base;
     unsigned long long next_chunk;      /* persistent form: the workgroup's next chunk (claimed ahead) */
+    uint32_t step_next;                 /* the group's next unclaimed step */
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -474,6 +479,21 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);   /* wave-uniform: scalar step loop */
     unsigned long long tokens_w = 0;
     bool clean = false;             /* the LDS table is clear (every flush clears what it emits) */
+#ifdef SL_STAMPS
+    /* diagnostic build: per-wave s_memtime cycles per phase (0 chunk set-up, 1 walk,
+     * 2 token list, 3 round build, 4 round finish + loads, 5 the group's last rounds,
+     * 6 chunk end, 7 waiting for the other waves before the flush, 8 flush) */
+    unsigned long long st_acc[SL_NPH] = {};
+    unsigned long long st_t = __builtin_amdgcn_s_memtime(), st_chunks = 0;
+#define SL_STAMP(k)                                                         \
+    do {                                                                    \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();         \
+        st_acc[k] += t_ - st_t;                                             \
+        st_t = t_;                                                          \
+    } while (0)
+#else
+#define SL_STAMP(k) do {} while (0)
+#endif
     /* chunks are claimed from a global counter (their sizes vary: a static share leaves a
      * tail of the slowest workgroups); the next claim is sent when a chunk starts, so its
      * round trip is hidden behind the chunk */
@@ -486,6 +506,9 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
     if (tid == 0) claim = c0 + atomicAdd(o->chunk_ctr, 1ull);
     const uint64_t cs = chunk_start[chunk], ce = chunk_start[chunk + 1];
     const uint32_t dfirst = chunk_doc[chunk], dlast = chunk_doc[chunk + 1];
+#ifdef SL_STAMPS
+    ++st_chunks;
+#endif
     if (cs < ce) {
 
     /* chunk base and the corpus buffer: byte at chunk-relative p is at buffer offset p + shift */
@@ -533,12 +556,14 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
             S.gdoc[k] = d < b0 ? -64 : (d - b0 > (uint64_t)span + 64 ? span + 64 : (int32_t)(d - b0));
         }
         if (tid < GCAP) { S.dsz[tid] = 0; S.dpart[tid] = 0; }
+        if (tid == 0) S.step_next = NWAVE;
         lds_barrier();
         if ((uint32_t)tid < ng) S.dfull[tid] = S.gdoc[tid] >= cs_rel && S.gdoc[tid + 1] <= span;
         const int32_t g0 = __builtin_amdgcn_readfirstlane(S.gdoc[0]);
         const int32_t gn = __builtin_amdgcn_readfirstlane(S.gdoc[ng]);
         const int32_t gs = g0 > cs_rel ? g0 : cs_rel;
         const int32_t ge = gn < span ? gn : span;
+        SL_STAMP(0);
 
         Round pend, acc;
         pend.kind = 0;
@@ -630,11 +655,18 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
             if (gd0 != dfirst || bs != 0) pf = bload16<2>(crs, bs + wid * WSTEP + 16 * lane - 16 + shift);
             uint32_t wr = 0;                    /* wave-uniform: document containing the step start */
             int32_t wcur = g0, wnext = ng > 1 ? __builtin_amdgcn_readfirstlane(S.gdoc[1]) : gn;
-            for (int32_t s = wid; s < nsteps; s += NWAVE) {
+            /* steps claimed from an LDS counter (wave w's first step is w): the waves of a
+             * chunk finish within one step of each other whatever their steps cost */
+            for (int32_t s = wid, snext = wid; s < nsteps; s = snext) {
+                {
+                    uint32_t nx = 0;
+                    if (lane == 0) nx = atomicAdd(&S.step_next, 1u);
+                    snext = __builtin_amdgcn_readfirstlane((int)nx);
+                }
                 const int32_t sbp = bs + s * WSTEP;              /* first owned byte */
                 const int32_t gpos = sbp + 16 * lane - 16;       /* this lane's group */
                 const uint4 cur = pf;
-                pf = bload16<2>(crs, gpos + NWAVE * WSTEP + shift);   /* next step (harmless past ge) */
+                pf = bload16<2>(crs, bs + snext * WSTEP + 16 * lane - 16 + shift);   /* next step (harmless past ge) */
                 reinterpret_cast<uint4*>(stage)[lane] = cur;
                 uint32_t lt9 = 0;
                 uint32_t ws = ws_mask16_dot(cur, lt9);
@@ -669,6 +701,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
                 const uint32_t nmine = (uint32_t)__popc(starts);
                 const uint32_t incl = wave_incl_scan(nmine);
                 const uint32_t ntok = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                SL_STAMP(1);
                 if (ntok == 0) continue;
                 tokens_w += ntok;
                 if (!multi && lane == 0) atomicAdd(&S.dsz[wr], ntok);   /* the whole step is in document wr */
@@ -694,6 +727,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                     const uint32_t cnt = (ntok - tb) < (uint32_t)TLW ? (ntok - tb) : (uint32_t)TLW;
+                    SL_STAMP(2);
                     /* rounds are filled across steps: lanes [0, fill) of acc hold tokens built
                      * from earlier steps (their bytes already read, their vocabulary loads sent),
                      * so every counted round is a full 64 except the group's last */
@@ -723,10 +757,12 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
                             /* count the previous round, then send this one's vocabulary loads
                              * straight into the registers that round just released: a loaded
                              * value is never copied (a copy would wait for the load at once) */
+                            SL_STAMP(3);
                             finish(pend);
                             promote(pend, acc);
                             acc.kind = 0u;
                             fill = 0u;
+                            SL_STAMP(4);
                         }
                     }
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -735,11 +771,17 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
                 }
             }
         }
+        SL_STAMP(3);
         if (fill) {   /* the group's last, partial round */
             finish(pend);
             promote(pend, acc);
         }
         finish(pend);   /* drain */
+#ifdef SL_STAMPS
+        SL_STAMP(5);
+        lds_barrier();   /* (the flush's first barrier, made explicit to time the wait) */
+        SL_STAMP(7);
+#endif
         if (ng <= FEW) sl_flush_few(S, o, gd0, ng, sb);
         else sl_flush(S, o, gd0, ng, sb);
         if ((uint32_t)tid < ng) {
@@ -750,6 +792,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
             }
         }
         lds_barrier();
+        SL_STAMP(8);
         if (gd0 + gcap < gd0) break;   /* overflow guard */
     }
     }   /* cs < ce */
@@ -757,8 +800,17 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
     lds_barrier();
     chunk = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S.next_chunk) |
             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S.next_chunk >> 32)) << 32);
+    SL_STAMP(6);
     }   /* chunk */
     if (lane == 0 && tokens_w) atomicAdd(o->ntokens, tokens_w);
+#ifdef SL_STAMPS
+    SL_STAMP(6);
+    if (lane == 0 && o->stamps) {
+        for (int k = 0; k < SL_NPH; ++k) atomicAdd(&o->stamps[k], st_acc[k]);
+        atomicAdd(&o->stamps[SL_NPH], st_chunks);
+        atomicAdd(&o->stamps[SL_NPH + 1], 1ull);
+    }
+#endif
 }
 
 int launch_tokcount_sl(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc, uint64_t c0,

@@ -1,6 +1,6 @@
-"""K1 phase cycles (diagnostic build lib/libtfidf_hip_stamps.so, tokcount_st.hip K1_STAMPS):
-per-wave average s_memtime cycles per phase (tokcount_st.hip K1_STAMPS), over
-one c2 run.  Usage (GPU box): TFIDF_LIB=stamps TFIDF_STAMPS=1 python scripts/k1_stamps.py"""
+"""K1 phase cycles (diagnostic build lib/libtfidf_hip_stamps.so, tokcount_sl.hip SL_STAMPS):
+per-wave average s_memtime cycles per phase, summed over three runs of one config.
+Usage (GPU box): TFIDF_LIB=stamps TFIDF_STAMPS=1 python scripts/k1_stamps.py [config]"""
 import ctypes as C
 import os
 import sys
@@ -19,10 +19,11 @@ with tfidf_abi.Engine(0) as e:
     for _ in range(3):
         e.run_corpus(c)
     info = e.info()
-    buf = (C.c_uint64 * 22)()
-    n = L.tfidf_debug_k1_stamps(e.h, buf, 22)
+    buf = (C.c_uint64 * 32)()
+    n = L.tfidf_debug_k1_stamps(e.h, buf, 32)
     v = list(buf)[:n]
-names = ["setup", "walk", "rounds", "drain", "flush wait", "flush", "chunk end"]
+names = ["chunk setup", "walk", "token list", "round build", "round finish", "last rounds", "chunk end",
+         "flush wait", "flush"]
 NPH = len(names)
 waves = v[NPH + 1] or 1
 tot = sum(v[:NPH])
