@@ -413,8 +413,11 @@ hipStream_t tfidf_ctx_stream(const tfidf_ctx* ctx) { return ctx->stream; }
  *             ranks' term keys are all-gathered (padded to the largest V), every rank numbers
  *             the distinct keys identically (smallest gathered position), scatters its local
  *             df into a dense vector over those numbers, and ONE all-reduce (sum) gives every
- *             rank the global df; global V = the distinct keys.  One words agreement on the
- *             allocations, one all-gather, one all-reduce.
+ *             rank the global df; global V = the distinct keys.  Its buffers are sized
+ *             before step 1 from the rank's own V (padded by a quarter), so their allocation
+ *             status travels in step 1's word; only when the largest V exceeds some rank's
+ *             padding do all ranks grow them and agree once more.  Then one all-gather and
+ *             one all-reduce: one host synchronisation in all (step 1's).
  *      owner  (larger V: c4) — SURVEY §8e's hash-owner partitioning: every term goes to an
  *             owner rank (a hash of its key); the per-owner counts are all-gathered together
  *             with each rank's allocation status (an allocation failure is agreed there, no
@@ -547,30 +550,47 @@ static int exchange_owner(tfidf_ctx* ctx, uint32_t V, const std::vector<uint64_t
     return 0;
 }
 
+/* The dense form's buffers for gathers of R blocks of `maxv` keys.  Sized before the
+ * agreement from this rank's own V (padded: dense_pad) so that, when every rank's padded V
+ * covers the largest V, no second agreement is needed (allocation failures travel in the
+ * agreement's status word). */
+static uint64_t dense_pad(uint64_t v) { return v + v / 4 + 64; }
+static int dense_alloc(tfidf_ctx* ctx, uint32_t V, uint64_t maxv, uint64_t R) {
+    const uint64_t n = R * maxv, sumv = R * maxv;
+    if (ctx->x_mine.ensure(maxv * 16 + 16) || ctx->x_gkeys.ensure(n * 16 + 16) ||
+        ctx->x_tkey.ensure(table_cap(sumv) * 16) || ctx->x_tdf.ensure(table_cap(sumv) * 4) ||
+        ctx->x_pos.ensure((size_t)V * 4 + 4) || ctx->x_dense.ensure(n * 4 + 4))
+        return TFIDF_E_NOMEM;
+    return 0;
+}
+
 /* the dense form (step 2 above) */
 static int exchange_dense(tfidf_ctx* ctx, uint32_t V, const std::vector<uint64_t>& vs, bool* agreed) {
     hipStream_t s = ctx->stream;
     Xport* xp = ctx->xp;
     const int R = xp->nranks, me = xp->rank;
     unsigned long long* cnt = ctx->counters.as<unsigned long long>();
-    uint64_t maxv = 1, sumv = 0;
-    for (uint64_t x : vs) { maxv = x > maxv ? x : maxv; sumv += x; }
-    const uint64_t n = (uint64_t)R * maxv;   /* gathered positions */
-    int arc = 0;
-    auto ens = [&](DevBuf& b, size_t bytes) { if (!arc && b.ensure(bytes) != 0) arc = TFIDF_E_NOMEM; };
-    ens(ctx->x_mine, maxv * 16 + 16);
-    ens(ctx->x_gkeys, n * 16 + 16);
-    ens(ctx->x_tkey, table_cap(sumv) * 16);
-    ens(ctx->x_tdf, table_cap(sumv) * 4);   /* the shared positions of the table's keys */
-    ens(ctx->x_pos, (size_t)V * 4 + 4);
-    ens(ctx->x_dense, n * 4 + 4);
-    if (ctx->xnomem_rank == me) {   /* tests: an agreed allocation failure (once) */
-        ctx->xnomem_rank = -1;
-        arc = TFIDF_E_NOMEM;
+    uint64_t maxv = 1, sumv = 0, minpad = ~0ull;
+    for (uint64_t x : vs) {
+        maxv = x > maxv ? x : maxv;
+        sumv += x;
+        minpad = dense_pad(x) < minpad ? dense_pad(x) : minpad;
     }
-    int rc = exchange_agree(ctx, arc, 0, nullptr);
-    if (rc == 1) rc = TFIDF_E_STATE;
-    if (rc) { *agreed = true; return rc; }
+    const uint64_t n = (uint64_t)R * maxv;   /* gathered positions */
+    /* every rank sized its buffers for R blocks of dense_pad(its V) before the agreement
+     * (exchange_df); only when some rank's padding is short of the largest V do all ranks
+     * grow them and agree once more (the same decision on every rank: it depends on vs) */
+    if (maxv > minpad) {
+        int arc = dense_alloc(ctx, V, maxv, (uint64_t)R);
+        if (ctx->xnomem_rank == me) {   /* tests: an agreed allocation failure (once) */
+            ctx->xnomem_rank = -1;
+            arc = TFIDF_E_NOMEM;
+        }
+        int rc = exchange_agree(ctx, arc, 0, nullptr);
+        if (rc == 1) rc = TFIDF_E_STATE;
+        if (rc) { *agreed = true; return rc; }
+    }
+    int rc = 0;
     if (ctx->xfail_rank == me) {   /* tests: a rank-local failure after a collective (once) */
         ctx->xfail_rank = -1;
         fprintf(stderr, "tfidf: rank %d: injected exchange failure (TFIDF_TEST_XFAIL_RANK)\n", me);
@@ -599,6 +619,16 @@ static int exchange_dense(tfidf_ctx* ctx, uint32_t V, const std::vector<uint64_t
 
 static int exchange_df(tfidf_ctx* ctx, int local_rc, uint32_t V) {
     std::vector<uint64_t> vs;
+    /* the dense form's buffers, sized from this rank's V before the agreement (any failure
+     * is agreed in step 1: no extra exchange for it) */
+    if (local_rc == 0 && ctx->xchg_mode != 1 && V <= DENSE_XCHG_MAXV) {
+        int arc = dense_alloc(ctx, V, dense_pad(V), (uint64_t)ctx->xp->nranks);
+        if (ctx->xnomem_rank == ctx->xp->rank) {   /* tests: an agreed allocation failure (once) */
+            ctx->xnomem_rank = -1;
+            arc = TFIDF_E_NOMEM;
+        }
+        if (arc) local_rc = arc;
+    }
     int rc = exchange_agree(ctx, local_rc, V, &vs);   /* step 1 */
     if (rc) return rc;
     uint64_t maxv = 0;

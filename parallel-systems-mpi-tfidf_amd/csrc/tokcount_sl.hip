@@ -19,9 +19,12 @@
  *     two slots a round loads never wrap;
  *   - a round is a straight line for the common case (both vocabulary slots compared, the
  *     LDS bucket read, one CAS and one add per lane whatever the outcome: branching on the
- *     outcome measured 0.16 ms slower on c2); the rare cases (vocabulary miss, a term of 16
- *     bytes or more, a full bucket or a lost claim, overflow mode) run in out-of-line
- *     functions behind one wave-uniform test each;
+ *     outcome measured 0.16 ms slower on c2); a claim lost to another lane of the same
+ *     round (1.4 per round on c2: 64 lanes over 448 buckets) retries inline at the next
+ *     slots, and a full home bucket is probed once more inline at the next bucket (c2 K1
+ *     1.96 -> 1.76 ms: the out-of-line call had run in 69 % of the rounds); the rest
+ *     (vocabulary miss, a term of 16 bytes or more, overflow mode, 6 % of the rounds) runs
+ *     in out-of-line functions behind one wave-uniform test each;
  *   - docSize is counted per step in the walk (one scalar LDS add when the step lies in one
  *     document), the LDS table's fill per wave in a scalar register.
  *
@@ -150,6 +153,7 @@ __device__ __forceinline__ uint32_t bkt_hash(uint32_t key) {
 struct BktK {
     uint4 a, b;
 };
+__device__ __forceinline__ uint32_t bkt_slot(uint32_t b, uint32_t j) { return BW * b + j; }
 __device__ __forceinline__ BktK bkt_read(const uint32_t* TK, uint32_t b) {
     const uint4* t = reinterpret_cast<const uint4*>(TK) + 2 * b;
     BktK k;
@@ -193,13 +197,13 @@ __device__ __noinline__ uint32_t bkt_slow(uint32_t* TK, uint32_t* TC, uint8_t* d
     for (int probe = 0, tries = 0; probe < PMAX && tries < 64; ++tries) {
         const BktK kk = bkt_read(TK, b);
         const uint32_t j = bkt_match(kk, key);
-        if (j < BW) { atomicAdd(&TC[BW * b + j], 1u); return 0u; }
+        if (j < BW) { atomicAdd(&TC[bkt_slot(b, j)], 1u); return 0u; }
         const uint32_t e = bkt_fill(kk);   /* the first empty slot (hole-free bucket) */
         if (e < BW) {
             if (over) break;
-            const uint32_t old = atomicCAS(&TK[BW * b + e], 0u, key);
+            const uint32_t old = atomicCAS(&TK[bkt_slot(b, e)], 0u, key);
             if (old == 0u || old == key) {
-                atomicAdd(&TC[BW * b + e], 1u);
+                atomicAdd(&TC[bkt_slot(b, e)], 1u);
                 return old == 0u ? 1u : 0u;
             }
             continue;
@@ -485,6 +489,10 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
      * 6 chunk end, 7 waiting for the other waves before the flush, 8 flush) */
     unsigned long long st_acc[SL_NPH] = {};
     unsigned long long st_t = __builtin_amdgcn_s_memtime(), st_chunks = 0;
+    unsigned long long st_cnt[8] = {};   /* rounds with a slow lane, slow lanes, lost claims, rounds
+                                            still slow after the inline retries, rounds; lanes
+                                            still slow by cause (lost every retry, bucket full,
+                                            overflow mode) */
 #define SL_STAMP(k)                                                         \
     do {                                                                    \
         const unsigned long long t_ = __builtin_amdgcn_s_memtime();         \
@@ -634,13 +642,71 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
             const uint32_t n = bkt_fill(kk);
             const bool hit = key != 0u && found;
             const bool claim = key != 0u && !found && n < BW && !over;
-            const uint32_t idx = BW * b + (found ? j : (n & (BW - 1u)));
+            const uint32_t idx = bkt_slot(b, found ? j : (n & (BW - 1u)));
             /* only a new key waits for an LDS round trip (its CAS); a match adds at once */
             const uint32_t old = atomicCAS(&S.TK[idx], hit ? key : (claim ? 0u : 0x7FFFFFFFu), key);
             const bool ok = hit || (claim && (old == 0u || old == key));
             atomicAdd(&S.TC[idx], ok ? 1u : 0u);
-            const bool claimed = claim && old == 0u;
-            const bool slow = key != 0u && !ok;
+            bool claimed = claim && old == 0u;
+            bool slow = key != 0u && !ok;
+#ifdef SL_STAMPS
+            st_cnt[0] += __ballot(slow) != 0ull ? 1u : 0u;
+            st_cnt[1] += (uint32_t)__popcll(__ballot(slow));
+            st_cnt[2] += (uint32_t)__popcll(__ballot(claim && !ok));
+            ++st_cnt[4];
+#endif
+            /* claims lost to other lanes of this round (every lane read the bucket before any
+             * claimed, so the k-th winner took slot n + k - 1): inline claims of slots n + 1,
+             * then n + 2, without re-reading the bucket (a lost CAS returns the slot's key:
+             * the same key counts there) */
+            uint32_t nn = n;
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const bool lost = claim && slow && nn + 1u < BW;
+                if (__ballot(lost) == 0ull) break;
+                if (lost) {
+                    ++nn;
+                    const uint32_t i2 = bkt_slot(b, nn);
+                    const uint32_t o2 = atomicCAS(&S.TK[i2], 0u, key);
+                    if (o2 == 0u || o2 == key) {
+                        atomicAdd(&S.TC[i2], 1u);
+                        slow = false;
+                        claimed = o2 == 0u;
+                    }
+                }
+            }
+            /* the home bucket full without the key: one inline probe of the next bucket (a
+             * fresh read: match there, else claim its first empty slot) */
+            {
+                const bool full = slow && !claim && !over && key != 0u;
+                if (__ballot(full) != 0ull) {
+                    if (full) {
+                        const uint32_t b2 = b + 1u == NB ? 0u : b + 1u;
+                        const BktK k2 = bkt_read(S.TK, b2);
+                        const uint32_t j2 = bkt_match(k2, key);
+                        uint32_t e2 = j2;
+                        bool ok2 = j2 < BW;
+                        if (!ok2) {
+                            e2 = bkt_fill(k2);
+                            if (e2 < BW) {
+                                const uint32_t o2 = atomicCAS(&S.TK[bkt_slot(b2, e2)], 0u, key);
+                                ok2 = o2 == 0u || o2 == key;
+                                claimed = o2 == 0u;
+                            }
+                        }
+                        if (ok2) {
+                            atomicAdd(&S.TC[bkt_slot(b2, e2)], 1u);
+                            slow = false;
+                        }
+                    }
+                }
+            }
+#ifdef SL_STAMPS
+            st_cnt[3] += __ballot(slow) != 0ull ? 1u : 0u;
+            st_cnt[5] += (uint32_t)__popcll(__ballot(slow && claim));            /* lost every retry */
+            st_cnt[6] += (uint32_t)__popcll(__ballot(slow && !claim && !over));  /* bucket full */
+            st_cnt[7] += (uint32_t)__popcll(__ballot(slow && over));             /* overflow mode */
+#endif
             uint32_t claims = claimed ? 1u : 0u;
             if (__ballot(slow) != 0ull) {
                 if (slow) claims = bkt_slow(S.TK, S.TC, S.dpart, o, key, b, over, gd0, sb);
@@ -809,6 +875,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
         for (int k = 0; k < SL_NPH; ++k) atomicAdd(&o->stamps[k], st_acc[k]);
         atomicAdd(&o->stamps[SL_NPH], st_chunks);
         atomicAdd(&o->stamps[SL_NPH + 1], 1ull);
+        for (int k = 0; k < 8; ++k) atomicAdd(&o->stamps[SL_NPH + 2 + k], st_cnt[k]);
     }
 #endif
 }

@@ -30,3 +30,10 @@ tot = sum(v[:NPH])
 print(cfg, "K1 ms", round(info["ms_tokcount"], 4), "waves", waves, "chunk visits/wave", round(v[NPH] / waves, 1))
 for k, nm in enumerate(names):
     print("  %-12s %10.0f cycles/wave  %5.1f %%" % (nm, v[k] / waves, 100.0 * v[k] / max(tot, 1)))
+cnt = v[NPH + 2:NPH + 10]
+if len(cnt) == 8 and cnt[4]:
+    print("  rounds %d (per wave %.0f): with a slow lane %.1f %%, slow lanes/round %.2f, lost claims/round %.2f,"
+          " still slow after the inline retry %.1f %% (SL_RETRY builds)" %
+          (cnt[4], cnt[4] / waves, 100.0 * cnt[0] / cnt[4], cnt[1] / cnt[4], cnt[2] / cnt[4], 100.0 * cnt[3] / cnt[4]))
+    print("  lanes still slow per round: lost every retry %.3f, bucket full %.3f, overflow mode %.3f" %
+          (cnt[5] / cnt[4], cnt[6] / cnt[4], cnt[7] / cnt[4]))
