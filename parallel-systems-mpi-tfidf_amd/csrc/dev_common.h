@@ -184,6 +184,21 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 /* Workgroup barrier that orders LDS only.  __syncthreads() is a release/acquire fence over
  * all address spaces, so it also waits for every outstanding global store of the wave
  * (vmcnt(0)); kernels whose barriers only publish LDS data use this one. */
+/* A generic pointer known to address device memory, as a global-address-space pointer:
+ * stores through it compile to global_store (counted in vmcnt only) instead of flat_store,
+ * which also counts in lgkmcnt, so that every later LDS wait would wait for the store too
+ * (pointers loaded from memory, e.g. a K1Out block, are generic to the compiler). */
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gmem(T* p) {
+    return (__attribute__((address_space(1))) T*)p;
+}
+
+/* device-scope atomic add on device memory through a global-address-space pointer
+ * (global_atomic: a returning flat atomic would hold lgkmcnt until it returns) */
+__device__ __forceinline__ unsigned long long gatomic_add(unsigned long long* p, unsigned long long v) {
+    return __hip_atomic_fetch_add(gmem(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();

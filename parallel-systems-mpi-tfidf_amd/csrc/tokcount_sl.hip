@@ -66,7 +66,7 @@ constexpr uint32_t LEN_LONG = 31u;
 constexpr uint32_t SLOT_BITS = 22;      /* vocabulary slots < 2^22 (K1_ST_MAX_CAP) */
 constexpr int PMAX = 16;
 #ifdef SL_STAMPS
-constexpr int SL_NPH = 9;               /* diagnostic phases (SL_STAMPS) */
+constexpr int SL_NPH = 11;              /* diagnostic phases (SL_STAMPS) */
 #endif                /* LDS buckets probed before a key becomes a partial record */
 
 struct SlShared {
@@ -181,10 +181,10 @@ __device__ __noinline__ void overflow_record(const K1Out* o, uint32_t doc, uint3
     const uint64_t am = __ballot(1);
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u));
     unsigned long long b = 0;
-    if (rank == 0u) b = atomicAdd(o->part_alloc, (unsigned long long)__popcll(am));
+    if (rank == 0u) b = gatomic_add(o->part_alloc, (unsigned long long)__popcll(am));
     const unsigned long long q = (((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(b >> 32)) << 32) |
                                   (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b)) + rank;
-    if (q < o->part_cap) { o->part_doc[q] = doc; o->part_slot[q] = slot; o->part_cnt[q] = 1u; }
+    if (q < o->part_cap) { gmem(o->part_doc)[q] = doc; gmem(o->part_slot)[q] = slot; gmem(o->part_cnt)[q] = 1u; }
     else atomicOr(o->status, ST_PART_FULL);
 }
 
@@ -277,6 +277,11 @@ __device__ __forceinline__ uint32_t wave_agg_add_rtn(uint32_t* ctr, uint32_t idx
  * adds, a block scan, every entry written at its document's base + its rank. */
 __device__ __forceinline__ void sl_flush(SlShared& S, const K1Out* o, uint32_t gd0, uint32_t ng, uint32_t sb) {
     const int tid = threadIdx.x;
+    uint32_t* const rec_slot = o->rec_slot;   /* read once: see sl_flush_few */
+    uint32_t* const rec_cnt = o->rec_cnt;
+    uint32_t* const part_doc = o->part_doc;
+    uint32_t* const part_slot = o->part_slot;
+    uint32_t* const part_cnt = o->part_cnt;
     lds_barrier();
     if (tid < GCAP) { S.f.dcnt[tid] = 0; S.f.drun[tid] = 0; }
     lds_barrier();
@@ -299,7 +304,7 @@ __device__ __forceinline__ void sl_flush(SlShared& S, const K1Out* o, uint32_t g
             st = complete ? 2 : 1;
             packed = complete ? cnt : (cnt << 16);
         }
-        if (st == 1 || part) o->doc_flags[gd0 + tid] = DF_PARTIAL;
+        if (st == 1 || part) gmem(o->doc_flags)[gd0 + tid] = DF_PARTIAL;
         S.f.dstate[tid] = st;
     }
     uint32_t tot;
@@ -307,11 +312,11 @@ __device__ __forceinline__ void sl_flush(SlShared& S, const K1Out* o, uint32_t g
     if ((uint32_t)tid < ng) S.f.doff[tid] = off;
     const uint32_t nrec = tot & 0xFFFFu, npart = tot >> 16;
     if (tid == 0) {
-        const unsigned long long rb = nrec ? atomicAdd(o->rec_alloc, (unsigned long long)nrec) : 0ull;
+        const unsigned long long rb = nrec ? gatomic_add(o->rec_alloc, (unsigned long long)nrec) : 0ull;
         if (rb + nrec > o->rec_cap) atomicOr(o->status, ST_REC_FULL);
         S.rec_base = rb;
     } else if (tid == 64) {
-        const unsigned long long pb = npart ? atomicAdd(o->part_alloc, (unsigned long long)npart) : 0ull;
+        const unsigned long long pb = npart ? gatomic_add(o->part_alloc, (unsigned long long)npart) : 0ull;
         if (pb + npart > o->part_cap) atomicOr(o->status, ST_PART_FULL);
         S.part_base = pb;
     }
@@ -319,8 +324,8 @@ __device__ __forceinline__ void sl_flush(SlShared& S, const K1Out* o, uint32_t g
     const unsigned long long rb = S.rec_base, pb = S.part_base;
     const bool rec_ok = rb + nrec <= o->rec_cap, part_ok = pb + npart <= o->part_cap;
     if ((uint32_t)tid < ng && S.f.dstate[tid] == 2) {
-        o->doc_recoff[gd0 + tid] = rb + (off & 0xFFFFu);
-        o->doc_npairs[gd0 + tid] = S.f.dcnt[tid];
+        gmem(o->doc_recoff)[gd0 + tid] = rb + (off & 0xFFFFu);
+        gmem(o->doc_npairs)[gd0 + tid] = S.f.dcnt[tid];
     }
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
@@ -331,10 +336,10 @@ __device__ __forceinline__ void sl_flush(SlShared& S, const K1Out* o, uint32_t g
             const uint32_t dof = S.f.doff[rel];
             if (S.f.dstate[rel] == 2) {
                 const uint64_t q = rb + (dof & 0xFFFFu) + k;
-                if (rec_ok) { o->rec_slot[q] = key & smask; o->rec_cnt[q] = ec[j]; }
+                if (rec_ok) { gmem(rec_slot)[q] = key & smask; gmem(rec_cnt)[q] = ec[j]; }
             } else {
                 const uint64_t q = pb + (dof >> 16) + k;
-                if (part_ok) { o->part_doc[q] = gd0 + rel; o->part_slot[q] = key & smask; o->part_cnt[q] = ec[j]; }
+                if (part_ok) { gmem(part_doc)[q] = gd0 + rel; gmem(part_slot)[q] = key & smask; gmem(part_cnt)[q] = ec[j]; }
             }
             S.TK[j * NT + tid] = 0u;
             S.TC[j * NT + tid] = 0u;
@@ -345,9 +350,29 @@ __device__ __forceinline__ void sl_flush(SlShared& S, const K1Out* o, uint32_t g
 /* The flush of a group of at most FEW documents (most chunks hold one or two): per-thread
  * 16-bit document counters and one block scan, no LDS atomics.  Same output as sl_flush. */
 constexpr uint32_t FEW = 8;
-__device__ __forceinline__ void sl_flush_few(SlShared& S, const K1Out* o, uint32_t gd0, uint32_t ng, uint32_t sb) {
+#ifdef SL_STAMPS
+#define SLF_STAMP(k)                                                        \
+    do {                                                                    \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();         \
+        st_acc[k] += t_ - st_t;                                             \
+        st_t = t_;                                                          \
+    } while (0)
+#define SLF_ARGS , unsigned long long* st_acc, unsigned long long& st_t
+#else
+#define SLF_STAMP(k) do {} while (0)
+#define SLF_ARGS
+#endif
+__device__ __forceinline__ void sl_flush_few(SlShared& S, const K1Out* o, uint32_t gd0, uint32_t ng, uint32_t sb SLF_ARGS) {
     const int tid = threadIdx.x;
     const int lane = tid & 63, w = tid >> 6;
+    /* the output arrays' addresses read once (scalar loads): read at the stores, the
+     * per-lane choice between the two streams made the compiler load them per entry with
+     * vector loads and wait for each */
+    uint32_t* const rec_slot = o->rec_slot;
+    uint32_t* const rec_cnt = o->rec_cnt;
+    uint32_t* const part_doc = o->part_doc;
+    uint32_t* const part_slot = o->part_slot;
+    uint32_t* const part_cnt = o->part_cnt;
     lds_barrier();
     const uint32_t smask = (1u << sb) - 1u;
     uint32_t ek[EPT], ec[EPT];
@@ -368,6 +393,7 @@ __device__ __forceinline__ void sl_flush_few(SlShared& S, const K1Out* o, uint32
         inc[q] = wave_incl_scan(pk[q]);
         if (lane == 63) S.f.dcnt[w * (FEW / 2) + q] = inc[q];
     }
+    SLF_STAMP(9);
     lds_barrier();
     uint32_t rank[FEW / 2], tot[FEW / 2];
 #pragma unroll
@@ -396,15 +422,15 @@ __device__ __forceinline__ void sl_flush_few(SlShared& S, const K1Out* o, uint32
                 st = complete ? 2 : 1;
                 packed = complete ? cnt : (cnt << 16);
             }
-            if (st == 1 || part) o->doc_flags[gd0 + d] = DF_PARTIAL;
+            if (st == 1 || part) gmem(o->doc_flags)[gd0 + d] = DF_PARTIAL;
         }
         const uint32_t incl = wave_incl_scan(packed);
         const uint32_t all = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         const uint32_t off = incl - packed;
         const uint32_t nrec = all & 0xFFFFu, npart = all >> 16;
         unsigned long long a0 = 0, a1 = 0;
-        if (lane == 0 && nrec) a0 = atomicAdd(o->rec_alloc, (unsigned long long)nrec);
-        if (lane == 32 && npart) a1 = atomicAdd(o->part_alloc, (unsigned long long)npart);
+        if (lane == 0 && nrec) a0 = gatomic_add(o->rec_alloc, (unsigned long long)nrec);
+        if (lane == 32 && npart) a1 = gatomic_add(o->part_alloc, (unsigned long long)npart);
         const unsigned long long rb = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(a0 >> 32), 0) << 32) |
                                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a0, 0);
         const unsigned long long pb = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(a1 >> 32), 32) << 32) |
@@ -416,8 +442,8 @@ __device__ __forceinline__ void sl_flush_few(SlShared& S, const K1Out* o, uint32
             uint64_t fb = ~0ull;
             if (st == 2) {
                 fb = rec_ok ? rb + (off & 0xFFFFu) : ~0ull;
-                o->doc_recoff[gd0 + d] = rb + (off & 0xFFFFu);
-                o->doc_npairs[gd0 + d] = cnt;
+                gmem(o->doc_recoff)[gd0 + d] = rb + (off & 0xFFFFu);
+                gmem(o->doc_npairs)[gd0 + d] = cnt;
             } else if (st == 1) {
                 fb = part_ok ? pb + (off >> 16) : ~0ull;
             }
@@ -426,6 +452,7 @@ __device__ __forceinline__ void sl_flush_few(SlShared& S, const K1Out* o, uint32
         }
     }
     lds_barrier();
+    SLF_STAMP(10);
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
         const uint32_t key = ek[j];
@@ -441,8 +468,8 @@ __device__ __forceinline__ void sl_flush_few(SlShared& S, const K1Out* o, uint32
             const uint64_t fb = S.fbase[rel];
             if (fb != ~0ull) {
                 const uint64_t qq = fb + r;
-                if (S.f.dstate[rel] == 2) { o->rec_slot[qq] = key & smask; o->rec_cnt[qq] = ec[j]; }
-                else { o->part_doc[qq] = gd0 + rel; o->part_slot[qq] = key & smask; o->part_cnt[qq] = ec[j]; }
+                if (S.f.dstate[rel] == 2) { gmem(rec_slot)[qq] = key & smask; gmem(rec_cnt)[qq] = ec[j]; }
+                else { gmem(part_doc)[qq] = gd0 + rel; gmem(part_slot)[qq] = key & smask; gmem(part_cnt)[qq] = ec[j]; }
             }
             S.TK[j * NT + tid] = 0u;
             S.TC[j * NT + tid] = 0u;
@@ -486,7 +513,9 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
 #ifdef SL_STAMPS
     /* diagnostic build: per-wave s_memtime cycles per phase (0 chunk set-up, 1 walk,
      * 2 token list, 3 round build, 4 round finish + loads, 5 the group's last rounds,
-     * 6 chunk end, 7 waiting for the other waves before the flush, 8 flush) */
+     * 6 chunk end, 7 waiting for the other waves before the flush, 8 flush (few-document
+     * flushes: its record writes and clear), 9 flush entry counts, 10 flush record-space
+     * allocation and its barriers) */
     unsigned long long st_acc[SL_NPH] = {};
     unsigned long long st_t = __builtin_amdgcn_s_memtime(), st_chunks = 0;
     unsigned long long st_cnt[8] = {};   /* rounds with a slow lane, slow lanes, lost claims, rounds
@@ -505,13 +534,13 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
     /* chunks are claimed from a global counter (their sizes vary: a static share leaves a
      * tail of the slowest workgroups); the next claim is sent when a chunk starts, so its
      * round trip is hidden behind the chunk */
-    if (tid == 0) S.next_chunk = c0 + atomicAdd(o->chunk_ctr, 1ull);
+    if (tid == 0) S.next_chunk = c0 + gatomic_add(o->chunk_ctr, 1ull);
     lds_barrier();
     unsigned long long claim = 0;
     for (uint64_t chunk = (uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S.next_chunk) |
                           ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S.next_chunk >> 32)) << 32);
          chunk < c1;) {
-    if (tid == 0) claim = c0 + atomicAdd(o->chunk_ctr, 1ull);
+    if (tid == 0) claim = c0 + gatomic_add(o->chunk_ctr, 1ull);
     const uint64_t cs = chunk_start[chunk], ce = chunk_start[chunk + 1];
     const uint32_t dfirst = chunk_doc[chunk], dlast = chunk_doc[chunk + 1];
 #ifdef SL_STAMPS
@@ -848,12 +877,16 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
         lds_barrier();   /* (the flush's first barrier, made explicit to time the wait) */
         SL_STAMP(7);
 #endif
+#ifdef SL_STAMPS
+        if (ng <= FEW) sl_flush_few(S, o, gd0, ng, sb, st_acc, st_t);
+#else
         if (ng <= FEW) sl_flush_few(S, o, gd0, ng, sb);
+#endif
         else sl_flush(S, o, gd0, ng, sb);
         if ((uint32_t)tid < ng) {
             const uint32_t n = S.dsz[tid];
             if (n) {
-                if (S.dfull[tid]) o->doc_size[gd0 + tid] = n;
+                if (S.dfull[tid]) gmem(o->doc_size)[gd0 + tid] = n;
                 else atomicAdd(&o->doc_size[gd0 + tid], n);
             }
         }
