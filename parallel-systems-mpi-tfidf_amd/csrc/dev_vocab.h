@@ -25,10 +25,13 @@
  * loop that its wave's claimer might be scheduled behind); the wait is bounded.
  * Probing starts at the EVEN slot of the key's hash (home = hash & mask & ~1): the K1
  * kernels load a key's home pair (two 16-byte slots, one aligned 32-byte piece, never
- * wrapping) and find every key that sits in its home pair without a dependent load. */
+ * wrapping) and find every key that sits in its home pair without a dependent load.  A
+ * table probed by quads (HOME = ~3: four slots, one aligned 64-byte line) starts at a
+ * multiple of four instead; one run uses one form throughout. */
+template <uint64_t HOME = ~1ull>   /* home alignment: ~1 even pairs (tokcount_sl/st), ~3 quads */
 __device__ __forceinline__ uint32_t vocab_insert_s(uint4* __restrict__ keys, uint64_t* __restrict__ reps, uint64_t mask,
                                                 uint64_t klo, uint64_t khi, uint64_t rep, uint32_t* status) {
-    uint64_t h = key_hash(klo, khi) & mask & ~1ull;
+    uint64_t h = key_hash(klo, khi) & mask & HOME;
     uint32_t spins = 0;
     bool reread = false;
     for (uint32_t probe = 0; probe < VOCAB_MAX_PROBE && probe <= mask;) {
@@ -75,9 +78,10 @@ __device__ __forceinline__ uint32_t vocab_insert_s(uint4* __restrict__ keys, uin
     atomicOr(status, ST_VOCAB_FULL);
     return INVALID_SLOT;
 }
+template <uint64_t HOME = ~1ull>
 __device__ __forceinline__ uint32_t vocab_insert(const VocabDev& v, uint64_t klo, uint64_t khi, uint64_t rep,
                                                  uint32_t* status) {
-    return vocab_insert_s(v.keys, v.rep, v.mask, klo, khi, rep, status);
+    return vocab_insert_s<HOME>(v.keys, v.rep, v.mask, klo, khi, rep, status);
 }
 
 #endif

@@ -66,7 +66,7 @@ constexpr uint32_t LEN_LONG = 31u;
 constexpr uint32_t SLOT_BITS = 22;      /* vocabulary slots < 2^22 (K1_ST_MAX_CAP) */
 constexpr int PMAX = 16;
 #ifdef SL_STAMPS
-constexpr int SL_NPH = 11;              /* diagnostic phases (SL_STAMPS) */
+constexpr int SL_NPH = 12;              /* diagnostic phases (SL_STAMPS) */
 #endif                /* LDS buckets probed before a key becomes a partial record */
 
 struct SlShared {
@@ -515,7 +515,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
      * 2 token list, 3 round build, 4 round finish + loads, 5 the group's last rounds,
      * 6 chunk end, 7 waiting for the other waves before the flush, 8 flush (few-document
      * flushes: its record writes and clear), 9 flush entry counts, 10 flush record-space
-     * allocation and its barriers) */
+     * allocation and its barriers, 11 a round finish's wait for its loads) */
     unsigned long long st_acc[SL_NPH] = {};
     unsigned long long st_t = __builtin_amdgcn_s_memtime(), st_chunks = 0;
     unsigned long long st_cnt[8] = {};   /* rounds with a slow lane, slow lanes, lost claims, rounds
@@ -628,6 +628,12 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
             p.s1 = bload16<0>(vrs, (int32_t)(p.h << 4) + 16);
         };
         auto finish = [&](const Round& r) {
+#ifdef SL_STAMPS
+            /* diagnostic: the wait for the round's vocabulary loads (and, in order, every
+             * older or younger load still in flight) on its own */
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            SL_STAMP(11);
+#endif
             /* whole-key compares without short-circuit branches */
             const bool h0 = ((r.s0.x ^ r.k0) | (r.s0.y ^ r.k1) | (r.s0.z ^ r.k2) | (r.s0.w ^ r.k3)) == 0u;
             const bool h1 = ((r.s1.x ^ r.k0) | (r.s1.y ^ r.k1) | (r.s1.z ^ r.k2) | (r.s1.w ^ r.k3)) == 0u;

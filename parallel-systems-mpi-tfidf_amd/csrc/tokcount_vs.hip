@@ -53,6 +53,8 @@ constexpr int EPT = TB / NT;              /* table entries per thread in a flush
 constexpr uint32_t FILL_LIMIT = TB - NT * 2 - 64; /* claims after which overflow mode starts */
 constexpr int GCAP = 256;                 /* documents per group (doc-in-group: 8 bits) */
 constexpr uint32_t SLOT_BITS = 28;
+constexpr uint64_t VS_HOME = ~1ull;     /* even pairs (quads, one 64-byte line per key, measured slower:
+                                           c4 K1 4.92 -> 5.36 ms at 32M slots, 6.73 at 16M) */
 constexpr uint32_t CNT_BITS = 24;
 constexpr uint64_t CNT_MASK = (1ull << CNT_BITS) - 1ull;
 
@@ -149,14 +151,14 @@ __device__ __forceinline__ uint32_t slow_slot(const uint8_t* __restrict__ bytes,
             if (k < 8) lo |= b << (8 * k); else hi |= b << (8 * (k - 8));
         }
         make_short_key(lo, hi, (uint32_t)n, &klo, &khi);
-        return vocab_insert(v, klo, khi, 0, status);
+        return vocab_insert<VS_HOME>(v, klo, khi, 0, status);
     }
     make_long_key(bytes + p0, n, &klo, &khi);
     /* rep = (length << 40) | offset holds 24 length bits: a term of 16 MiB or more would be
      * emitted truncated, so the run fails with TFIDF_E_CAPACITY instead */
     if (n >= 0xFFFFFFull) atomicOr(status, ST_TERM_LONG);
     const uint64_t rep = ((n < 0xFFFFFFull ? n : 0xFFFFFFull) << 40) | p0;
-    return vocab_insert(v, klo, khi, rep, status);
+    return vocab_insert<VS_HOME>(v, klo, khi, rep, status);
 }
 
 /* A (document, term) pair met after the table reached FILL_LIMIT and not in it: one
@@ -384,7 +386,7 @@ __global__ __launch_bounds__(NT, K1_WAVES_PER_SIMD) void k_tokcount_vs(CorpusDev
             const bool hit1 = r.t4.x == (uint32_t)r.klo && r.t4.y == (uint32_t)(r.klo >> 32) &&
                               r.t4.z == (uint32_t)r.khi && r.t4.w == (uint32_t)(r.khi >> 32);
             CNT(1, (hit0 || hit1) ? 0 : 1);
-            slot = hit0 ? r.hv : hit1 ? ((r.hv + 1) & (uint32_t)v.mask) : vocab_insert(v, r.klo, r.khi, 0, o.status);
+            slot = hit0 ? r.hv : hit1 ? ((r.hv + 1) & (uint32_t)v.mask) : vocab_insert<VS_HOME>(v, r.klo, r.khi, 0, o.status);
         } else if (r.kind == 2u) {
             slot = slow_slot(c.bytes, v, r.ap, S.gdoc[r.rel + 1], o.status);
         }
@@ -575,7 +577,7 @@ __global__ __launch_bounds__(NT, K1_WAVES_PER_SIMD) void k_tokcount_vs(CorpusDev
                                 uint32_t rel = wr;
                                 for (uint32_t k = wr + 1; k < kend; ++k) rel += uni64(S.gdoc[k]) <= q.ap ? 1u : 0u;
                                 q.rel = rel;
-                                q.hv = q.kind == 1u ? (uint32_t)(key_hash(q.klo, q.khi) & v.mask & ~1ull) : 0u;   /* even home (dev_vocab.h) */
+                                q.hv = q.kind == 1u ? (uint32_t)(key_hash(q.klo, q.khi) & v.mask & VS_HOME) : 0u;   /* home (dev_vocab.h) */
                                 /* the home slot and the next one: a key displaced by one slot
                                  * (linear probing) still resolves without a dependent load */
                                 q.s4 = v.keys[q.hv];

@@ -23,7 +23,7 @@ with tfidf_abi.Engine(0) as e:
     n = L.tfidf_debug_k1_stamps(e.h, buf, 32)
     v = list(buf)[:n]
 names = ["chunk setup", "walk", "token list", "round build", "round finish", "last rounds", "chunk end",
-         "flush wait", "flush writes", "flush counts", "flush alloc"]
+         "flush wait", "flush writes", "flush counts", "flush alloc", "finish: load wait"]
 NPH = len(names)
 waves = v[NPH + 1] or 1
 tot = sum(v[:NPH])
