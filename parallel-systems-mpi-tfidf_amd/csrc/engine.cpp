@@ -828,24 +828,22 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
         ctx->sorted_skey = cur ? ctx->skey1.as<uint4>() : ctx->skey0.as<uint4>();
         ctx->sorted_dense = cur ? ctx->seq1.as<uint32_t>() : ctx->seq0.as<uint32_t>();
     } else {
-        /* two u64 LSD sorts over the varying bytes: the keys' low halves, then (stable) the
-         * high halves gathered in that order; skey0 stays in dense order, skey1 holds the
-         * two u64 ping-pong buffers (c4: 12-byte instead of 20-byte pairs per digit pass) */
+        /* a u64 LSD sort of the keys' high halves (their first 8 bytes) over the varying
+         * bytes, then the runs of equal prefixes re-ordered by the low halves
+         * (launch_vocab_prefix_ties: few at c4, so 8 digit passes instead of 13; vocabulary
+         * 2.19 -> 2.00 ms, profiles/r04_c4_vocab_quads_ab.txt); skey0 stays in dense order,
+         * skey1 holds the two u64 ping-pong buffers */
         uint32_t vm = 0;
         LCHK(key_varying_bytes_u128(ctx->skey0.as<uint4>(), V, &vm, ar, s));
         uint64_t* const ka = (uint64_t*)ctx->skey1.p;
         uint64_t* const kb = ka + V;
         uint32_t* const sa = ctx->seq0.as<uint32_t>();
         uint32_t* const sbq = ctx->seq1.as<uint32_t>();
-        LCHK(launch_sortkey_half(ctx->skey0.as<uint4>(), V, nullptr, 0, ka, s));
-        const int c1 = radix_sort_u64(ka, sa, kb, sbq, V, vm & 0xFFu, ar, s);
+        LCHK(launch_sortkey_half(ctx->skey0.as<uint4>(), V, nullptr, 1, ka, s));
+        const int c1 = radix_sort_u64(ka, sa, kb, sbq, V, (vm >> 8) & 0xFFu, ar, s);
         LCHK(c1);
-        uint64_t* const kc = c1 ? kb : ka;
-        uint32_t* const sc = c1 ? sbq : sa;
-        LCHK(launch_sortkey_half(ctx->skey0.as<uint4>(), V, sc, 1, kc, s));
-        const int c2 = radix_sort_u64(kc, sc, c1 ? ka : kb, c1 ? sa : sbq, V, (vm >> 8) & 0xFFu, ar, s);
-        LCHK(c2);
-        ctx->sorted_dense = c2 ? (c1 ? sa : sbq) : sc;
+        ctx->sorted_dense = c1 ? sbq : sa;
+        LCHK(launch_vocab_prefix_ties(c1 ? kb : ka, ctx->sorted_dense, ctx->skey0.as<uint4>(), V, vm & 0xFFu, ar, s));
         ctx->sorted_skey = nullptr;
         if (st & ST_HAS_LONG) {   /* the fix-up reads the keys in sorted order */
             LCHK(launch_gather_u128(ctx->skey0.as<uint4>(), ctx->sorted_dense, V, ctx->skey1.as<uint4>(), s));
@@ -1064,6 +1062,10 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
     a.idf_idx = full_lut ? nullptr : ctx->present.as<uint32_t>();   /* null: idf indexed by df */
     a.idf = ctx->idf_vals.as<double>();
     a.idf_rank = ctx->idf_rank.as<double>();
+#ifdef K5_DFIDF
+    /* large V: 4-byte df gathers + the small idf-by-df table instead of 8-byte idf gathers */
+    a.idf_by_df = (full_lut && V >= (1u << 21)) ? 1u : 0u;
+#endif
     a.large_list = ctx->large_list.as<uint32_t>() + 1;
     a.large_count = ctx->large_list.as<uint32_t>();
     a.cls_nblk = (N + 255) / 256;

@@ -287,6 +287,84 @@ int launch_vocab_long_fixup(const uint4* sorted_keys, uint32_t* sorted_dense, co
     return ok();
 }
 
+/* ---- large-V vocabulary sort, prefix first: the keys sorted by their first 8 bytes
+ * (the high halves) only; positions whose high half equals a neighbour's are "tied" and
+ * re-ordered by their low halves within each run of equal prefixes.  Tied positions are
+ * numbered in position order and the (run, low half)-sorted tied items are written back
+ * to them in that order, so item j of the sorted list lands at the j-th tied position.
+ * Most terms differ in their first 8 bytes (c4: 9.75 M terms, 13 radix passes -> 8 + a
+ * fix-up of the few tied ones). */
+__global__ void k_pt_flags(const uint64_t* __restrict__ hi, uint32_t V, uint32_t* __restrict__ tied,
+                           uint32_t* __restrict__ head) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= V) return;
+    const bool prev = i > 0 && hi[i] == hi[i - 1];
+    const bool next = i + 1 < V && hi[i] == hi[i + 1];
+    tied[i] = (prev || next) ? 1u : 0u;
+    head[i] = (!prev && next) ? 1u : 0u;
+}
+__global__ void k_pt_collect(const uint32_t* __restrict__ tied_scan, const uint32_t* __restrict__ head_scan,
+                             const uint32_t* __restrict__ head, const uint32_t* __restrict__ sorted_dense,
+                             const uint4* __restrict__ skey, uint32_t V, uint32_t* __restrict__ pos,
+                             uint64_t* __restrict__ klow, uint32_t* __restrict__ val, uint64_t* __restrict__ seg,
+                             uint32_t* __restrict__ dense_copy) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= V || tied_scan[i + 1] == tied_scan[i]) return;
+    const uint32_t j = tied_scan[i];
+    const uint32_t d = sorted_dense[i];
+    const uint4 k = skey[d];
+    pos[j] = i;
+    klow[j] = ((uint64_t)k.y << 32) | k.x;
+    val[j] = j;
+    seg[j] = head_scan[i] + head[i];   /* run ordinal (inclusive count of run heads) */
+    dense_copy[j] = d;
+}
+__global__ void k_pt_apply(const uint32_t* __restrict__ final_idx, uint32_t m, const uint32_t* __restrict__ pos,
+                           const uint32_t* __restrict__ dense_copy, uint32_t* __restrict__ sorted_dense) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < m) sorted_dense[pos[j]] = dense_copy[final_idx[j]];
+}
+
+int launch_vocab_prefix_ties(const uint64_t* sorted_hi, uint32_t* sorted_dense, const uint4* skey, uint32_t V,
+                             uint32_t low_mask, Arena& ar, hipStream_t s) {
+    if (V < 2 || !low_mask) return 0;
+    const size_t m0 = ar.mark();
+    uint32_t* tied = (uint32_t*)ar.get(((size_t)V + 2) * 4);
+    uint32_t* head = (uint32_t*)ar.get(((size_t)V + 2) * 4);
+    uint32_t* ts = (uint32_t*)ar.get(((size_t)V + 2) * 4);
+    uint32_t* hs = (uint32_t*)ar.get(((size_t)V + 2) * 4);
+    if (!tied || !head || !ts || !hs) return -2;
+    k_pt_flags<<<grid_for(V), NT, 0, s>>>(sorted_hi, V, tied, head);
+    if (scan_excl_u32(tied, ts, V, ar, s)) return -2;
+    uint32_t m = 0;
+    if (hipMemcpyAsync(&m, ts + V, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
+    if (hipStreamSynchronize(s) != hipSuccess) return -1;
+    if (m) {
+        if (scan_excl_u32(head, hs, V, ar, s)) return -2;
+        uint32_t* pos = (uint32_t*)ar.get((size_t)m * 4);
+        uint64_t* k0 = (uint64_t*)ar.get((size_t)m * 8);
+        uint64_t* k1 = (uint64_t*)ar.get((size_t)m * 8);
+        uint32_t* v0 = (uint32_t*)ar.get((size_t)m * 4);
+        uint32_t* v1 = (uint32_t*)ar.get((size_t)m * 4);
+        uint64_t* sg = (uint64_t*)ar.get((size_t)m * 8);
+        uint64_t* s0 = (uint64_t*)ar.get((size_t)m * 8);
+        uint64_t* s1 = (uint64_t*)ar.get((size_t)m * 8);
+        uint32_t* dc = (uint32_t*)ar.get((size_t)m * 4);
+        if (!pos || !k0 || !k1 || !v0 || !v1 || !sg || !s0 || !s1 || !dc) return -2;
+        k_pt_collect<<<grid_for(V), NT, 0, s>>>(ts, hs, head, sorted_dense, skey, V, pos, k0, v0, sg, dc);
+        const int cur = radix_sort_u64(k0, v0, k1, v1, m, low_mask, ar, s);
+        if (cur < 0) return cur;
+        uint32_t* vk = cur ? v1 : v0;
+        uint32_t* vo = cur ? v0 : v1;
+        k_vlf_seg_of<<<grid_for(m), NT, 0, s>>>(vk, sg, m, s0);
+        const int cs = radix_sort_u64(s0, vk, s1, vo, m, 0x0Fu, ar, s);   /* stable on the run ordinal */
+        if (cs < 0) return cs;
+        k_pt_apply<<<grid_for(m), NT, 0, s>>>(cs ? vo : vk, m, pos, dc, sorted_dense);
+    }
+    ar.release(m0);
+    return ok();
+}
+
 /* -------------------------------------------------------------- partials -- */
 
 __global__ void k_part_keys(const uint32_t* __restrict__ pdoc, const uint32_t* __restrict__ pslot,
@@ -986,13 +1064,20 @@ __global__ void k_idf_of_rank(const uint32_t* __restrict__ df_of_rank, const uin
     if (r < V) out[r] = idf_idx ? idf[idf_idx[df_of_rank[r]]] : idf[df_of_rank[r]];   /* null: table over all df */
 }
 
+/* idf of term rank r: the per-rank table, or (idf_by_df) the idf table over df values
+ * indexed by the term's df */
+__device__ __forceinline__ double k5_idf(const K5Args& a, uint32_t r) {
+    if (a.idf_by_df) return G(a.idf)[G(a.df_of_rank)[r]];
+    return G(a.idf_rank)[r];
+}
+
 /* The output is 16 bytes per pair (term rank, count, score): the document, docSize and
  * df of a pair are per-document / per-term values the fetch expands on the host. */
 __device__ __forceinline__ void k5_emit(const K5Args& a, uint64_t o, double ds, uint32_t rank, uint32_t cnt) {
     const double tf = (double)cnt / ds;   /* TFIDF.c:202 */
     sto(&a.out_term[o], (uint32_t)(rank));
     sto(&a.out_cnt[o], (uint32_t)(cnt));
-    sto(&a.out_score[o], (double)(tf * G(a.idf_rank)[rank])); /* TFIDF.c:243-244 (idf from the host-libm LUT) */
+    sto(&a.out_score[o], (double)(tf * k5_idf(a, rank))); /* TFIDF.c:243-244 (idf from the host-libm LUT) */
 }
 
 /* records hold term ranks once the DF pass has run (k_df_hist_* rewrite them in place) */
@@ -1240,7 +1325,7 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
             }
             double idf[QC];
 #pragma unroll
-            for (int q = 0; q < QC; ++q) idf[q] = (64u * q + lane < n) ? G(a.idf_rank)[r[q]] : 0.0;
+            for (int q = 0; q < QC; ++q) idf[q] = (64u * q + lane < n) ? k5_idf(a, r[q]) : 0.0;
 #pragma unroll
             for (int q = 0; q < QC; ++q) {
                 const uint32_t j = 64u * q + lane;
@@ -1334,7 +1419,7 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
                         pos[e] = gs + less;
                         cnt[e] = buf0[j];
                     }
-                    idf[e] = j < n ? G(a.idf_rank)[rk] : 0.0;
+                    idf[e] = j < n ? k5_idf(a, rk) : 0.0;
                 }
 #pragma unroll
                 for (int e = 0; e < EB; ++e) {
@@ -1407,7 +1492,7 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
                 cnt[q] = j < n ? buf0[key[q] & ((1u << K5_IDX_BITS) - 1u)] : 0u;
             }
 #pragma unroll
-            for (int q = 0; q < EB; ++q) idf[q] = G(a.idf_rank)[key[q] >> K5_IDX_BITS];
+            for (int q = 0; q < EB; ++q) idf[q] = k5_idf(a, key[q] >> K5_IDX_BITS);
 #pragma unroll
             for (int q = 0; q < EB; ++q) {
                 const uint32_t j = j0 + 64 * q + lane;
@@ -1487,7 +1572,7 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
             for (int e = 0; e < K5L_EB; ++e) {
                 const uint32_t j = j0 + NT * e + tid;
                 if (j < n) rk[e] = k5_rank(a, rk[e]);
-                f[e] = j < n ? G(a.idf_rank)[rk[e]] : 0.0;
+                f[e] = j < n ? k5_idf(a, rk[e]) : 0.0;
             }
 #pragma unroll
             for (int e = 0; e < K5L_EB; ++e) {
@@ -1564,7 +1649,7 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
                         ps[e] = gs + less;
                         cn[e] = vbuf[0][vbuf[1][p]];
                     }
-                    f[e] = p < n ? G(a.idf_rank)[kk[e]] : 0.0;
+                    f[e] = p < n ? k5_idf(a, kk[e]) : 0.0;
                 }
 #pragma unroll
                 for (int e = 0; e < K5L_EB; ++e) {
@@ -1782,7 +1867,7 @@ __global__ __launch_bounds__(256, K5S_OCC) void k_score_small(K5Args a) {
         for (int q = 0; q < Q; ++q) {
             const bool v = 64u * q + lane < d.n;
             if (v) r[q] = k5_rank(a, r[q]);
-            f[q] = v ? G(a.idf_rank)[r[q]] : 0.0;
+            f[q] = v ? k5_idf(a, r[q]) : 0.0;
         }
     };
     K5SDoc D0 = doc_at(0), D1 = doc_at(1);
@@ -1876,7 +1961,7 @@ __global__ __launch_bounds__(256) void k_emit_split(K5Args a) {
             for (int e = 0; e < K5L_EB; ++e) {
                 const uint32_t j = j0 + 256u * e + threadIdx.x;
                 if (j < j1) rk[e] = k5_rank(a, rk[e]);
-                f[e] = j < j1 ? G(a.idf_rank)[rk[e]] : 0.0;
+                f[e] = j < j1 ? k5_idf(a, rk[e]) : 0.0;
             }
 #pragma unroll
             for (int e = 0; e < K5L_EB; ++e) {
@@ -1900,8 +1985,9 @@ int launch_score_order(const K5Args& a, Arena& ar, hipStream_t s, hipStream_t s2
     if (!a.ndocs) return 0;
     if (hipMemsetAsync(a.large_count, 0, 4, s) != hipSuccess) return -1;
     if (a.split_count && hipMemsetAsync(a.split_count, 0, 4, s) != hipSuccess) return -1;
-    k_idf_of_rank<<<grid_for(a.nterms ? a.nterms : 1), NT, 0, s>>>(a.df_of_rank, a.idf_idx, a.idf, a.nterms,
-                                                                  a.idf_rank);
+    if (!a.idf_by_df)
+        k_idf_of_rank<<<grid_for(a.nterms ? a.nterms : 1), NT, 0, s>>>(a.df_of_rank, a.idf_idx, a.idf, a.nterms,
+                                                                      a.idf_rank);
     static int ncu = 0;
     if (!ncu) {
         int dev = 0;

@@ -122,6 +122,10 @@ int launch_vocab_rank(const uint32_t* sorted_dense, const uint32_t* vslot, uint3
                       uint32_t* slot_of_rank, uint16_t* rank16, hipStream_t s);
 /* long terms tied on their first 16 bytes: ordered by iterated segmented sorts (host loop,
  * one sync per 16 bytes of common prefix); -2 when the arena is too small */
+/* the large-V sort's tie fix-up (finalize.hip): runs of equal first 8 bytes in the
+ * prefix-sorted order re-ordered by the low halves (low_mask: their varying bytes) */
+int launch_vocab_prefix_ties(const uint64_t* sorted_hi, uint32_t* sorted_dense, const uint4* skey, uint32_t V,
+                             uint32_t low_mask, Arena& ar, hipStream_t s);
 int launch_vocab_long_fixup(const uint4* sorted_keys, uint32_t* sorted_dense, const uint32_t* vslot,
                             const VocabDev& v, const CorpusDev& c, uint32_t V, Arena& ar, hipStream_t s);
 
@@ -184,6 +188,9 @@ struct K5Args {
     uint32_t ndocs;
     uint32_t nterms;
     uint32_t rank_bits;          /* bits of the largest term rank (radix passes) */
+    uint32_t idf_by_df;          /* 1: the score kernels read idf[df_of_rank[r]] (large V with a full idf
+                                    table: a 4-byte gather into V words + an L2-resident table instead of
+                                    an 8-byte gather into V doubles; idf_rank is not built) */
     uint64_t rec_total;          /* bounds guard: records in rec_slot/rec_cnt */
     uint64_t slot_cap;           /* bounds guard: vocabulary capacity */
     uint32_t* status;            /* ST_BOUNDS set instead of faulting */
