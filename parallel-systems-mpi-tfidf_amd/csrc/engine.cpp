@@ -831,7 +831,7 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
         /* a u64 LSD sort of the keys' high halves (their first 8 bytes) over the varying
          * bytes, then the runs of equal prefixes re-ordered by the low halves
          * (launch_vocab_prefix_ties: few at c4, so 8 digit passes instead of 13; vocabulary
-         * 2.19 -> 2.00 ms, profiles/r04_c4_vocab_quads_ab.txt); skey0 stays in dense order,
+         * 2.19 -> 2.00 ms, profiles/r04_c4_ab.txt); skey0 stays in dense order,
          * skey1 holds the two u64 ping-pong buffers */
         uint32_t vm = 0;
         LCHK(key_varying_bytes_u128(ctx->skey0.as<uint4>(), V, &vm, ar, s));
@@ -1062,10 +1062,8 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
     a.idf_idx = full_lut ? nullptr : ctx->present.as<uint32_t>();   /* null: idf indexed by df */
     a.idf = ctx->idf_vals.as<double>();
     a.idf_rank = ctx->idf_rank.as<double>();
-#ifdef K5_DFIDF
     /* large V: 4-byte df gathers + the small idf-by-df table instead of 8-byte idf gathers */
     a.idf_by_df = (full_lut && V >= (1u << 21)) ? 1u : 0u;
-#endif
     a.large_list = ctx->large_list.as<uint32_t>() + 1;
     a.large_count = ctx->large_list.as<uint32_t>();
     a.cls_nblk = (N + 255) / 256;
