@@ -51,11 +51,17 @@ namespace {
 
 constexpr int NT = 256;                 /* threads per workgroup */
 constexpr int NWAVE = NT / 64;
-constexpr int WG_PER_CU = 4;            /* 16 waves per CU */
+#ifndef SL_WGCU
+#define SL_WGCU 4
+#endif
+constexpr int WG_PER_CU = SL_WGCU;      /* 16 waves per CU */
 constexpr int WSTEP = 992;              /* bytes a wave step owns: lanes 1..62 one 16-byte group each;
                                            lane 0 holds the 16 bytes before the step, lane 63 the 16
                                            after it (terms crossing the step end) */
-constexpr int TB = 3584;                /* LDS count table entries (u32 key + u32 count) */
+#ifndef SL_TB
+#define SL_TB 3584
+#endif
+constexpr int TB = SL_TB;               /* LDS count table entries (u32 key + u32 count) */
 constexpr int EPT = TB / NT;
 constexpr uint32_t BW = 8;              /* slots per bucket (two ds_read_b128) */
 constexpr uint32_t NB = TB / BW;
