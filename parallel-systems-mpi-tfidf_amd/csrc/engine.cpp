@@ -175,8 +175,11 @@ struct tfidf_ctx {
     DevBuf x_rrec, x_rslot, x_reply, x_tkey, x_tdf;
     /* dense exchange (small vocabularies): gathered keys, shared positions, the DF vector */
     DevBuf x_gkeys, x_pos, x_dense;
-    int xchg_mode = 0;      /* env TFIDF_XCHG: 0 auto (dense up to DENSE_XCHG_MAXV terms per rank), 1 owner, 2 dense */
+    int xchg_mode = 0;      /* env TFIDF_XCHG: 0 auto (dense up to DENSE_XCHG_MAXV terms per rank), 1 owner, 2 dense,
+                               3 dense with table numbering */
     bool last_dense = false;   /* the last exchange used the dense form */
+    bool local_long = false;
+    bool xagg_table = false;   /* env TFIDF_XAGG=table: the owner aggregates in an HBM table (A/B) */   /* this rank's vocabulary holds terms of >= 16 bytes (K1 status) */
     /* sizes the local part of a run hands to the exchange and the stages after it */
     uint32_t run_N = 0, run_V = 0;
     uint64_t run_cap = 0, run_R_total = 0;
@@ -287,6 +290,9 @@ int tfidf_open(int device, tfidf_ctx** out) {
     const char* kxm = getenv("TFIDF_XCHG");
     if (kxm && !strcmp(kxm, "owner")) ctx->xchg_mode = 1;
     if (kxm && !strcmp(kxm, "dense")) ctx->xchg_mode = 2;
+    if (kxm && !strcmp(kxm, "dense_table")) ctx->xchg_mode = 3;
+    const char* kxa = getenv("TFIDF_XAGG");
+    ctx->xagg_table = kxa && !strcmp(kxa, "table");
     const char* kn = getenv("TFIDF_TEST_XNOMEM_RANK");
     ctx->xnomem_rank = kn ? atoi(kn) : -1;
     /* diagnostics: initial vocabulary capacity (power of two) and the loads it may reach
@@ -411,9 +417,13 @@ hipStream_t tfidf_ctx_stream(const tfidf_ctx* ctx) { return ctx->stream; }
  *   2. one of two forms (the same results; TFIDF_XCHG=owner|dense forces one):
  *      dense  (every rank's V <= DENSE_XCHG_MAXV: c2, c3, c5) — north_star's form: the
  *             ranks' term keys are all-gathered (padded to the largest V), every rank numbers
- *             the distinct keys identically (smallest gathered position), scatters its local
- *             df into a dense vector over those numbers, and ONE all-reduce (sum) gives every
- *             rank the global df; global V = the distinct keys.  Its buffers are sized
+ *             the distinct keys identically, scatters its local df into a dense vector over
+ *             those numbers, and ONE all-reduce (sum) gives every rank the global df; global
+ *             V = the distinct keys.  The numbering: when no rank holds terms of >= 16 bytes
+ *             (a flag in step 1's word) each gathered list is in term order and a key's
+ *             number is its position in the merged lists (binary searches, no table:
+ *             launch_dense_merge_ids); otherwise its smallest gathered position, from a hash
+ *             table of all gathered keys (TFIDF_XCHG=dense_table forces this).  Buffers are sized
  *             before step 1 from the rank's own V (padded by a quarter), so their allocation
  *             status travels in step 1's word; only when the largest V exceeds some rank's
  *             padding do all ranks grow them and agree once more.  Then one all-gather and
@@ -488,7 +498,9 @@ static int exchange_owner(tfidf_ctx* ctx, uint32_t V, const std::vector<uint64_t
     ens(ctx->x_rslot, sumv * 4 + 4);
     ens(ctx->x_reply, (sumv + R) * 4 + 4);
     ens(ctx->x_tkey, table_cap(sumv) * 16);
-    ens(ctx->x_tdf, table_cap(sumv) * 4);
+    /* the table form's df column, or the bucketed form's spread counters */
+    const size_t xb_cnt = ((size_t)owner_buckets(sumv) + 1) * 128;
+    ens(ctx->x_tdf, table_cap(sumv) * 4 > xb_cnt ? table_cap(sumv) * 4 : xb_cnt);
     if (ctx->xnomem_rank == me) {   /* tests: an agreed allocation failure (once) */
         ctx->xnomem_rank = -1;
         arc = TFIDF_E_NOMEM;
@@ -540,9 +552,17 @@ static int exchange_owner(tfidf_ctx* ctx, uint32_t V, const std::vector<uint64_t
     if (rc) return rc;
     /* the owner: df summed per distinct key, every received record answered in order */
     unsigned long long* used = cnt + 10;
-    XCHK(launch_owner_aggregate(ctx->x_rrec.as<uint32_t>(), nrecv, roff, (uint32_t)R, ctx->x_tkey.as<uint4>(),
-                                table_cap(nrecv), ctx->x_tdf.as<uint32_t>(), ctx->x_rslot.as<uint32_t>(),
-                                ctx->x_reply.as<uint32_t>(), used, (uint32_t*)(cnt + 3), s));
+    if (ctx->xagg_table) {   /* TFIDF_XAGG=table: round 3's table of 1.5x the records (A/B) */
+        XCHK(launch_owner_aggregate(ctx->x_rrec.as<uint32_t>(), nrecv, roff, (uint32_t)R, ctx->x_tkey.as<uint4>(),
+                                    table_cap(nrecv), ctx->x_tdf.as<uint32_t>(), ctx->x_rslot.as<uint32_t>(),
+                                    ctx->x_reply.as<uint32_t>(), used, (uint32_t*)(cnt + 3), s));
+    } else {   /* bucketed: x_tkey (24 B per received record) and x_tdf are its scratch */
+        uint4* bkey = ctx->x_tkey.as<uint4>();
+        uint32_t* bdf = (uint32_t*)(bkey + nrecv);
+        XCHK(launch_owner_aggregate_buckets(ctx->x_rrec.as<uint32_t>(), nrecv, roff, (uint32_t)R, bkey, bdf,
+                                            bdf + nrecv, ctx->x_rslot.as<uint32_t>(), ctx->x_tdf.as<uint32_t>(),
+                                            ctx->x_reply.as<uint32_t>(), used, (uint32_t*)(cnt + 3), s));
+    }
     rc = xp->alltoallv(ctx->x_reply.p, rcnt1.data(), ctx->x_back.p, scnt1.data(), 4, s);
     if (rc) return rc;
     XCHK(launch_owner_back(ctx->x_back.as<uint32_t>(), soff, (uint32_t)R, ctx->x_sidx.as<uint32_t>(), V,
@@ -565,7 +585,7 @@ static int dense_alloc(tfidf_ctx* ctx, uint32_t V, uint64_t maxv, uint64_t R) {
 }
 
 /* the dense form (step 2 above) */
-static int exchange_dense(tfidf_ctx* ctx, uint32_t V, const std::vector<uint64_t>& vs, bool* agreed) {
+static int exchange_dense(tfidf_ctx* ctx, uint32_t V, const std::vector<uint64_t>& vs, bool merge, bool* agreed) {
     hipStream_t s = ctx->stream;
     Xport* xp = ctx->xp;
     const int R = xp->nranks, me = xp->rank;
@@ -597,10 +617,23 @@ static int exchange_dense(tfidf_ctx* ctx, uint32_t V, const std::vector<uint64_t
         return TFIDF_E_HIP;
     }
     uint4* mine = ctx->x_mine.as<uint4>();
-    HIPCHK(hipMemsetAsync(mine, 0xEE, maxv * 16, s));   /* padding: EMPTY keys */
+    /* padding: all-ones keys (above every short key) for the merge numbering, else EMPTY */
+    HIPCHK(hipMemsetAsync(mine, merge ? 0xFF : 0xEE, maxv * 16, s));
     XCHK(launch_keys_by_rank(ctx->vkeys.as<uint4>(), ctx->slot_of_rank.as<uint32_t>(), V, mine, s));
     rc = xp->allgather(mine, ctx->x_gkeys.p, maxv * 16, s);
     if (rc) return rc;
+    if (merge) {   /* positions in the merged term order: no table (x_tdf holds the R x V lb's) */
+        HIPCHK(hipMemsetAsync(ctx->x_dense.p, 0, (sumv + 1) * 4, s));
+        XCHK(launch_dense_merge_ids(ctx->x_gkeys.as<uint4>(), maxv, (uint32_t)R, (uint32_t)me, V,
+                                    ctx->x_tdf.as<uint32_t>(), ctx->df_local.as<uint32_t>(), sumv,
+                                    ctx->x_pos.as<uint32_t>(), ctx->x_dense.as<uint32_t>(), s));
+        rc = xp->allreduce_u32(ctx->x_dense.as<uint32_t>(), sumv + 1, s);
+        if (rc) return rc;
+        XCHK(launch_dense_gather(ctx->x_dense.as<uint32_t>(), ctx->x_pos.as<uint32_t>(), V,
+                                 ctx->df_global.as<uint32_t>(), s));
+        HIPCHK(hipMemcpyAsync(cnt + 12, ctx->x_dense.as<uint32_t>() + sumv, 4, hipMemcpyDeviceToDevice, s));
+        return 0;
+    }
     const uint64_t tcap = table_cap(sumv);
     uint32_t* status = (uint32_t*)(cnt + 3);
     XCHK(launch_dense_ids(ctx->x_gkeys.as<uint4>(), n, ctx->x_tkey.as<uint4>(), ctx->x_tdf.as<uint32_t>(), tcap, cnt + 10,
@@ -621,7 +654,7 @@ static int exchange_df(tfidf_ctx* ctx, int local_rc, uint32_t V) {
     std::vector<uint64_t> vs;
     /* the dense form's buffers, sized from this rank's V before the agreement (any failure
      * is agreed in step 1: no extra exchange for it) */
-    if (local_rc == 0 && ctx->xchg_mode != 1 && V <= DENSE_XCHG_MAXV) {
+    if (local_rc == 0 && (ctx->xchg_mode >= 2 || (ctx->xchg_mode == 0 && V <= DENSE_XCHG_MAXV))) {
         int arc = dense_alloc(ctx, V, dense_pad(V), (uint64_t)ctx->xp->nranks);
         if (ctx->xnomem_rank == ctx->xp->rank) {   /* tests: an agreed allocation failure (once) */
             ctx->xnomem_rank = -1;
@@ -629,14 +662,21 @@ static int exchange_df(tfidf_ctx* ctx, int local_rc, uint32_t V) {
         }
         if (arc) local_rc = arc;
     }
-    int rc = exchange_agree(ctx, local_rc, V, &vs);   /* step 1 */
+    /* step 1; bit 32 of the word: this rank holds terms of >= 16 bytes */
+    int rc = exchange_agree(ctx, local_rc, (uint64_t)V | (ctx->local_long ? 1ull << 32 : 0ull), &vs);
     if (rc) return rc;
     uint64_t maxv = 0;
-    for (uint64_t x : vs) maxv = x > maxv ? x : maxv;
-    const bool dense = ctx->xchg_mode == 2 || (ctx->xchg_mode == 0 && maxv <= DENSE_XCHG_MAXV);
+    bool any_long = false;
+    for (uint64_t& x : vs) {
+        any_long |= (x >> 32) != 0;
+        x &= 0xFFFFFFFFull;
+        maxv = x > maxv ? x : maxv;
+    }
+    const bool dense = ctx->xchg_mode >= 2 || (ctx->xchg_mode == 0 && maxv <= DENSE_XCHG_MAXV);
     ctx->last_dense = dense;
     bool agreed = false;
-    rc = dense ? exchange_dense(ctx, V, vs, &agreed) : exchange_owner(ctx, V, vs, &agreed);
+    rc = dense ? exchange_dense(ctx, V, vs, !any_long && ctx->xchg_mode != 3, &agreed)
+               : exchange_owner(ctx, V, vs, &agreed);
     if (rc && rc != TFIDF_E_PEER && !agreed) ctx->xp->abort();
     return rc;
 }
@@ -753,6 +793,7 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     for (int i = 0; i < 8; ++i) hc[i] = hp[i];
     const uint64_t R_main = hc[0], Q = hc[1], nbig = hc[6];
     const uint32_t st = (uint32_t)hc[3];
+    ctx->local_long = (st & ST_HAS_LONG) != 0;
     ctx->ntokens = hc[2];
     ctx->nchunks = nchunks;
     ctx->nrec_part = Q;

@@ -2279,6 +2279,154 @@ int launch_owner_aggregate(const uint32_t* rrec, uint64_t n, const uint32_t* rof
     k_owner_reply<<<grid_for(m), NT, 0, s>>>(rslot, n, roff, R, tdf, used, reply);
     return ok();
 }
+/* ---- the owner's aggregation, bucketed (round 4): the received records are partitioned by
+ * the top bits of their key hash into buckets of ~XB_MEAN records (every copy of a key in
+ * one bucket), then one workgroup per bucket sums the df of equal keys in an LDS table of
+ * record indices (claim = a 32-bit CAS of the index: the key itself is already in memory,
+ * so no pending state) and answers each record.  Sequential passes over the records
+ * instead of random probes into a table of 1.5x the records in HBM (c4 at 8 shards: 128 MB
+ * of keys per owner) and no table clears. */
+constexpr uint32_t XB_MEAN = 1024;   /* mean records per bucket */
+constexpr uint32_t XB_T = 4096;      /* LDS slots of the largest table (4x the mean; a bucket's table is
+                                        the power of two >= 2x its records, cleared per bucket) */
+constexpr uint32_t XB_CS = 32;       /* bucket counters 128 bytes apart: the count pass's atomics
+                                        spread over as many L2 lines as buckets */
+constexpr uint32_t XB_SCAN_NT = 1024;
+/* bucket = the top bits of a 64-bit mix (key_hash is 32-bit; its low bits pick the LDS slot),
+ * independent of owner_of's mix */
+__device__ __forceinline__ uint64_t xb_hash(const uint32_t* r) {
+    const uint64_t lo = ((uint64_t)r[1] << 32) | r[0], hi = ((uint64_t)r[3] << 32) | r[2];
+    return mix64(hi ^ (lo * 0xD6E8FEB86659FD93ull) ^ 0x2545F4914F6CDD1Dull);
+}
+/* rank[i] = the record's place in its bucket; cnt[b] = the bucket's records */
+__global__ void k_xb_count(const uint32_t* __restrict__ rrec, uint64_t n, uint32_t shift, uint32_t* __restrict__ cnt,
+                           uint32_t* __restrict__ rank) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) rank[i] = atomicAdd(&cnt[(uint32_t)(xb_hash(rrec + 5 * i) >> shift) * XB_CS], 1u);
+}
+/* exclusive scan of nb counts in place, one workgroup; off[nb] = total */
+__global__ void __launch_bounds__(XB_SCAN_NT) k_xb_scan(uint32_t* __restrict__ off, uint32_t nb) {
+    __shared__ uint32_t ws[XB_SCAN_NT / 64];
+    const uint32_t per = (nb + XB_SCAN_NT - 1) / XB_SCAN_NT, a = threadIdx.x * per, e = a + per < nb ? a + per : nb;
+    uint32_t t = 0;
+    for (uint32_t b = a; b < e; ++b) t += off[b * XB_CS];
+    /* exclusive scan of the per-thread totals */
+    uint32_t inc = t;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if ((threadIdx.x & 63) >= (uint32_t)d) inc += y;
+    }
+    if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    uint32_t base = 0;
+    for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) base += ws[w];
+    uint32_t acc = base + inc - t;
+    for (uint32_t b = a; b < e; ++b) {
+        const uint32_t c = off[b * XB_CS];
+        off[b * XB_CS] = acc;
+        acc += c;
+    }
+    if (threadIdx.x == XB_SCAN_NT - 1) off[nb * XB_CS] = acc;
+}
+__global__ void k_xb_scatter(const uint32_t* __restrict__ rrec, uint64_t n, uint32_t shift, const uint32_t* __restrict__ off,
+                             const uint32_t* __restrict__ rank, uint4* __restrict__ bkey, uint32_t* __restrict__ bdf,
+                             uint32_t* __restrict__ bidx) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t* r = rrec + 5 * i;
+    const uint32_t p = off[(uint32_t)(xb_hash(r) >> shift) * XB_CS] + rank[i];
+    bkey[p] = make_uint4(r[0], r[1], r[2], r[3]);
+    bdf[p] = r[4];
+    bidx[p] = (uint32_t)i;
+}
+/* one workgroup per bucket (grid-stride over buckets): LDS slot -> the bucket's first
+ * record of the key + the summed df; then every record answered (reply[i + sender]) */
+__global__ void __launch_bounds__(NT) k_xb_bucket(const uint4* __restrict__ bkey, const uint32_t* __restrict__ bdf,
+                                                  const uint32_t* __restrict__ bidx, const uint32_t* __restrict__ off,
+                                                  uint32_t nb, const uint32_t* __restrict__ roff, uint32_t R,
+                                                  uint32_t* __restrict__ reply, unsigned long long* __restrict__ used,
+                                                  uint32_t* __restrict__ status) {
+    __shared__ uint32_t tix[XB_T], tdf[XB_T];
+    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const uint32_t b0 = off[b * XB_CS], nrec = off[(b + 1) * XB_CS] - b0;
+        uint32_t T = 256;
+        while (T < 2 * nrec && T < XB_T) T *= 2;
+        const uint32_t tm = T - 1;
+        for (uint32_t t = threadIdx.x; t < T; t += NT) { tix[t] = 0xFFFFFFFFu; tdf[t] = 0; }
+        __syncthreads();
+        uint32_t claims = 0;
+        for (uint32_t j0 = 0; j0 < nrec; j0 += NT) {   /* find-or-claim, df added */
+            const uint32_t j = j0 + threadIdx.x;
+            if (j < nrec) {
+                const uint4 k = bkey[b0 + j];
+                uint32_t h = (uint32_t)key_hash(((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z) & tm;
+                uint32_t probe = 0;
+                for (; probe < T; ++probe, h = (h + 1) & tm) {
+                    uint32_t x = tix[h];
+                    if (x == 0xFFFFFFFFu) {
+                        x = atomicCAS(&tix[h], 0xFFFFFFFFu, j);
+                        if (x == 0xFFFFFFFFu) { ++claims; break; }
+                    }
+                    const uint4 o = bkey[b0 + x];
+                    if (o.x == k.x && o.y == k.y && o.z == k.z && o.w == k.w) break;
+                }
+                if (probe < T) atomicAdd(&tdf[h], bdf[b0 + j]);
+                else atomicOr(status, ST_BOUNDS);   /* more distinct keys than slots in one bucket */
+            }
+        }
+        __syncthreads();
+        for (uint32_t j0 = 0; j0 < nrec; j0 += NT) {   /* the answers */
+            const uint32_t j = j0 + threadIdx.x;
+            if (j < nrec) {
+                const uint4 k = bkey[b0 + j];
+                uint32_t h = (uint32_t)key_hash(((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z) & tm;
+                uint32_t d = 0;
+                for (uint32_t probe = 0; probe < T; ++probe, h = (h + 1) & tm) {
+                    const uint32_t x = tix[h];
+                    if (x == 0xFFFFFFFFu) break;
+                    const uint4 o = bkey[b0 + x];
+                    if (o.x == k.x && o.y == k.y && o.z == k.z && o.w == k.w) { d = tdf[h]; break; }
+                }
+                const uint32_t i = bidx[b0 + j];
+                reply[i + seg_of(roff, R, i)] = d;
+            }
+        }
+        const uint32_t c = wave_sum(claims);
+        if ((threadIdx.x & 63) == 0 && c) atomicAdd(used, (unsigned long long)c);
+        __syncthreads();   /* the table is cleared for the next bucket only after every lookup */
+    }
+}
+__global__ void k_xb_trailer(const uint32_t* __restrict__ roff, uint32_t R, const unsigned long long* __restrict__ used,
+                             uint32_t* __restrict__ reply) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < R) reply[(uint64_t)roff[p + 1] + p] = (uint32_t)*used;
+}
+/* scratch: bkey n x 16 B + bdf, rank n x 4 B (keys), bidx n x 4 B, cnt nb + 1 words */
+uint32_t owner_buckets(uint64_t n) {   /* >= 2: the bucket is hash >> (64 - lg), lg >= 1 */
+    uint32_t nb = 2;
+    while ((uint64_t)nb * XB_MEAN < n && nb < (1u << 24)) nb *= 2;
+    return nb;
+}
+int launch_owner_aggregate_buckets(const uint32_t* rrec, uint64_t n, const uint32_t* roff, uint32_t R, uint4* bkey,
+                                   uint32_t* bdf, uint32_t* rank, uint32_t* bidx, uint32_t* cnt, uint32_t* reply,
+                                   unsigned long long* used, uint32_t* status, hipStream_t s) {
+    const uint32_t nb = owner_buckets(n);
+    uint32_t lg = 0;
+    while ((1u << lg) < nb) ++lg;
+    const uint32_t shift = 64 - lg;
+    if (hipMemsetAsync(used, 0, 8, s) != hipSuccess || hipMemsetAsync(cnt, 0, ((size_t)nb + 1) * XB_CS * 4, s) != hipSuccess)
+        return -1;
+    if (n) {
+        if (n >= 0xFFFFFFFFull) return -2;
+        const unsigned g = (unsigned)((n + NT - 1) / NT);
+        k_xb_count<<<g, NT, 0, s>>>(rrec, n, shift, cnt, rank);
+        k_xb_scan<<<1, XB_SCAN_NT, 0, s>>>(cnt, nb);
+        k_xb_scatter<<<g, NT, 0, s>>>(rrec, n, shift, cnt, rank, bkey, bdf, bidx);
+        k_xb_bucket<<<nb < 8192 ? nb : 8192, NT, 0, s>>>(bkey, bdf, bidx, cnt, nb, roff, R, reply, used, status);
+    }
+    k_xb_trailer<<<(R + NT - 1) / NT, NT, 0, s>>>(roff, R, used, reply);
+    return ok();
+}
 int launch_owner_back(const uint32_t* back, const uint32_t* soff, uint32_t R, const uint32_t* sidx, uint32_t V,
                       uint32_t* df_global, uint32_t* vg, hipStream_t s) {
     k_owner_back<<<grid_for(V > 1 ? V : 1), NT, 0, s>>>(back, soff, R, sidx, V, df_global, vg);
@@ -2340,6 +2488,41 @@ int launch_sum_rows_u32(const uint32_t* rows, uint32_t nrows, uint64_t n, uint32
     k_sum_rows_u32<<<grid_for(n), NT, 0, s>>>(rows, nrows, n, out);
     return ok();
 }
+/* every word of every segment by one grid-stride pass (segment of a word: a search of off) */
+__global__ void k_xcopy(const XCopyList l) {
+    const uint64_t total = l.off[l.n];
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t lo = 0, hi = l.n;   /* last segment with off <= i */
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (l.off[mid] <= i) lo = mid; else hi = mid;
+        }
+        l.dst[lo][i - l.off[lo]] = l.src[lo][i - l.off[lo]];
+    }
+}
+__global__ void k_xsum_slice(const XCopyList l, uint64_t lo, uint64_t len, uint32_t* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t t = 0;
+        for (uint32_t r = 0; r < l.n; ++r) t += l.src[r][lo + i];
+        out[i] = t;
+    }
+}
+static unsigned xgrid(uint64_t n) {
+    const uint64_t b = (n + NT - 1) / NT;
+    return (unsigned)(b < 4096 ? (b ? b : 1) : 4096);
+}
+int launch_xcopy(const XCopyList& l, hipStream_t s) {
+    if (l.n < 1 || l.n > XCOPY_MAX) return -3;
+    if (!l.off[l.n]) return 0;
+    k_xcopy<<<xgrid(l.off[l.n]), NT, 0, s>>>(l);
+    return ok();
+}
+int launch_xsum_slice(const XCopyList& l, uint64_t lo, uint64_t len, uint32_t* out, hipStream_t s) {
+    if (l.n < 1 || l.n > XCOPY_MAX) return -3;
+    if (!len) return 0;
+    k_xsum_slice<<<xgrid(len), NT, 0, s>>>(l, lo, len, out);
+    return ok();
+}
 int launch_dense_ids(const uint4* gkeys, uint64_t n, uint4* tkey, uint32_t* tpos, uint64_t tcap,
                      unsigned long long* used, uint32_t* status, hipStream_t s) {
     if (hipMemsetAsync(tkey, 0xEE, tcap * 16, s) != hipSuccess || hipMemsetAsync(tpos, 0xFF, tcap * 4, s) != hipSuccess ||
@@ -2360,6 +2543,75 @@ int launch_dense_scatter(const uint4* mine, const uint32_t* df, uint32_t V, cons
 int launch_dense_gather(const uint32_t* dense, const uint32_t* pos, uint32_t V, uint32_t* df_global, hipStream_t s) {
     if (!V) return 0;
     k_dense_gather<<<grid_for(V), NT, 0, s>>>(dense, pos, V, df_global);
+    return ok();
+}
+
+/* ---- the dense exchange's merge numbering (no rank holds terms of >= 16 bytes).  Then
+ * every rank's key list is in term order (its rank order = the big-endian byte order of
+ * the identity keys, k_vocab_compact), so a term's number can be its position in the merged
+ * lists: pos(k) = sum over ranks q of lb_q(k), the keys of list q below k.  Equal keys get
+ * equal numbers, distinct keys distinct ones (for a < b, lb_q(a) <= lb_q(b) on every list
+ * and < on the list holding a), all in [0, sum V).  A key is counted for global V by the
+ * first rank holding it (no list q < me holds it).  No table, no clears: R binary searches
+ * per term over the gathered lists (each padded to maxv with all-ones keys, above every
+ * short key since those hold a TAB). */
+__device__ __forceinline__ void term_order(const uint4 k, uint64_t& a, uint64_t& b) {
+    a = bswap64(((uint64_t)k.y << 32) | k.x);
+    b = bswap64(((uint64_t)k.w << 32) | k.z);
+}
+/* lbm[q V + i] = lb_q(key i) | 2^31 if q < me holds it */
+__global__ void k_dense_lb(const uint4* __restrict__ gkeys, uint64_t maxv, uint32_t me, uint32_t V,
+                           uint32_t* __restrict__ lbm) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t q = blockIdx.y;
+    if (i >= V) return;
+    uint32_t lb = i;   /* own list: key i is at position i */
+    bool held = false;
+    if (q != me) {
+        const uint4* L = gkeys + (uint64_t)q * maxv;
+        uint64_t ka, kb;
+        term_order(gkeys[(uint64_t)me * maxv + i], ka, kb);
+        uint32_t lo = 0, n = (uint32_t)maxv;
+        while (n) {   /* first position whose key is >= key i */
+            const uint32_t h = n >> 1;
+            uint64_t a, b;
+            term_order(L[lo + h], a, b);
+            if (a < ka || (a == ka && b < kb)) { lo += h + 1; n -= h + 1; }
+            else n = h;
+        }
+        lb = lo;
+        if (q < me && lo < maxv) {
+            uint64_t a, b;
+            term_order(L[lo], a, b);
+            held = a == ka && b == kb;
+        }
+    }
+    lbm[(uint64_t)q * V + i] = lb | (held ? 0x80000000u : 0u);
+}
+/* pos[i] = sum of the lb's; dense[pos] = df; dense[sumv] += keys first held here */
+__global__ void k_dense_merge_scatter(const uint32_t* __restrict__ lbm, uint32_t R, uint32_t V,
+                                      const uint32_t* __restrict__ df, uint64_t sumv, uint32_t* __restrict__ pos,
+                                      uint32_t* __restrict__ dense) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t p = 0, held = 0;
+    if (i < V) {
+        for (uint32_t q = 0; q < R; ++q) {
+            const uint32_t x = lbm[(uint64_t)q * V + i];
+            p += x & 0x7FFFFFFFu;
+            held |= x >> 31;
+        }
+        pos[i] = p;
+        dense[p] = df[i];
+    }
+    const uint32_t first = (uint32_t)__popcll(__ballot(i < V && !held));
+    if ((threadIdx.x & 63) == 0 && first) atomicAdd(&dense[sumv], first);
+}
+int launch_dense_merge_ids(const uint4* gkeys, uint64_t maxv, uint32_t R, uint32_t me, uint32_t V, uint32_t* lbm,
+                           const uint32_t* df, uint64_t sumv, uint32_t* pos, uint32_t* dense, hipStream_t s) {
+    if (!V) return 0;
+    if (maxv >= 0x80000000ull || sumv >= 0x80000000ull || R > 65535u) return -2;
+    k_dense_lb<<<dim3((V + NT - 1) / NT, R), NT, 0, s>>>(gkeys, maxv, me, V, lbm);
+    k_dense_merge_scatter<<<grid_for(V), NT, 0, s>>>(lbm, R, V, df, sumv, pos, dense);
     return ok();
 }
 

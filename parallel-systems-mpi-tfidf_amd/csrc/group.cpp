@@ -159,6 +159,7 @@ struct Hub {
     uint64_t gen = 0;
     bool poisoned = false;
     std::vector<const void*> ptr;
+    std::vector<const void*> ptr2;   /* allreduce: every rank's reduced slice */
     std::vector<int> dev;
     std::vector<uint64_t> w;
     std::vector<uint64_t> sc;   /* alltoallv: rank r's count for peer p at sc[r * n + p] */
@@ -193,6 +194,14 @@ struct Hub {
 struct LocalXport final : Xport {
     Hub* hub = nullptr;
     int device = 0;
+    /* every rank on this device (and few enough for one copy list): each collective is one
+     * or two kernels reading the peers' buffers directly, instead of one copy per peer */
+    bool one_device() const {
+        if (nranks > XCOPY_MAX) return false;
+        for (int r = 0; r < nranks; ++r)
+            if (hub->dev[r] != device) return false;
+        return true;
+    }
     int words(const uint64_t mine[2], uint64_t* all, hipStream_t s) override {
         (void)s;
         hub->w[2 * rank] = mine[0];
@@ -208,7 +217,18 @@ struct LocalXport final : Xport {
         hub->ptr[rank] = send;
         if (!hub->barrier()) return TFIDF_E_PEER;
         int rc = TFIDF_OK;
-        for (int r = 0; r < nranks && !rc && bytes; ++r) {
+        if (bytes % 4 == 0 && one_device()) {
+            XCopyList l;
+            l.n = (uint32_t)nranks;
+            l.off[0] = 0;
+            for (int r = 0; r < nranks; ++r) {
+                l.src[r] = (const uint32_t*)hub->ptr[r];
+                l.dst[r] = (uint32_t*)((uint8_t*)recv + (size_t)r * bytes);
+                l.off[r + 1] = l.off[r] + bytes / 4;
+            }
+            if (launch_xcopy(l, s)) rc = TFIDF_E_HIP;
+        }
+        for (int r = 0; r < nranks && !rc && bytes && !(bytes % 4 == 0 && one_device()); ++r) {
             uint8_t* dst = (uint8_t*)recv + (size_t)r * bytes;
             const hipError_t e = hub->dev[r] == device
                 ? hipMemcpyAsync(dst, hub->ptr[r], bytes, hipMemcpyDeviceToDevice, s)
@@ -229,13 +249,22 @@ struct LocalXport final : Xport {
         if (!hub->barrier()) return TFIDF_E_PEER;
         int rc = TFIDF_OK;
         uint64_t ro = 0;
+        const bool fast = eb % 4 == 0 && one_device();
+        XCopyList l;
+        l.n = 0;
+        l.off[0] = 0;
         for (int p = 0; p < nranks && !rc; ++p) {
             /* peer p's segment for this rank starts after its segments for ranks < rank */
             uint64_t so = 0;
             for (int q = 0; q < rank; ++q) so += hub->sc[(size_t)p * nranks + q];
             const uint64_t n = hub->sc[(size_t)p * nranks + rank];
             if (n != rcnt[p]) rc = TFIDF_E_STATE;
-            if (!rc && n) {
+            if (!rc && n && fast) {
+                l.src[l.n] = (const uint32_t*)((const uint8_t*)hub->ptr[p] + so * eb);
+                l.dst[l.n] = (uint32_t*)((uint8_t*)recv + ro * eb);
+                l.off[l.n + 1] = l.off[l.n] + n * eb / 4;
+                ++l.n;
+            } else if (!rc && n) {
                 uint8_t* dst = (uint8_t*)recv + ro * eb;
                 const uint8_t* src = (const uint8_t*)hub->ptr[p] + so * eb;
                 const hipError_t e = hub->dev[p] == device
@@ -245,6 +274,7 @@ struct LocalXport final : Xport {
             }
             ro += rcnt[p];
         }
+        if (!rc && l.n && launch_xcopy(l, s)) rc = TFIDF_E_HIP;
         if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = TFIDF_E_HIP;
         if (rc) { abort(); return rc; }
         if (!hub->barrier()) return TFIDF_E_PEER;   /* no send buffer is reused before all copied */
@@ -260,6 +290,7 @@ struct LocalXport final : Xport {
     }
     int allreduce_u32(uint32_t* buf, size_t n, hipStream_t s) override {
         if (!n) return hub->barrier() && hub->barrier() && hub->barrier() ? TFIDF_OK : TFIDF_E_PEER;
+        if (one_device()) return allreduce_slices(buf, n, s);
         if (stage_n < n * (size_t)nranks) {
             if (stage) (void)hipFree(stage);
             stage = nullptr;
@@ -283,6 +314,48 @@ struct LocalXport final : Xport {
         if (launch_sum_rows_u32(stage, (uint32_t)nranks, n, buf, s)) { abort(); return TFIDF_E_HIP; }
         if (hipStreamSynchronize(s) != hipSuccess) { abort(); return TFIDF_E_HIP; }
         if (!hub->barrier()) return TFIDF_E_PEER;
+        return TFIDF_OK;
+    }
+    /* one device: a reduce-scatter (rank r sums slice r of every rank's vector into its
+     * staging) and an all-gather of the slices back into every vector; 2 launches per rank,
+     * ~3n words of traffic instead of R copies of n words and a row sum */
+    int allreduce_slices(uint32_t* buf, size_t n, hipStream_t s) {
+        const size_t chunk = (n + nranks - 1) / nranks;
+        if (stage_n < chunk) {
+            if (stage) (void)hipFree(stage);
+            stage = nullptr;
+            stage_n = 0;
+            if (tfidf_dev_malloc((void**)&stage, chunk * 4) != hipSuccess) { abort(); return TFIDF_E_NOMEM; }
+            stage_n = chunk;
+        }
+        auto slice = [&](int r, size_t* lo) {
+            *lo = chunk * r < n ? chunk * r : n;
+            return (chunk * (r + 1) < n ? chunk * (r + 1) : n) - *lo;
+        };
+        if (hipStreamSynchronize(s) != hipSuccess) { abort(); return TFIDF_E_HIP; }
+        hub->ptr[rank] = buf;
+        hub->ptr2[rank] = stage;
+        if (!hub->barrier()) return TFIDF_E_PEER;
+        XCopyList l;
+        l.n = (uint32_t)nranks;
+        for (int r = 0; r < nranks; ++r) l.src[r] = (const uint32_t*)hub->ptr[r];
+        size_t lo;
+        const size_t len = slice(rank, &lo);
+        int rc = launch_xsum_slice(l, lo, len, stage, s) ? TFIDF_E_HIP : TFIDF_OK;
+        if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = TFIDF_E_HIP;
+        if (rc) { abort(); return rc; }
+        if (!hub->barrier()) return TFIDF_E_PEER;   /* every slice summed: the vectors are free */
+        l.off[0] = 0;
+        for (int r = 0; r < nranks; ++r) {
+            const size_t m = slice(r, &lo);
+            l.src[r] = (const uint32_t*)hub->ptr2[r];
+            l.dst[r] = buf + lo;
+            l.off[r + 1] = l.off[r] + m;
+        }
+        if (launch_xcopy(l, s)) rc = TFIDF_E_HIP;
+        if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = TFIDF_E_HIP;
+        if (rc) { abort(); return rc; }
+        if (!hub->barrier()) return TFIDF_E_PEER;   /* every slice read before a staging is reused */
         return TFIDF_OK;
     }
     void abort() override { hub->poison(); }
@@ -333,6 +406,7 @@ int tfidf_group_open(int nranks, const int* devices, uint32_t flags, tfidf_group
         g->hub = new Hub();
         g->hub->n = nranks;
         g->hub->ptr.assign((size_t)nranks, nullptr);
+        g->hub->ptr2.assign((size_t)nranks, nullptr);
         g->hub->dev = dev;
         g->hub->w.assign(2 * (size_t)nranks, 0);
         g->hub->sc.assign((size_t)nranks * nranks, 0);

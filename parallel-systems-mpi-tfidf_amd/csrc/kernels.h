@@ -218,10 +218,28 @@ int launch_owner_offsets(const uint32_t* m, uint32_t R, uint32_t me, uint32_t* s
 int launch_owner_aggregate(const uint32_t* rrec, uint64_t n, const uint32_t* roff, uint32_t R, uint4* tkey, uint64_t tcap,
                            uint32_t* tdf, uint32_t* rslot, uint32_t* reply, unsigned long long* used, uint32_t* status,
                            hipStream_t s);
+/* the same, bucketed: records partitioned by key hash into owner_buckets(n) buckets, each
+ * aggregated in LDS (scratch: bkey n x 16 B; bdf, rank, bidx n x 4 B; cnt (nb + 1) x 128 B) */
+uint32_t owner_buckets(uint64_t n);
+int launch_owner_aggregate_buckets(const uint32_t* rrec, uint64_t n, const uint32_t* roff, uint32_t R, uint4* bkey,
+                                   uint32_t* bdf, uint32_t* rank, uint32_t* bidx, uint32_t* cnt, uint32_t* reply,
+                                   unsigned long long* used, uint32_t* status, hipStream_t s);
 int launch_owner_back(const uint32_t* back, const uint32_t* soff, uint32_t R, const uint32_t* sidx, uint32_t V,
                       uint32_t* df_global, uint32_t* vg, hipStream_t s);
 /* out[i] = sum of rows[r * n + i] over r < nrows (the in-process transport's all-reduce) */
 int launch_sum_rows_u32(const uint32_t* rows, uint32_t nrows, uint64_t n, uint32_t* out, hipStream_t s);
+/* the in-process transport's collectives between contexts on one device, one launch each:
+ * XCOPY_MAX segments of 4-byte words copied src[i] -> dst[i] (words[i] each) */
+#define XCOPY_MAX 64
+struct XCopyList {
+    const uint32_t* src[XCOPY_MAX];
+    uint32_t* dst[XCOPY_MAX];
+    uint64_t off[XCOPY_MAX + 1];   /* prefix sums of the segments' word counts */
+    uint32_t n;
+};
+int launch_xcopy(const XCopyList& l, hipStream_t s);
+/* out[i] = sum over r < n of src[r][lo + i], i < len (a reduce-scatter slice) */
+int launch_xsum_slice(const XCopyList& l, uint64_t lo, uint64_t len, uint32_t* out, hipStream_t s);
 /* dense DF exchange (small vocabularies): gathered keys -> shared positions (tpos[slot] =
  * smallest gathered position of the key, *used = distinct keys), this rank's df scattered
  * over them (pos[r] = position of term rank r), and read back after the all-reduce */
@@ -230,6 +248,11 @@ int launch_dense_ids(const uint4* gkeys, uint64_t n, uint4* tkey, uint32_t* tpos
 int launch_dense_scatter(const uint4* mine, const uint32_t* df, uint32_t V, const uint4* tkey, uint64_t tcap,
                          const uint32_t* tpos, uint32_t* pos, uint32_t* dense, uint32_t* status, hipStream_t s);
 int launch_dense_gather(const uint32_t* dense, const uint32_t* pos, uint32_t V, uint32_t* df_global, hipStream_t s);
+/* the same with merge numbering when no rank holds long terms (lists in term order, padded
+ * with all-ones keys): pos = the keys below each term over all lists; lbm: R x V words;
+ * dense[sumv] accumulates the keys first held by each rank (global V after the sum) */
+int launch_dense_merge_ids(const uint4* gkeys, uint64_t maxv, uint32_t R, uint32_t me, uint32_t V, uint32_t* lbm,
+                           const uint32_t* df, uint64_t sumv, uint32_t* pos, uint32_t* dense, hipStream_t s);
 
 /* synthetic corpus generation on the device */
 struct SynSpecDev;

@@ -66,13 +66,17 @@ def _run_group(shards, K, **kw):
     return texts, res, infos
 
 
-@pytest.mark.parametrize("xchg", ["dense", "owner"])
+@pytest.mark.parametrize("xchg", ["dense", "dense_table", "owner", "owner_table"])
 @pytest.mark.parametrize("cfg,scale,K", [("c2", 0.003, 2), ("c2", 0.003, 3), ("c5", 0.0005, 2), ("c5", 0.0005, 3),
-                                         ("c4", 0.001, 2), ("c2", 0.003, 5)])
+                                         ("c4", 0.001, 2), ("c2", 0.003, 5), ("c4", 0.01, 4)])
 def test_group_shards_equal_single_rank_oracle(cfg, scale, K, xchg, monkeypatch):
     """Both forms of the DF exchange (engine.cpp): the dense all-reduce over shared
-    positions (the default up to 2^17 terms per rank) and the hash-owner all-to-all."""
-    monkeypatch.setenv("TFIDF_XCHG", xchg)   # read by tfidf_open
+    positions (the default up to 2^17 terms per rank; numbered by merging the ranks' term
+    lists, or through a table of the gathered keys with dense_table) and the hash-owner
+    all-to-all (the owners aggregate in LDS buckets, or in an HBM table with owner_table)."""
+    monkeypatch.setenv("TFIDF_XCHG", xchg.replace("owner_table", "owner"))   # read by tfidf_open
+    if xchg == "owner_table":
+        monkeypatch.setenv("TFIDF_XAGG", "table")
     shards = _shards(cfg, scale, K)
     ora = _full(cfg, scale)
     texts, res, infos = _run_group(shards, K)
@@ -82,6 +86,31 @@ def test_group_shards_equal_single_rank_oracle(cfg, scale, K, xchg, monkeypatch)
     assert all(i["nterms_global"] == ora["nterms"] for i in infos)
     # shards really differ in vocabulary (the 0xEE padding of the all-gather is exercised)
     assert len({i["nterms"] for i in infos}) > 1
+
+
+@pytest.mark.parametrize("xchg", ["dense", "dense_table", "owner"])
+def test_group_long_terms(xchg, monkeypatch):
+    """Terms of >= 16 bytes (hash-tagged identity keys, not in term order) on the ranks: the
+    flag travels in the agreement word and every rank numbers the dense exchange through the
+    table; the same long term on two ranks gets one global DF."""
+    monkeypatch.setenv("TFIDF_XCHG", xchg)
+    base = _shards("c2", 0.002, 2)
+    N = base[0][3] + 2
+    nid = int(max(int(b[2].max()) for b in base)) + 1
+    extra = [b"supercalifragilisticexpialidocious internationalization a\n",
+             b"zz supercalifragilisticexpialidocious\n"]
+    shards = []
+    for r, (d, o, ids, _) in enumerate(base):
+        x = np.frombuffer(extra[r], dtype=np.uint8)
+        shards.append((np.concatenate([d, x]), np.concatenate([o, [o[-1] + len(x)]]).astype(np.uint64),
+                       np.concatenate([ids, [nid + r]]).astype(np.uint32), N))
+    texts, res, infos = _run_group(shards, 2)
+    data = np.concatenate([shards[0][0], shards[1][0]])
+    off = np.concatenate([shards[0][1], shards[0][1][-1] + shards[1][1][1:]])
+    ids = np.concatenate([shards[0][2], shards[1][2]])
+    ora = oracle_py.run(data, off, ids, N)
+    assert sorted(b"".join(texts).split(b"\n")) == sorted(ora["output_txt"].split(b"\n"))
+    assert all(i["nterms_global"] == ora["nterms"] for i in infos)
 
 
 def test_group_retry_is_collective(monkeypatch):
