@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 4 final measurement, part PART (1 or 2) on the committed tree:
-#   1: full GPU suite, smoke, the driver's default bench (c2), c3/c4/c5 benches
+#   1: full GPU suite, smoke, the driver's default bench (c2), c3/c4/c5 benches, 8-shard exchange benches
 #   2: K1 traffic passes (c2 c4 c5) + c2 kernel trace, the 8-shard exchange benches
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
@@ -17,6 +17,10 @@ if [ "${PART:-1}" = 1 ]; then
   for c in c3 c4 c5; do
     timeout -k 10 600 python3 bench.py --no-cpu-baseline --no-probe --config $c > $OUT/bench_$c.json 2> $OUT/bench_$c.err || { echo "bench $c failed"; tail -20 $OUT/bench_$c.err; exit 1; }
     echo "$c: $(tail -1 $OUT/bench_$c.json | cut -c1-160)"
+  done
+  for c in c5 c3 c4; do
+    timeout -k 10 600 python3 bench.py --shards 8 --steps 3 --warmup 1 --no-cpu-baseline --no-probe --no-emit --config $c > $OUT/shards8_$c.json 2> $OUT/shards8_$c.err || { echo "shards $c failed"; tail -20 $OUT/shards8_$c.err; exit 1; }
+    echo "shards8 $c: $(tail -1 $OUT/shards8_$c.json | cut -c1-200)"
   done
 else
   cd /tmp && export TMPDIR=/tmp
