@@ -432,8 +432,9 @@ hipStream_t tfidf_ctx_stream(const tfidf_ctx* ctx) { return ctx->stream; }
  *             owner rank (a hash of its key); the per-owner counts are all-gathered together
  *             with each rank's allocation status (an allocation failure is agreed there, no
  *             extra exchange), one all-to-all sends 20-byte (key, local df) records, each owner
- *             sums equal keys in a hash table and one all-to-all returns the global df of each
- *             record plus, per sender, the owner's distinct-key count (global V = their sum).
+ *             sums equal keys (LDS tables over hash buckets of the received records; an HBM
+ *             hash table with TFIDF_XAGG=table) and one all-to-all returns the global df of
+ *             each record plus, per sender, the owner's distinct-key count (global V = their sum).
  *             Per rank ~V entries move; the owner aggregates ~ΣV/R.
  *   Global V stays on the device and is read with the run's final status (no host round
  *   trip of its own).  From step 2 on no stage of the run returns "retry" (run_local checked
