@@ -9,6 +9,12 @@ tfidf_configs.plan(rank, nranks)), computes its local (term, df) with the oracle
      sender in the order received (the owner's hash aggregation + the reply all-to-all);
      global V = the owners' distinct terms summed,
   3. rescores its pairs with the global DF and N (TFIDF.c:202,243-245).
+The dense form (exchange_dense, merge numbering: every rank's V <= 2^17 and no long terms)
+is restated too: the ranks' term lists in term order (the bytes of "term\t", the output's
+strcmp order) are all-gathered, a term's number is the count of keys below it over all
+lists, each rank scatters its local df at its terms' numbers into a vector of sum(V) + 1
+entries (the last counts the keys no lower rank holds), and ONE all-reduce (sum) gives
+the global df of every number and the global V.
 The concatenation of the ranks' output lines in rank order must equal the single-rank
 oracle output (the reference's gather + qsort, TFIDF.c:253-273, are not needed).
 """
@@ -30,7 +36,35 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(rank, world, port, cfg, scale, outdir):
+def _dense_merge(rank, world, terms, df_local):
+    """exchange_dense's merge numbering (k_dense_lb, k_dense_merge_scatter) + the all-reduce"""
+    import bisect
+    mine = sorted(t + b"\t" for t in terms)
+    lists = [None] * world
+    dist.all_gather_object(lists, mine)
+    sumv = sum(len(x) for x in lists)
+    dfk = {t + b"\t": int(d) for t, d in zip(terms, df_local)}
+    vec = torch.zeros(sumv + 1, dtype=torch.int64)
+    pos = {}
+    first = 0
+    for k in mine:
+        p = 0
+        held = False
+        for q, L in enumerate(lists):
+            lb = bisect.bisect_left(L, k)
+            p += lb
+            if q < rank and lb < len(L) and L[lb] == k:
+                held = True
+        pos[k] = p
+        vec[p] = dfk[k]
+        first += 0 if held else 1
+    assert len(set(pos.values())) == len(mine)   # distinct keys, distinct numbers
+    vec[sumv] = first
+    dist.all_reduce(vec, op=dist.ReduceOp.SUM)
+    return {k[:-1]: int(vec[p]) for k, p in pos.items()}, int(vec[sumv])
+
+
+def _rank_main(rank, world, port, cfg, scale, outdir, xchg="owner"):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     repo = os.path.dirname(here)
@@ -50,10 +84,15 @@ def _rank_main(rank, world, port, cfg, scale, outdir):
         # local df per local term (the oracle's df is over this shard's documents)
         df_local = np.zeros(len(terms), dtype=np.int64)
         df_local[loc["term"]] = loc["df"]
+        if xchg == "dense":
+            gdf, vg = _dense_merge(rank, world, terms, df_local)
+            if rank == 0:
+                with open(os.path.join(outdir, "vglobal.txt"), "w") as f:
+                    f.write(str(vg))
         # 1. (term, local df) to the owners; all_gather_object restates the all-to-all
         import zlib
         out = [[] for _ in range(world)]
-        for t, d in zip(terms, df_local):
+        for t, d in zip(terms, df_local if xchg == "owner" else []):
             out[zlib.crc32(t) % world].append((t, int(d)))
         sent = [None] * world
         dist.all_gather_object(sent, out)
@@ -66,13 +105,14 @@ def _rank_main(rank, world, port, cfg, scale, outdir):
         replies = [[tot[t] for t, _ in seg] for seg in recv]
         back_all = [None] * world
         dist.all_gather_object(back_all, replies)
-        gdf = {}
+        if xchg == "owner":
+            gdf = {}
         for o in range(world):
             for (t, _), g in zip(out[o], back_all[o][rank]):
                 gdf[t] = g
         nv = torch.tensor([len(tot)], dtype=torch.int64)
         dist.all_reduce(nv, op=dist.ReduceOp.SUM)
-        if rank == 0:
+        if rank == 0 and xchg == "owner":
             with open(os.path.join(outdir, "vglobal.txt"), "w") as f:
                 f.write(str(int(nv.item())))
         # 3. rescore with global df and N, emit this shard's lines in output order
@@ -93,13 +133,15 @@ def _rank_main(rank, world, port, cfg, scale, outdir):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("xchg", ["owner", "dense"])
 @pytest.mark.parametrize("cfg,scale,world", [("c2", 0.0008, 2), ("c5", 0.0002, 2), ("c2", 0.0008, 3), ("c2", 0.0008, 4)])
-def test_two_rank_shards_concatenate_to_single_rank_output(tmp_path, cfg, scale, world):
-    """Output invariant in the number of shards K (as the reference's is in -np)."""
+def test_two_rank_shards_concatenate_to_single_rank_output(tmp_path, cfg, scale, world, xchg):
+    """Output invariant in the number of shards K (as the reference's is in -np),
+    with either form of the DF exchange."""
     import oracle_py
     import tfidf_abi
     import tfidf_configs
-    mp.spawn(_rank_main, args=(world, _free_port(), cfg, scale, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_rank_main, args=(world, _free_port(), cfg, scale, str(tmp_path), xchg), nprocs=world, join=True)
     with open(tmp_path / "multirank.txt", "rb") as f:
         got = f.read()
     p = tfidf_configs.plan(cfg, scale=scale)
