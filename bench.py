@@ -306,8 +306,30 @@ def main_group(args):
         "cold_run_ms": round(cold_ms, 3),
         "cold_run": {"ms": round(cold_ms, 3), "device_allocs": a1[0] - a0[0]},
     }
+    if want_c3(args):
+        try:
+            c3 = []
+            for r in range(N):
+                p = tfidf_configs.plan("c3", rank=r, nranks=N, weak=False)
+                c3.append(g.ranks[r].synth_device(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"],
+                                                  p["ndocs_total"]))
+            g.run(c3)   # cold run of the new shard sizes
+            hip_device_sync_all(N)
+            nb = float(sum(e.info()["nbytes"] for e in g.ranks))
+
+            def steps_fn(k):
+                for _ in range(k):
+                    g.run(c3)
+            line["c3_strong"] = c3_strong_measure(steps_fn, lambda: g.ranks[0].info(), nb, N,
+                                                  lambda: hip_device_sync_all(N))
+        except Exception as ex:   # reported, never silently dropped
+            line["c3_strong"] = {"error": repr(ex)}
     print(json.dumps(line), flush=True)
     g.close()
+
+
+def want_c3(args) -> bool:
+    return args.gpus >= 2 and args.config == "c2" and not args.strong and not args.no_c3 and args.scale == 1.0
 
 
 def hip_device_sync_all(n: int):
@@ -316,6 +338,51 @@ def hip_device_sync_all(n: int):
     for d in range(n):
         if hip.hipSetDevice(d) != 0 or hip.hipDeviceSynchronize() != 0:
             raise RuntimeError("hipDeviceSynchronize failed on device %d" % d)
+
+
+def plan_summary(cfg: str, ngpu: int, strong: bool, scale: float = 1.0) -> dict:
+    """What a run would measure (no GPU touched): per-rank shards of `cfg` over `ngpu` ranks."""
+    shards = []
+    for r in range(ngpu):
+        p = tfidf_configs.plan(cfg, scale=scale, rank=r, nranks=ngpu, weak=not strong)
+        est = float(np.sum(p["ntok"])) * tfidf_configs.bytes_per_token(p["V"])
+        shards.append({"rank": r, "docs": int(len(p["doc_ids"])), "est_bytes": int(est)})
+    return {"config": cfg, "n_gpus": ngpu, "scaling": "strong" if strong else "weak",
+            "docs_total": int(tfidf_configs.plan(cfg, scale=scale, rank=0, nranks=ngpu,
+                                                 weak=not strong)["ndocs_total"]),
+            "docs_in_shards": int(sum(x["docs"] for x in shards)),
+            "est_bytes_total": int(sum(x["est_bytes"] for x in shards)), "shards": shards}
+
+
+# BASELINE.json config 3 ("10M docs, ~40 GB Zipfian corpus sharded over 8 MI355X"): a --gpus N
+# run (N >= 2) of the default c2 line measures it too, after the headline steps, so the
+# driver's scaling runs carry it unattended (not in `value`; --no-c3 skips it)
+C3_STRONG_STEPS, C3_STRONG_WARMUP = 3, 1
+
+
+def c3_strong_measure(run_steps, info_of, corpora_bytes, ngpu, sync, barrier=lambda: None, max_over=lambda x: x):
+    """Times C3_STRONG_STEPS collective runs of the c3 strong split; run_steps(k) runs k steps on
+    every rank, info_of() is this process's rank-0 info; returns the nested line."""
+    run_steps(C3_STRONG_WARMUP)
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    run_steps(C3_STRONG_STEPS)
+    sync()
+    barrier()
+    el = max_over(time.perf_counter() - t0)
+    i = info_of()
+    alg = i["nbytes"] + 12.0 * i["npairs"]
+    return {"workload": f"c3 strong: 10M docs / ~40 GB split over {ngpu} GPUs (BASELINE config 3)",
+            "value": round(corpora_bytes * C3_STRONG_STEPS / el / 1e9, 4), "unit": "GB/s",
+            "ms_per_step": round(el / C3_STRONG_STEPS * 1e3, 4), "steps": C3_STRONG_STEPS,
+            "warmup": C3_STRONG_WARMUP, "corpus_bytes_total": int(corpora_bytes),
+            "k1_ms_rank0": round(i["ms_tokcount"], 4),
+            "k1_frac_rank0": round(alg / (i["ms_tokcount"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "exchange_ms_rank0": round(i["stages"].get("exchange", 0.0), 4),
+            "exchange_mode": "dense all-reduce" if i["flags"] & tfidf_abi.RUN_XCHG_DENSE else "hash-owner all-to-all",
+            "command": f"python -m torch.distributed.run --nproc-per-node {ngpu} bench.py --gpus {ngpu} "
+                       f"--config c3 --strong (the same measurement as a headline line)"}
 
 
 def main():
@@ -335,6 +402,11 @@ def main():
     ap.add_argument("--no-probe", action="store_true", help="skip the measured HBM read/copy peak probe")
     ap.add_argument("--no-emit", action="store_true", help="skip the (untimed) output-emission measurement")
     ap.add_argument("--vocab", type=int, default=0, help="diagnostics only: override the config's vocabulary size")
+    ap.add_argument("--plan-only", action="store_true",
+                    help="print what would be measured (shards per rank, and the c3 strong follow-up of a "
+                         "multi-GPU c2 run) as JSON and exit, without touching a GPU")
+    ap.add_argument("--no-c3", action="store_true",
+                    help="--gpus N >= 2: skip the c3 strong (BASELINE config 3) measurement after the c2 line")
     ap.add_argument("--shards", type=int, default=0,
                     help="K >= 2: the config's corpus cut into K byte-balanced shards run by K contexts on ONE "
                          "GPU (tfidf_group, in-process transport): measures the multi-rank path and the DF "
@@ -345,6 +417,12 @@ def main():
 
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
+    if args.plan_only:
+        out = plan_summary(args.config, args.gpus, args.strong, args.scale)
+        if want_c3(args):
+            out["c3_strong"] = plan_summary("c3", args.gpus, True)
+        print(json.dumps(out))
+        return
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return main_group(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -390,7 +468,7 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    k1_ms, tot_ms, stage_steps = [], [], []
+    k1_ms, tot_ms, stage_steps, idf_steps = [], [], [], []
     barrier()
     hip_device_sync()
     alloc_t0 = eng.alloc_counters()
@@ -401,6 +479,7 @@ def main():
         k1_ms.append(info["ms_tokcount"])
         tot_ms.append(info["ms_total"])
         stage_steps.append(info["stages"])
+        idf_steps.append((info["idf_logs"], info["ms_idf_host"], info["ms_idf_wait"]))
     hip_device_sync()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -447,6 +526,30 @@ def main():
     # measured streaming peaks, outside the timed region, rank 0 only
     probe = eng.hbm_probe(2 << 30, 10) if (rank == 0 and not args.no_probe) else None
 
+    c3_line = None
+    if want_c3(args) and world > 1:   # BASELINE config 3 after the headline steps (not in value)
+        import torch
+        try:
+            p3 = tfidf_configs.plan("c3", rank=rank, nranks=world, weak=False)
+            c3c = eng.synth_device(p3["seed"], p3["V"], p3["mode"], p3["cdf"], p3["doc_ids"], p3["ntok"],
+                                   p3["ndocs_total"])
+            eng.run_corpus(c3c)   # cold run of the new shard size
+            hip_device_sync()
+            nb = torch.tensor([float(eng.info()["nbytes"])], dtype=torch.float64)
+            dist.all_reduce(nb, op=dist.ReduceOp.SUM)
+
+            def steps_fn(k):
+                for _ in range(k):
+                    eng.run_corpus(c3c)
+
+            def max_over(x):
+                t = torch.tensor([x], dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                return float(t.item())
+            c3_line = c3_strong_measure(steps_fn, eng.info, float(nb.item()), world, hip_device_sync, barrier, max_over)
+        except Exception as ex:   # reported, never silently dropped
+            c3_line = {"error": repr(ex)}
+
     if rank == 0:
         ms_step = elapsed / args.steps * 1e3
         k1_avg_ms = float(np.mean(k1_ms))
@@ -477,6 +580,13 @@ def main():
             "stage_ms": {k: round(v, 4) for k, v in info["stages"].items()},
             "stage_ms_mean": {k: round(float(np.mean([st[k] for st in stage_steps])), 4) for k in info["stages"]},
             "stage_ms_max": {k: round(float(np.max([st[k] for st in stage_steps])), 4) for k in info["stages"]},
+            # the idf table (log(N/df) on the host's libm, TFIDF.c:243) is rebuilt inside every
+            # timed step on host threads beside the device stages (TFIDF_IDF_CACHE=1: kept
+            # across runs of one N, reported as idf_cached)
+            "idf": {"idf_cached": bool(os.environ.get("TFIDF_IDF_CACHE") == "1"),
+                    "logs_per_step": int(np.mean([x[0] for x in idf_steps])),
+                    "lut_host_ms_mean": round(float(np.mean([x[1] for x in idf_steps])), 4),
+                    "wait_ms_mean": round(float(np.mean([x[2] for x in idf_steps])), 4)},
             "k1_work": {"chunks": int(info["nchunks"]), "partial_records": int(info["partial_records"]),
                         "vocab_capacity": int(info["vocab_capacity"]), "terms": int(info["nterms"])},
             "roofline": {"bound": "hbm", "kernel": f"{kern} (K1)", "achieved": round(achieved, 2),
@@ -499,6 +609,8 @@ def main():
                          "note": "first tfidf_run of a fresh context (warmup step 1): vocabulary/record "
                                  "capacity retries, the idf table of this N, first allocations; not in value"},
         }
+        if c3_line is not None:
+            line["c3_strong"] = c3_line
         if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
             hi = host_cpu_info()
             thr = args.cpu_threads or hi["affinity"]

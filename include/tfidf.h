@@ -102,36 +102,43 @@ int tfidf_abi_version(void);
 
 /* ---- multi-GPU: one process per GPU; replaces MPI_Init/Comm_size/Comm_rank
  *      (TFIDF.c:82,91-92) and the DF combine MPI_Reduce(CustomReduce)+MPI_Bcast
- *      (TFIDF.c:209-222,291-326) with RCCL collectives over xGMI: each term's global df is
- *      summed by an owner rank (a hash of the term) after an all-to-all of (term, df) and
- *      returned by a second all-to-all (grouped ncclSend / ncclRecv). */
+ *      (TFIDF.c:209-222,291-326) with RCCL collectives over xGMI, in one of two forms
+ *      chosen alike by every rank from the agreed per-rank term counts:
+ *        dense (every rank's V <= 2^17, the default for c2/c3/c5-size shards): the ranks'
+ *          term keys are all-gathered, numbered identically on every rank, and ONE
+ *          ncclAllReduce (sum) of a u32 df vector over those numbers gives the global df;
+ *        hash-owner (larger V, e.g. 10^7 terms): each term's df is summed by an owner rank
+ *          (a hash of the term) after an all-to-all of (term, df) and returned by a second
+ *          all-to-all (grouped ncclSend / ncclRecv).
+ *      TFIDF_XCHG=dense|owner|dense_table forces a form. */
 #define TFIDF_UNIQUE_ID_BYTES 128
 int tfidf_comm_unique_id(uint8_t id[TFIDF_UNIQUE_ID_BYTES]);
-/* Attaches an RCCL communicator rank (ncclCommInitRank).  From then on every tfidf_run
+/* Attaches an RCCL communicator rank (ncclCommInitRankConfig).  From then on every tfidf_run
  * of this context is collective: all ranks call it, each on its own shard (contiguous
  * ranges of the "docN@" order, ndocs_total = N of the whole corpus).  Capacity retries
  * are agreed between the ranks (all repeat or none does); a rank whose run fails makes
  * the others return TFIDF_E_PEER instead of waiting.
- * Abort contract: a failure agreed before the exchange's collectives (a local error, a
- * capacity retry) needs nothing from the caller.  A rank-local failure AFTER the agreement
- * (inside the count all-gather / (key, df) all-to-all sequence) aborts this rank's communicator; its
- * peers may then be blocked inside a collective, and with one process per GPU only the
- * caller can reach them: it must make every other rank call ncclCommAbort on its own
- * communicator (e.g. by tfidf_close on those contexts after its out-of-band failure notice)
- * — tfidf_group_* does exactly this for its clique.  A context whose communicator was
- * aborted returns TFIDF_E_PEER / TFIDF_E_STATE from then on: close and reopen it. */
+ * Abort contract: the communicator is created non-blocking (a peer that never joins makes
+ * this call return TFIDF_E_PEER after TFIDF_COMM_TIMEOUT_S seconds, default 600, 0 = no
+ * limit), and every RCCL call and every wait for a collective's kernels is polled.  A
+ * failure agreed before the exchange's collectives (a local error, a capacity retry) needs
+ * nothing from the caller.  A rank-local failure AFTER the agreement aborts this rank's
+ * communicator; a peer process waiting for it gives up at the same deadline (or when RCCL
+ * reports the peer's failure) and aborts its own.  A context whose communicator was aborted
+ * returns TFIDF_E_PEER from then on: close and reopen it. */
 int tfidf_comm_init(tfidf_ctx* ctx, const uint8_t id[TFIDF_UNIQUE_ID_BYTES], int rank, int nranks);   /* nranks <= 1024 */
 
 /* ---- one process, several shards: the drop-in for `mpirun -np P ./TFIDF`
  *      (TFIDF.c:82-92 process group, :125-130 document -> rank assignment, :253-273
  *      gather + sort).  Rank r runs on devices[r] (NULL: device r).  When every rank has
- *      its own GPU the ranks are one RCCL clique (ncclCommInitAll); when a device is
- *      listed more than once (or TFIDF_GROUP_LOCAL is set) they exchange through device
- *      copies in this process — same engine code, same results.  An error on one rank
- *      inside the exchange aborts EVERY communicator of the clique, so no peer stays
- *      blocked in a collective; the other ranks return TFIDF_E_PEER.  An RCCL group is
- *      unusable after such an abort (close and reopen it); an in-process group starts its
- *      next tfidf_group_run afresh. */
+ *      its own GPU the ranks are one RCCL clique (non-blocking communicators created in one
+ *      ncclGroupStart/End); when a device is listed more than once (or TFIDF_GROUP_LOCAL is
+ *      set) they exchange through device copies in this process — same engine code, same
+ *      results.  An error on one rank inside the exchange sets the clique's abort flag: every
+ *      rank, wherever it waits (inside an RCCL call, for a collective's kernels, or at its
+ *      next call), aborts its own communicator at its next poll, so no peer stays blocked; the
+ *      other ranks return TFIDF_E_PEER.  An RCCL group is unusable after such an abort (close
+ *      and reopen it); an in-process group starts its next tfidf_group_run afresh. */
 #define TFIDF_GROUP_LOCAL 1u
 typedef struct tfidf_group tfidf_group;
 int tfidf_group_open(int nranks, const int* devices, uint32_t flags, tfidf_group** out);
@@ -179,6 +186,13 @@ typedef struct tfidf_run_info {
      * steady-state runs reads them before and after and expects no change */
     uint64_t device_allocs;
     uint64_t device_alloc_bytes;
+    /* the run's idf table, log(N/df) on the host's libm (TFIDF.c:243): up to 2^24 documents
+     * every df = 1..N is tabulated on host threads while the device runs the stages before
+     * the score (beyond that only the distinct df values, after the DF stage) */
+    uint64_t idf_logs;        /* libm log() calls made for this run's table (0: the table of
+                                 the previous run's N was kept, TFIDF_IDF_CACHE=1) */
+    double   ms_idf_host;     /* wall time of those calls (host threads) */
+    double   ms_idf_wait;     /* time the run waited for them before the score stage */
 } tfidf_run_info;
 #define TFIDF_RUN_K1_VS   2u  /* slot-keyed tokenize+count kernel (the default path; the general
                                  kernel of TFIDF_K1=general or an unaligned corpus leaves it clear) */

@@ -27,6 +27,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <mutex>
 #include <string>
@@ -166,6 +167,19 @@ struct tfidf_ctx {
     DevBuf big_list, big_idx, dense_cnt, kcnt, tile_cnt;   /* dense merge of long documents */
     DevBuf df_local, df_global, present, idf_vals;
     uint64_t idf_full_n = 0;   /* idf_vals holds log(N/df) for df = 0..N of this N (0: not) */
+    /* the per-run idf table (N <= IDF_FULL_MAX): host threads fill the pinned idf_pin with
+     * log(N/df) for df = 0..N while the device runs the stages before the score; run_post
+     * joins them and uploads it.  TFIDF_IDF_CACHE=1 keeps the table of an unchanged N
+     * instead (round 4's behaviour; the bench reports which) */
+    bool idf_cache = false;
+    double* idf_pin = nullptr;
+    size_t idf_pin_n = 0;
+    hipEvent_t ev_idf = nullptr;          /* the table's upload (idf_pin reusable after it) */
+    std::vector<std::thread> idf_th;
+    std::vector<int64_t> idf_end_ns;      /* per thread: when it finished */
+    std::chrono::steady_clock::time_point idf_t0;
+    uint64_t idf_logs = 0;                /* log() calls of the last run */
+    double ms_idf_host = 0, ms_idf_wait = 0;
     DevBuf dkey0, dkey1, dseq0, dseq1, npairs_ord, out_off, doc_meta;
     DevBuf out_term, out_cnt, out_score, idf_rank, large_list, split_tasks, cls_off;
     /* DF exchange (hash owners): this rank's keys by term rank, the send side grouped by
@@ -211,7 +225,6 @@ struct tfidf_ctx {
     double ms_stage[S_NSTAGES] = {0};
     double ms_total = 0;
     hipError_t last_err = hipSuccess;
-    ncclResult_t last_nccl = ncclSuccess;
 };
 
 #define HIPCHK(x)                                                                          \
@@ -223,13 +236,15 @@ struct tfidf_ctx {
             return TFIDF_E_HIP;                                                            \
         }                                                                                  \
     } while (0)
-#define NCCLCHK(x)                                                                         \
+/* a wait for the run's stream once collectives may be in it: through the transport, so
+ * that a failed peer cannot leave this rank waiting (xport.h, comm_rank.h) */
+#define XSYNC(s_)                                                                          \
     do {                                                                                   \
-        ncclResult_t r_ = (x);                                                             \
-        if (r_ != ncclSuccess) {                                                           \
-            ctx->last_nccl = r_;                                                           \
-            fprintf(stderr, "tfidf: RCCL error %s at %s:%d\n", ncclGetErrorString(r_), __FILE__, __LINE__); \
-            return TFIDF_E_RCCL;                                                           \
+        if (ctx->xp) {                                                                     \
+            const int w_ = ctx->xp->wait(s_);                                              \
+            if (w_) return w_;                                                             \
+        } else {                                                                           \
+            HIPCHK(hipStreamSynchronize(s_));                                              \
         }                                                                                  \
     } while (0)
 #define ENSURE(buf, bytes)                                   \
@@ -317,6 +332,11 @@ int tfidf_open(int device, tfidf_ctx** out) {
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ctx->ev_order, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ctx->ev_idf, hipEventDisableTiming));
+    {
+        const char* ic = getenv("TFIDF_IDF_CACHE");
+        ctx->idf_cache = ic && ic[0] == '1';
+    }
     for (int i = 0; i <= S_NSTAGES; ++i) HIPCHK(hipEventCreate(&ctx->ev[i]));
     if (arena_reset(ctx, 64ull << 20) != 0) { delete ctx; return TFIDF_E_NOMEM; }
     if (ctx->counters.ensure(256) != 0) { delete ctx; return TFIDF_E_NOMEM; }
@@ -335,6 +355,9 @@ void tfidf_close(tfidf_ctx* ctx) {
     if (ctx->stream2) { (void)hipStreamSynchronize(ctx->stream2); (void)hipStreamDestroy(ctx->stream2); }
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_order) (void)hipEventDestroy(ctx->ev_order);
+    for (auto& t : ctx->idf_th) t.join();
+    if (ctx->ev_idf) { (void)hipEventSynchronize(ctx->ev_idf); (void)hipEventDestroy(ctx->ev_idf); }
+    if (ctx->idf_pin) (void)hipHostFree(ctx->idf_pin);
     for (int i = 0; i < WR_NBUF; ++i) {
         if (ctx->wr_buf[i]) (void)hipHostFree(ctx->wr_buf[i]);
         if (ctx->wr_ev[i]) (void)hipEventDestroy(ctx->wr_ev[i]);
@@ -386,11 +409,11 @@ int tfidf_comm_init(tfidf_ctx* ctx, const uint8_t id[TFIDF_UNIQUE_ID_BYTES], int
     if (!ctx || !id || nranks < 1 || nranks > 1024 || rank < 0 || rank >= nranks) return TFIDF_E_INVAL;
     HIPCHK(hipSetDevice(ctx->device));
     tfidf_ctx_attach_xport(ctx, nullptr);
-    ncclUniqueId u;
-    memcpy(&u, id, TFIDF_UNIQUE_ID_BYTES);
-    ncclComm_t comm = nullptr;
-    NCCLCHK(ncclCommInitRank(&comm, nranks, u, rank));
-    return tfidf_ctx_attach_xport(ctx, make_rccl_xport(comm, rank, nranks, ctx->device));
+    static_assert(sizeof(ncclUniqueId) == TFIDF_UNIQUE_ID_BYTES, "unique id size");
+    Xport* x = nullptr;
+    const int rc = rccl_init_rank(id, rank, nranks, ctx->device, &x);
+    if (rc) return rc;
+    return tfidf_ctx_attach_xport(ctx, x);
 }
 
 }  // extern "C"
@@ -526,7 +549,7 @@ static int exchange_owner(tfidf_ctx* ctx, uint32_t V, const std::vector<uint64_t
     if (rc) return rc;
     std::vector<uint32_t> m((size_t)R * (R + 1));
     HIPCHK(hipMemcpyAsync(m.data(), mat, m.size() * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    XSYNC(s);
     int peer_fail = 0;
     for (int p = 0; p < R; ++p)
         if (m[(size_t)p * (R + 1) + R]) peer_fail = 1;
@@ -653,27 +676,34 @@ static int exchange_dense(tfidf_ctx* ctx, uint32_t V, const std::vector<uint64_t
 
 static int exchange_df(tfidf_ctx* ctx, int local_rc, uint32_t V) {
     std::vector<uint64_t> vs;
-    /* the dense form's buffers, sized from this rank's V before the agreement (any failure
-     * is agreed in step 1: no extra exchange for it) */
+    /* the dense form's buffers, sized from this rank's V before the agreement; a failure
+     * travels as bit 33 of step 1's word (no extra exchange): the ranks then take the owner
+     * form, which sizes its own buffers, unless the dense form is forced */
+    bool dense_nomem = false;
     if (local_rc == 0 && (ctx->xchg_mode >= 2 || (ctx->xchg_mode == 0 && V <= DENSE_XCHG_MAXV))) {
         int arc = dense_alloc(ctx, V, dense_pad(V), (uint64_t)ctx->xp->nranks);
-        if (ctx->xnomem_rank == ctx->xp->rank) {   /* tests: an agreed allocation failure (once) */
+        if (ctx->xnomem_rank == ctx->xp->rank && ctx->xchg_mode != 1) {   /* tests: an allocation failure (once) */
             ctx->xnomem_rank = -1;
             arc = TFIDF_E_NOMEM;
         }
-        if (arc) local_rc = arc;
+        dense_nomem = arc != 0;
     }
-    /* step 1; bit 32 of the word: this rank holds terms of >= 16 bytes */
-    int rc = exchange_agree(ctx, local_rc, (uint64_t)V | (ctx->local_long ? 1ull << 32 : 0ull), &vs);
+    /* step 1; bit 32 of the word: this rank holds terms of >= 16 bytes; bit 33: its dense
+     * buffers could not be allocated */
+    int rc = exchange_agree(ctx, local_rc,
+                            (uint64_t)V | (ctx->local_long ? 1ull << 32 : 0ull) | (dense_nomem ? 1ull << 33 : 0ull), &vs);
     if (rc) return rc;
     uint64_t maxv = 0;
-    bool any_long = false;
+    bool any_long = false, any_dense_nomem = false;
     for (uint64_t& x : vs) {
-        any_long |= (x >> 32) != 0;
+        any_long |= ((x >> 32) & 1u) != 0;
+        any_dense_nomem |= ((x >> 33) & 1u) != 0;
         x &= 0xFFFFFFFFull;
         maxv = x > maxv ? x : maxv;
     }
-    const bool dense = ctx->xchg_mode >= 2 || (ctx->xchg_mode == 0 && maxv <= DENSE_XCHG_MAXV);
+    if (any_dense_nomem && ctx->xchg_mode >= 2)   /* the dense form forced: an agreed failure */
+        return dense_nomem ? TFIDF_E_NOMEM : TFIDF_E_PEER;
+    const bool dense = ctx->xchg_mode >= 2 || (ctx->xchg_mode == 0 && maxv <= DENSE_XCHG_MAXV && !any_dense_nomem);
     ctx->last_dense = dense;
     bool agreed = false;
     rc = dense ? exchange_dense(ctx, V, vs, !any_long && ctx->xchg_mode != 3, &agreed)
@@ -1013,6 +1043,57 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     return 0;
 }
 
+/* ---- the per-run idf table: log(N/df) for every df = 0..N on the host's libm
+ * (TFIDF.c:243 evaluates log(1.0*N/df) per pair; the table holds the same doubles), on up to
+ * eight host threads started when the run starts, so the logs run beside K1 .. DF on the
+ * device.  run_post waits for them (ms_idf_wait: normally 0) and uploads the table. */
+static int idf_start(tfidf_ctx* ctx, uint64_t Nt) {
+    ctx->idf_logs = 0;
+    ctx->ms_idf_host = ctx->ms_idf_wait = 0;
+    if (Nt > IDF_FULL_MAX) return TFIDF_OK;                          /* distinct-df path in run_post */
+    if (ctx->idf_cache && ctx->idf_full_n == Nt) return TFIDF_OK;    /* TFIDF_IDF_CACHE=1 */
+    HIPCHK(hipEventSynchronize(ctx->ev_idf));   /* the previous upload has read idf_pin */
+    const size_t n = (size_t)Nt + 1;
+    if (ctx->idf_pin_n < n) {
+        if (ctx->idf_pin) (void)hipHostFree(ctx->idf_pin);
+        ctx->idf_pin = nullptr;
+        ctx->idf_pin_n = 0;
+        if (hipHostMalloc((void**)&ctx->idf_pin, n * 8, hipHostMallocDefault) != hipSuccess) return TFIDF_E_NOMEM;
+        ctx->idf_pin_n = n;
+    }
+    ctx->idf_full_n = 0;   /* idf_vals is rewritten by this run */
+    const unsigned nt = (unsigned)(n / 8192 < 1 ? 1 : (n / 8192 > 8 ? 8 : n / 8192));
+    ctx->idf_end_ns.assign(nt, 0);
+    ctx->idf_t0 = std::chrono::steady_clock::now();
+    double* lut = ctx->idf_pin;
+    lut[0] = 0.0;   /* df >= 1 for every term that occurs */
+    for (unsigned t = 0; t < nt; ++t) {
+        const uint64_t lo = 1 + (Nt * t) / nt, hi = 1 + (Nt * (t + 1)) / nt;
+        ctx->idf_th.emplace_back([ctx, lut, lo, hi, Nt, t] {
+            for (uint64_t d = lo; d < hi; ++d) lut[d] = log(1.0 * (double)Nt / (double)d);
+            ctx->idf_end_ns[t] = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                     std::chrono::steady_clock::now() - ctx->idf_t0).count();
+        });
+    }
+    ctx->idf_logs = Nt;
+    return TFIDF_OK;
+}
+/* joins the table's threads (also on every error path of tfidf_run) */
+static void idf_join(tfidf_ctx* ctx) {
+    if (ctx->idf_th.empty()) return;
+    const auto w0 = std::chrono::steady_clock::now();
+    for (auto& t : ctx->idf_th) t.join();
+    ctx->idf_th.clear();
+    ctx->ms_idf_wait = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+    int64_t e = 0;
+    for (int64_t x : ctx->idf_end_ns) e = x > e ? x : e;
+    ctx->ms_idf_host = (double)e * 1e-6;
+}
+struct IdfJoin {
+    tfidf_ctx* c;
+    ~IdfJoin() { idf_join(c); }
+};
+
 /* The stages after the DF exchange: idf LUT, document order, score.  They never return 1
  * (run_local checked their scratch before the exchange), so no rank can ever enter the
  * collectives of a repeated attempt alone: every `return` below is an error or success. */
@@ -1035,13 +1116,14 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
     constexpr uint32_t IDF_SPEC = 16384;
     std::vector<uint32_t> vals;
     if (full_lut) {
-        if (ctx->idf_full_n != Nt) {
+        if (!ctx->idf_th.empty()) {   /* this run's table (idf_start): join, upload */
             ENSURE(ctx->idf_vals, (size_t)(Nt + 1) * 8);
-            std::vector<double> lut(Nt + 1);
-            lut[0] = 0.0;   /* df >= 1 for every term that occurs */
-            for (uint64_t d = 1; d <= Nt; ++d) lut[d] = log(1.0 * (double)Nt / (double)d);
-            HIPCHK(hipMemcpy(ctx->idf_vals.p, lut.data(), (size_t)(Nt + 1) * 8, hipMemcpyHostToDevice));
+            idf_join(ctx);
+            HIPCHK(hipMemcpyAsync(ctx->idf_vals.p, ctx->idf_pin, (size_t)(Nt + 1) * 8, hipMemcpyHostToDevice, s));
+            HIPCHK(hipEventRecord(ctx->ev_idf, s));
             ctx->idf_full_n = Nt;
+        } else if (ctx->idf_full_n != Nt) {
+            return TFIDF_E_STATE;   /* idf_start made no table and none is cached: not reachable */
         }
     } else {
         ctx->idf_full_n = 0;   /* idf_vals is rewritten below */
@@ -1068,7 +1150,7 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
                             ctx->npairs_ord.as<uint64_t>(), ctx->doc_meta.as<uint4>(), s));
     XCHK(scan_excl_u64(ctx->npairs_ord.as<uint64_t>(), ctx->out_off.as<uint64_t>(), N, ar, s));
     if (!full_lut) {
-        HIPCHK(hipStreamSynchronize(s));
+        XSYNC(s);
         const uint32_t spec = (uint32_t)vals.size();
         if (K > spec) {
             vals.resize(K);
@@ -1135,7 +1217,7 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
     HIPCHK(hipMemcpyAsync(ctx->hpin + 10, cnt + 3, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(ctx->hpin + 11, ctx->out_off.as<uint64_t>() + N, 8, hipMemcpyDeviceToHost, s));
     if (ctx->xp) HIPCHK(hipMemcpyAsync(ctx->hpin + 14, cnt + 12, 4, hipMemcpyDeviceToHost, s));   /* global V */
-    HIPCHK(hipStreamSynchronize(s));
+    XSYNC(s);
     const uint32_t st_end = (uint32_t)ctx->hpin[10];
     const uint64_t P = ctx->hpin[11];
     ctx->npairs = P;
@@ -1232,6 +1314,12 @@ extern "C" int tfidf_run(tfidf_ctx* ctx, const tfidf_corpus* in) {
     }
     hipStream_t s = ctx->stream;
     const uint32_t N = in->ndocs;
+    IdfJoin idf_guard{ctx};
+    rc = idf_start(ctx, Nt);
+    if (rc) {
+        if (ctx->xp) (void)exchange_agree(ctx, rc, 0, nullptr);
+        return rc;
+    }
     rc = 1;
     for (int attempt = 0; attempt < 8 && rc == 1; ++attempt) {
         const size_t need = ctx->arena.peak > ctx->arena_buf.cap ? ctx->arena.peak * 2 : ctx->arena_buf.cap;
@@ -1350,6 +1438,9 @@ extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* out) {
                   (ctx->xp && ctx->last_dense ? TFIDF_RUN_XCHG_DENSE : 0u);
     info->device_allocs = g_dev_allocs.load(std::memory_order_relaxed);
     info->device_alloc_bytes = g_dev_alloc_bytes.load(std::memory_order_relaxed);
+    info->idf_logs = ctx->idf_logs;
+    info->ms_idf_host = ctx->ms_idf_host;
+    info->ms_idf_wait = ctx->ms_idf_wait;
     full.size = want;
     memcpy(out, &full, want);
     return TFIDF_OK;
@@ -1765,12 +1856,16 @@ extern "C" int tfidf_write_output_gpu(tfidf_ctx* ctx, const char* path, int appe
     issuer.join();
     for (auto& t : th) t.join();
     (void)hipStreamSynchronize(cs);
-    if (close(fd) != 0 && !wrc) wrc = TFIDF_E_OUTPUT;
     rc = wrc;
     if (fmt) {
         const int r2 = format_finish(ctx, total);   /* synchronises the main stream */
         if (!rc) rc = r2;
+        /* a formatting error (a score outside the %.16f range: ST_BOUNDS) found after the
+         * blocks were written: no complete-looking file is left behind — the file (or the
+         * appended shard) is cut back to where this call started */
+        if (r2 && regular) (void)!ftruncate(fd, (off_t)base);
     }
+    if (close(fd) != 0 && !rc) rc = TFIDF_E_OUTPUT;
     oi.text_bytes = total;
     oi.ms_d2h_busy = nblk ? t_last_copy - t_prep : 0.0;
     oi.ms_write = write_ms;

@@ -33,83 +33,126 @@
 #include "../../include/tfidf.h"
 #include "kernels.h"
 #include "xport.h"
+#include "comm_rank.h"
 
 namespace {
 
 /* ------------------------------------------------------------------ RCCL -- */
 
-/* The communicators of one tfidf_group clique (ncclCommInitAll in one process, one host
- * thread per rank).  Each rank's communicator has its own lock, held only by that rank's
- * thread while it enqueues a collective: RCCL connects peers lazily inside those calls and
- * blocks until the peer ranks make the matching call, so a lock shared by the clique would
- * deadlock the first collective (rank A inside ncclGroupEnd waiting for B, B waiting for the
- * lock).  An error on one rank after the agreement aborts every communicator of the clique:
- * a peer already waiting for a collective's kernels (the stream synchronisation after it) is
- * released by the abort of its own communicator.  abort_all takes each rank's lock in turn
- * (bounded wait) so no communicator is freed while its thread is inside an RCCL call; a rank
- * whose lock it could not take aborts its own communicator when its call returns. */
+/* RCCL behind comm_rank.h's abort protocol: communicators are non-blocking, every call and
+ * every wait for a collective's kernels is a poll that also watches the clique's `aborted`
+ * flag, and each rank only ever aborts its own communicator (from its own thread). */
+struct RcclB {
+    using Comm = ncclComm_t;
+    static int async(Comm c) {
+        ncclResult_t st = ncclSuccess;
+        if (ncclCommGetAsyncError(c, &st) != ncclSuccess) return TFIDF_E_RCCL;
+        return st == ncclInProgress ? 1 : (st == ncclSuccess ? 0 : TFIDF_E_RCCL);
+    }
+    static void abort(Comm c) { (void)ncclCommAbort(c); }
+};
+static int nccl_issue(ncclResult_t r) { return r == ncclSuccess ? 0 : (r == ncclInProgress ? 1 : TFIDF_E_RCCL); }
+
+/* Finalizes (non-blocking: all at once, then polled) and destroys the live communicators of
+ * one process — a clique's ranks must not be finalized one after the other, since a
+ * finalize may wait for the peers'. Communicators that do not finalize within the deadline
+ * are aborted. */
+static void comms_close(std::vector<ncclComm_t>& comms, int64_t timeout_ms) {
+    std::vector<int> st(comms.size(), 0);   /* 1 finalizing, 2 finalized, -1 failed */
+    for (size_t r = 0; r < comms.size(); ++r)
+        if (comms[r]) st[r] = nccl_issue(ncclCommFinalize(comms[r])) < 0 ? -1 : 1;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (bool busy = true; busy;) {
+        busy = false;
+        for (size_t r = 0; r < comms.size(); ++r) {
+            if (st[r] != 1) continue;
+            const int a = RcclB::async(comms[r]);
+            if (a == 1) busy = true;
+            else st[r] = a == 0 ? 2 : -1;
+        }
+        if (busy && timeout_ms > 0 && std::chrono::duration_cast<std::chrono::milliseconds>(
+                                          std::chrono::steady_clock::now() - t0).count() > timeout_ms) {
+            for (size_t r = 0; r < comms.size(); ++r)
+                if (st[r] == 1) st[r] = -1;
+            break;
+        }
+        if (busy) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+    for (size_t r = 0; r < comms.size(); ++r) {
+        if (!comms[r]) continue;
+        if (st[r] == 2) (void)ncclCommDestroy(comms[r]);
+        else (void)ncclCommAbort(comms[r]);
+        comms[r] = nullptr;
+    }
+}
+
+/* The communicators of one tfidf_group clique (one process, one host thread per rank).
+ * Created together (non-blocking ncclCommInitRankConfig in one group), closed together;
+ * during runs rank r's communicator is touched by rank r's thread only. */
 struct Clique {
     std::vector<ncclComm_t> comms;
-    std::vector<std::unique_ptr<std::mutex>> mu;   /* one per rank */
-    std::atomic<bool> aborted{false};
-    explicit Clique(int n) : comms((size_t)n, nullptr) {
-        for (int r = 0; r < n; ++r) mu.emplace_back(new std::mutex());
-    }
+    std::vector<char> dead;                 /* rank r aborted its communicator (written by rank r) */
+    std::shared_ptr<CommShared> shared = std::make_shared<CommShared>();
+    int64_t timeout_ms = comm_timeout_ms_from_env();
+    explicit Clique(int n) : comms((size_t)n, nullptr), dead((size_t)n, 0) {}
     ~Clique() {
-        for (ncclComm_t c : comms)
-            if (c) (void)ncclCommDestroy(c);
-    }
-    /* with mu[r] held */
-    void abort_rank_locked(int r) {
-        if (comms[r]) { (void)ncclCommAbort(comms[r]); comms[r] = nullptr; }
-    }
-    void abort_all() {
-        aborted.store(true);
-        for (size_t r = 0; r < comms.size(); ++r) {
-            for (int t = 0; t < 2000; ++t) {   /* up to ~2 s per rank */
-                if (mu[r]->try_lock()) {
-                    abort_rank_locked((int)r);
-                    mu[r]->unlock();
-                    break;
-                }
-                std::this_thread::sleep_for(std::chrono::milliseconds(1));
-            }
-        }
+        for (size_t r = 0; r < comms.size(); ++r)
+            if (dead[r]) comms[r] = nullptr;   /* ncclCommAbort freed it */
+        comms_close(comms, timeout_ms);
     }
 };
 
+/* polls every communicator of a non-blocking init until it is ready (0), failed or timed out */
+static int comms_ready(std::vector<ncclComm_t>& comms, int64_t timeout_ms) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        bool busy = false;
+        for (ncclComm_t c : comms) {
+            const int a = c ? RcclB::async(c) : TFIDF_E_RCCL;
+            if (a < 0) return a;
+            busy |= a == 1;
+        }
+        if (!busy) return TFIDF_OK;
+        if (timeout_ms > 0 && std::chrono::duration_cast<std::chrono::milliseconds>(
+                                  std::chrono::steady_clock::now() - t0).count() > timeout_ms)
+            return TFIDF_E_PEER;
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
 struct RcclXport final : Xport {
-    ncclComm_t own = nullptr;              /* a single-rank-per-process communicator (tfidf_comm_init) */
-    std::shared_ptr<Clique> clique;        /* ... or this rank's communicator in a group clique */
+    CommRank<RcclB> cr;                    /* this rank's communicator and the clique's flag */
+    std::shared_ptr<Clique> clique;        /* a tfidf_group clique owns the communicator; else this */
     int device = 0;
     uint64_t* dwords = nullptr;   /* 2 (send) + 2 * nranks (recv) */
     ~RcclXport() override {
-        if (own) (void)ncclCommDestroy(own);
+        if (!clique && !cr.dead && cr.comm) {
+            std::vector<ncclComm_t> one{cr.comm};
+            comms_close(one, cr.timeout_ms);
+        }
         if (dwords) (void)hipFree(dwords);
     }
-    /* enqueues f(comm) under this rank's lock; TFIDF_E_PEER once the clique was aborted */
-    template <class F> int enqueue(F&& f) {
-        if (clique) {
-            std::lock_guard<std::mutex> lk(*clique->mu[rank]);
-            if (clique->aborted.load() || !clique->comms[rank]) {
-                clique->abort_rank_locked(rank);
-                return TFIDF_E_PEER;
-            }
-            const ncclResult_t r = f(clique->comms[rank]);
-            if (clique->aborted.load()) {   /* aborted while this call ran: release our kernels */
-                clique->abort_rank_locked(rank);
-                return TFIDF_E_PEER;
-            }
-            return r == ncclSuccess ? TFIDF_OK : TFIDF_E_RCCL;
-        }
-        if (!own) return TFIDF_E_STATE;
-        return f(own) == ncclSuccess ? TFIDF_OK : TFIDF_E_RCCL;
+    void note_dead() {
+        if (clique && cr.dead) clique->dead[rank] = 1;
     }
-    /* a synchronisation that an abort of the clique released reports TFIDF_E_PEER */
-    int sync(hipStream_t s) {
-        const hipError_t e = hipStreamSynchronize(s);
-        if (clique && clique->aborted.load()) return TFIDF_E_PEER;
-        return e == hipSuccess ? TFIDF_OK : TFIDF_E_HIP;
+    /* one RCCL call f(comm) and its completion; TFIDF_E_PEER once the clique was aborted */
+    template <class F> int enqueue(F&& f) {
+        const int rc = cr.enqueue([&](ncclComm_t c) { return nccl_issue(f(c)); });
+        note_dead();
+        return rc;
+    }
+    /* the stream's work (a collective's kernels among it) done, polled; an abort of the
+     * clique aborts this rank's communicator, which releases kernels still waiting for a
+     * failed peer, and the stream is then drained */
+    int wait(hipStream_t s) override {
+        const int rc = cr.wait_stream([&] {
+            const hipError_t e = hipStreamQuery(s);
+            return e == hipSuccess ? 0 : (e == hipErrorNotReady ? 1 : TFIDF_E_HIP);
+        });
+        (void)hipGetLastError();   /* hipErrorNotReady must not linger as the thread's last error */
+        note_dead();
+        if (rc) (void)hipStreamSynchronize(s);
+        return rc;
     }
     int words(const uint64_t mine[2], uint64_t* all, hipStream_t s) override {
         if (!dwords && tfidf_dev_malloc((void**)&dwords, 16 * (size_t)(nranks + 1)) != hipSuccess) return TFIDF_E_NOMEM;
@@ -118,7 +161,7 @@ struct RcclXport final : Xport {
         if (rc) return rc;
         if (hipMemcpyAsync(all, dwords + 2, 16 * (size_t)nranks, hipMemcpyDeviceToHost, s) != hipSuccess)
             return TFIDF_E_HIP;
-        return sync(s);
+        return wait(s);
     }
     int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
         return enqueue([&](ncclComm_t c) { return ncclAllGather(send, recv, bytes, ncclUint8, c, s); });
@@ -136,15 +179,17 @@ struct RcclXport final : Xport {
                 ro += rcnt[p];
             }
             const ncclResult_t e = ncclGroupEnd();
-            return r != ncclSuccess ? r : e;
+            return (r != ncclSuccess && r != ncclInProgress) ? r : e;
         });
     }
     int allreduce_u32(uint32_t* buf, size_t n, hipStream_t s) override {
         return enqueue([&](ncclComm_t c) { return ncclAllReduce(buf, buf, n, ncclUint32, ncclSum, c, s); });
     }
+    /* this rank failed between collectives: the clique gives up (each peer aborts its own
+     * communicator at its next poll), this rank's communicator at once */
     void abort() override {
-        if (clique) clique->abort_all();
-        else if (own) { (void)ncclCommAbort(own); own = nullptr; }
+        cr.fail();
+        note_dead();
     }
     const char* name() const override { return "rccl"; }
 };
@@ -364,13 +409,35 @@ struct LocalXport final : Xport {
 
 }  // namespace
 
-Xport* make_rccl_xport(void* nccl_comm, int rank, int nranks, int device) {
+/* one rank of a process-per-GPU job (tfidf_comm_init): a non-blocking ncclCommInitRankConfig,
+ * polled until every rank joined (or the deadline: TFIDF_E_PEER) */
+int rccl_init_rank(const void* unique_id, int rank, int nranks, int device, Xport** out) {
+    *out = nullptr;
+    ncclUniqueId u;
+    memcpy(&u, unique_id, sizeof(u));
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclComm_t comm = nullptr;
+    if (hipSetDevice(device) != hipSuccess) return TFIDF_E_HIP;
+    const int64_t tmo = comm_timeout_ms_from_env();
+    if (nccl_issue(ncclCommInitRankConfig(&comm, nranks, u, rank, &cfg)) < 0 || !comm) {
+        if (comm) (void)ncclCommAbort(comm);
+        return TFIDF_E_RCCL;
+    }
+    std::vector<ncclComm_t> one{comm};
+    const int rc = comms_ready(one, tmo);
+    if (rc) {
+        (void)ncclCommAbort(comm);
+        return rc;
+    }
     RcclXport* x = new RcclXport();
-    x->own = (ncclComm_t)nccl_comm;
+    x->cr.comm = comm;
+    x->cr.timeout_ms = tmo;
     x->rank = rank;
     x->nranks = nranks;
     x->device = device;
-    return x;
+    *out = x;
+    return TFIDF_OK;
 }
 
 struct tfidf_group {
@@ -420,13 +487,36 @@ int tfidf_group_open(int nranks, const int* devices, uint32_t flags, tfidf_group
         }
     } else if (!rc) {
         /* one RCCL communicator per GPU of the clique (a 1-rank group gets one too, so the
-         * exchange path is the same at every size), owned by the clique so that an error on
-         * one rank aborts them all */
+         * exchange path is the same at every size), created non-blocking in one group and
+         * owned by the clique: an error on one rank makes every rank abort its own */
         auto cl = std::make_shared<Clique>(nranks);
-        if (ncclCommInitAll(cl->comms.data(), nranks, dev.data()) != ncclSuccess) rc = TFIDF_E_RCCL;
+        ncclUniqueId u;
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        if (ncclGetUniqueId(&u) != ncclSuccess) rc = TFIDF_E_RCCL;
+        if (!rc) {
+            ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+            cfg.blocking = 0;
+            int bad = nccl_issue(ncclGroupStart()) < 0;
+            for (int r = 0; r < nranks && !bad; ++r) {
+                if (hipSetDevice(dev[r]) != hipSuccess) bad = 1;
+                else bad = nccl_issue(ncclCommInitRankConfig(&cl->comms[r], nranks, u, r, &cfg)) < 0;
+            }
+            if (nccl_issue(ncclGroupEnd()) < 0) bad = 1;
+            (void)hipSetDevice(cur);
+            if (bad) rc = TFIDF_E_RCCL;
+            else rc = comms_ready(cl->comms, cl->timeout_ms);
+            if (rc) {   /* nothing usable: abort what was created */
+                for (ncclComm_t& c : cl->comms)
+                    if (c) { (void)ncclCommAbort(c); c = nullptr; }
+            }
+        }
         for (int r = 0; r < nranks && !rc; ++r) {
             RcclXport* x = new RcclXport();
             x->clique = cl;
+            x->cr.comm = cl->comms[r];
+            x->cr.shared = cl->shared;
+            x->cr.timeout_ms = cl->timeout_ms;
             x->rank = r;
             x->nranks = nranks;
             x->device = dev[r];

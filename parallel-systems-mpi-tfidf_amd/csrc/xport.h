@@ -43,6 +43,9 @@ struct Xport {
                           hipStream_t s) = 0;
     /* device all-reduce (sum) of n u32 in place: the dense DF exchange's one collective */
     virtual int allreduce_u32(uint32_t* buf, size_t n, hipStream_t s) = 0;
+    /* waits for the stream's work, collectives among it.  RcclXport polls, so that an abort
+     * of the clique releases a rank waiting for a failed peer's part (TFIDF_E_PEER) */
+    virtual int wait(hipStream_t s) { return hipStreamSynchronize(s) == hipSuccess ? 0 : -3 /* TFIDF_E_HIP */; }
     /* a rank failed between collectives: release the peers (they return errors) */
     virtual void abort() = 0;
     virtual const char* name() const = 0;
@@ -57,6 +60,7 @@ hipStream_t tfidf_ctx_stream(const tfidf_ctx* ctx);
 hipError_t tfidf_dev_malloc(void** p, size_t bytes);
 
 /* group.cpp */
-Xport* make_rccl_xport(void* nccl_comm, int rank, int nranks, int device);   /* takes the comm */
+/* a process-per-GPU rank: non-blocking ncclCommInitRankConfig with the job's unique id */
+int rccl_init_rank(const void* unique_id, int rank, int nranks, int device, Xport** out);
 
 #endif

@@ -68,6 +68,7 @@ class RunInfo(C.Structure):
         ("ndocs", C.c_uint32), ("vocab_capacity", C.c_uint32), ("ms_total", C.c_double),
         ("ms_tokcount", C.c_double), ("ms_stage", C.c_double * 16), ("nstages", C.c_uint32), ("flags", C.c_uint32),
         ("device_allocs", C.c_uint64), ("device_alloc_bytes", C.c_uint64),
+        ("idf_logs", C.c_uint64), ("ms_idf_host", C.c_double), ("ms_idf_wait", C.c_double),
     ]
 
 

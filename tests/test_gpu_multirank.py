@@ -210,6 +210,24 @@ def test_exchange_agreed_alloc_failure_keeps_group_usable(failing, xchg, monkeyp
         assert b"".join(g.ranks[r].text() for r in range(3)) == ora["output_txt"]
 
 
+def test_dense_prealloc_failure_falls_back_to_owner_form(monkeypatch):
+    """Auto form: one rank cannot allocate the dense form's buffers (TFIDF_TEST_XNOMEM_RANK
+    fires at their pre-allocation).  The failure travels as a flag of the first agreement,
+    every rank takes the hash-owner form instead (which sizes its own buffers), and the run
+    succeeds with the oracle's output — the group does not fail with NOMEM."""
+    shards = _shards("c2", 0.001, 3)
+    monkeypatch.delenv("TFIDF_XCHG", raising=False)
+    monkeypatch.setenv("TFIDF_TEST_XNOMEM_RANK", "1")
+    with tfidf_abi.Group(3, devices=[0, 0, 0]) as g:
+        g.run_host(shards)
+        assert not (g.ranks[0].info()["flags"] & tfidf_abi.RUN_XCHG_DENSE)
+        ora = _full("c2", 0.001)
+        assert b"".join(g.ranks[r].text() for r in range(3)) == ora["output_txt"]
+        g.run_host(shards)   # the next run: every rank allocates, the dense form again
+        assert g.ranks[0].info()["flags"] & tfidf_abi.RUN_XCHG_DENSE
+        assert b"".join(g.ranks[r].text() for r in range(3)) == ora["output_txt"]
+
+
 @pytest.mark.parametrize("xchg", ["dense", "owner"])
 def test_rccl_single_rank_runs_the_exchange(xchg, monkeypatch):
     """A 1-rank RCCL communicator: exchange_df runs (agreement; dense: the key ncclAllGather
@@ -315,3 +333,57 @@ def test_c3_sharded_over_8_properties():
     N = plans[0]["ndocs_total"]
     ref = (cnt / cat["docsize"].astype(np.float64)) * np.log(N / cat["df"].astype(np.float64))
     np.testing.assert_allclose(cat["score"], ref, rtol=1e-12, atol=1e-300)
+
+
+_INIT_TIMEOUT_CHILD = r"""
+import sys, time
+sys.path.insert(0, sys.argv[1])
+import tfidf_abi
+with tfidf_abi.Engine(0) as e:
+    t0 = time.time()
+    try:
+        e.comm_init(tfidf_abi.comm_unique_id(), 0, 2)   # rank 1 never joins
+        print("RESULT joined")
+    except tfidf_abi.TfidfError as ex:
+        print("RESULT rc=%d after %.1f s" % (ex.rc, time.time() - t0))
+"""
+
+
+def test_rccl_init_peer_never_joins_times_out():
+    """Process-per-GPU mode: rank 0 of a 2-rank job whose peer never calls tfidf_comm_init.
+    The communicator is created non-blocking and polled (comm_rank.h), so the call gives up
+    at TFIDF_COMM_TIMEOUT_S with TFIDF_E_PEER and aborts it, instead of blocking forever the
+    way the reference's ranks wait for mpirun to kill them (TFIDF.c:122,137).  Run in a child
+    process with its own time limit, so a regression fails this test instead of hanging."""
+    import subprocess
+    import sys
+    env = dict(os.environ, TFIDF_COMM_TIMEOUT_S="3")
+    pydir = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                         "parallel-systems-mpi-tfidf_amd", "python")
+    r = subprocess.run([sys.executable, "-c", _INIT_TIMEOUT_CHILD, pydir], env=env, capture_output=True,
+                       text=True, timeout=90)
+    out = [l for l in r.stdout.splitlines() if l.startswith("RESULT")]
+    assert out, r.stdout + r.stderr
+    assert out[0].startswith("RESULT rc=-11"), out[0]   # TFIDF_E_PEER
+    secs = float(out[0].split("after ")[1].split(" ")[0])
+    assert 2.5 <= secs < 30, out[0]
+
+
+@pytest.mark.parametrize("xchg", ["dense", "owner"])
+def test_rccl_clique_failure_releases_peers(xchg, monkeypatch):
+    """An RCCL clique over distinct GPUs (skipped on a 1-GPU box): a rank-local failure
+    inside the exchange (TFIDF_TEST_XFAIL_RANK, after the first collective) releases the peer
+    waiting in the next collective: every rank aborts its own communicator at its next poll
+    (comm_rank.h), the group reports the failing rank's error, and nobody hangs."""
+    if tfidf_abi.device_count() < 2:
+        pytest.skip("needs two GPUs for an RCCL clique")
+    shards = _shards("c2", 0.001, 2)
+    monkeypatch.setenv("TFIDF_XCHG", xchg)
+    monkeypatch.setenv("TFIDF_TEST_XFAIL_RANK", "1")
+    with tfidf_abi.Group(2, devices=[0, 1]) as g:
+        with pytest.raises(tfidf_abi.TfidfError) as ei:
+            g.run_host(shards)
+        assert ei.value.rc == -3   # TFIDF_E_HIP from rank 1; rank 0 returned TFIDF_E_PEER
+        with pytest.raises(tfidf_abi.TfidfError) as ei2:
+            g.run_host(shards)     # the clique was aborted: unusable until reopened
+        assert ei2.value.rc in (-11, -10)
