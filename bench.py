@@ -46,7 +46,7 @@ def hip_device_sync():
         raise RuntimeError("hipDeviceSynchronize failed")
 
 
-K1_SOURCES = {"k_tokcount_sl": "tokcount_sl.hip", "k_tokcount_st": "tokcount_st.hip", "k_tokcount_vs": "tokcount_vs.hip",
+K1_SOURCES = {"k_tokcount_sl": "tokcount_sl.hip", "k_tokcount_vs": "tokcount_vs.hip",
               "k_tokcount": "tokcount.hip"}
 
 
@@ -54,8 +54,6 @@ def k1_kernel(flags: int) -> str:
     """The tokenize+count kernel the last run used (tfidf_run_info.flags)."""
     if flags & tfidf_abi.RUN_K1_SL:
         return "k_tokcount_sl"
-    if flags & tfidf_abi.RUN_K1_ST:
-        return "k_tokcount_st"
     return "k_tokcount_vs" if flags & tfidf_abi.RUN_K1_VS else "k_tokcount"
 
 

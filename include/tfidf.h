@@ -38,7 +38,9 @@ enum tfidf_status {
     TFIDF_E_OUTPUT = -8,    /* output.txt cannot be written    (TFIDF.c:274-278) */
     TFIDF_E_CAPACITY = -9,  /* an internal table could not be grown, or a term (a token's bytes
                                up to its first NUL) is 16 MiB or longer: its offset/length
-                               word holds 24 length bits */
+                               word holds 24 length bits, or two distinct terms of 16 bytes or
+                               more share their 120-bit identity key (compared byte by byte on
+                               every key match: reported, never merged) */
     TFIDF_E_STATE = -10,    /* call out of order (e.g. fetch before run) */
     TFIDF_E_PEER = -11      /* another rank of the DF exchange failed (this rank did not) */
 };
@@ -196,7 +198,7 @@ typedef struct tfidf_run_info {
 } tfidf_run_info;
 #define TFIDF_RUN_K1_VS   2u  /* slot-keyed tokenize+count kernel (the default path; the general
                                  kernel of TFIDF_K1=general or an unaligned corpus leaves it clear) */
-#define TFIDF_RUN_K1_ST   4u  /* ... run as the LDS-staged persistent k_tokcount_st (TFIDF_K1=st) */
+#define TFIDF_RUN_K1_ST   4u  /* retired: round 3's k_tokcount_st (removed in round 5), never set */
 #define TFIDF_RUN_K1_SL   8u  /* ... run as k_tokcount_sl (the default, vocabulary table <= 4M slots);
                                  neither ST nor SL with VS set: k_tokcount_vs (larger tables) */
 #define TFIDF_RUN_XCHG_DENSE 16u  /* multi-rank: the DF exchange used the dense all-reduce form

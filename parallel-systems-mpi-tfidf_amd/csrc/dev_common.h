@@ -135,6 +135,10 @@ __device__ __forceinline__ void make_long_key(const uint8_t* p, uint64_t n, uint
     }
     *klo = mix64(h1 ^ (h2 << 1));
     *khi = (mix64(h2 + 0x7F4A7C15ull * h1) & 0x00FFFFFFFFFFFFFFull) | KEY_LONG_TAG;
+#ifdef TFIDF_LONG_KEY_BITS   /* test build only: a truncated tag that forces collisions (dev_vocab.h detects them) */
+    *klo &= (1ull << TFIDF_LONG_KEY_BITS) - 1ull;
+    *khi = KEY_LONG_TAG;
+#endif
 }
 
 __device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }

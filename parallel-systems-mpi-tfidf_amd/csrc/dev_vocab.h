@@ -28,9 +28,27 @@
  * wrapping) and find every key that sits in its home pair without a dependent load.  A
  * table probed by quads (HOME = ~3: four slots, one aligned 64-byte line) starts at a
  * multiple of four instead; one run uses one form throughout. */
+/* Identity of a long term (>= 16 bytes: its key is a 120-bit hash, dev_common.h) is exact:
+ * when a long key matches the incumbent, the incumbent's first occurrence (its rep: length
+ * << 40 | corpus offset, published before the key) is compared with this occurrence byte by
+ * byte, as TFIDF.c:152,172's strcmp would; two distinct terms sharing a hash are reported
+ * (ST_LONG_COLLIDE, the run fails) instead of being merged. */
+__device__ __noinline__ bool long_term_differs(const uint8_t* __restrict__ bytes, const uint64_t* reps, uint64_t h,
+                                               uint64_t rep) {
+    const uint64_t inc = atomicOr(const_cast<unsigned long long*>(reinterpret_cast<const unsigned long long*>(&reps[h])),
+                                  0ull);   /* memory side: published before the key */
+    if ((inc >> 40) != (rep >> 40)) return true;
+    const uint64_t n = rep >> 40, a = inc & 0xFFFFFFFFFFull, b = rep & 0xFFFFFFFFFFull;
+    if (a == b) return false;
+    for (uint64_t i = 0; i < n; ++i)
+        if (bytes[a + i] != bytes[b + i]) return true;
+    return false;
+}
+
 template <uint64_t HOME = ~1ull>   /* home alignment: ~1 even pairs (tokcount_sl/st), ~3 quads */
 __device__ __forceinline__ uint32_t vocab_insert_s(uint4* __restrict__ keys, uint64_t* __restrict__ reps, uint64_t mask,
-                                                uint64_t klo, uint64_t khi, uint64_t rep, uint32_t* status) {
+                                                uint64_t klo, uint64_t khi, uint64_t rep, uint32_t* status,
+                                                const uint8_t* __restrict__ bytes = nullptr) {
     uint64_t h = key_hash(klo, khi) & mask & HOME;
     uint32_t spins = 0;
     bool reread = false;
@@ -54,7 +72,7 @@ __device__ __forceinline__ uint32_t vocab_insert_s(uint4* __restrict__ keys, uin
             if (old == KEY_EMPTY_HI) {
                 atomicExch(&slot[0], (unsigned long long)klo);
                 if ((khi >> 56) == 0xFFu) {   /* once per distinct long term */
-                    reps[h] = rep;
+                    atomicExch(reinterpret_cast<unsigned long long*>(&reps[h]), (unsigned long long)rep);
                     atomicOr(status, ST_HAS_LONG);
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -71,7 +89,13 @@ __device__ __forceinline__ uint32_t vocab_insert_s(uint4* __restrict__ keys, uin
             continue;
         }
         /* a published hi carries its lo (lo is written first, both in one line) */
-        if (hi == khi && lo == klo) return (uint32_t)h;
+        if (hi == khi && lo == klo) {
+            if (bytes && (khi >> 56) == 0xFFu && long_term_differs(bytes, reps, h, rep)) {
+                atomicOr(status, ST_LONG_COLLIDE);
+                return INVALID_SLOT;
+            }
+            return (uint32_t)h;
+        }
         h = (h + 1) & mask;
         ++probe;
     }
@@ -80,8 +104,8 @@ __device__ __forceinline__ uint32_t vocab_insert_s(uint4* __restrict__ keys, uin
 }
 template <uint64_t HOME = ~1ull>
 __device__ __forceinline__ uint32_t vocab_insert(const VocabDev& v, uint64_t klo, uint64_t khi, uint64_t rep,
-                                                 uint32_t* status) {
-    return vocab_insert_s<HOME>(v.keys, v.rep, v.mask, klo, khi, rep, status);
+                                                 uint32_t* status, const uint8_t* __restrict__ bytes = nullptr) {
+    return vocab_insert_s<HOME>(v.keys, v.rep, v.mask, klo, khi, rep, status, bytes);
 }
 
 #endif

@@ -115,8 +115,8 @@ struct tfidf_ctx {
     bool timing = true;
     int k1_mode = 0;        /* 0 auto (k_tokcount_sl up to K1_ST_MAX_CAP slots, k_tokcount_vs beyond),
                                1 round-1 kernel (TFIDF_K1=vs), 2 general K1 (TFIDF_K1=general),
-                               4 the persistent k_tokcount_st (TFIDF_K1=st), 3 k_tokcount_sl
-                               (TFIDF_K1=sl) — cross-checks and A/B timing */
+                               3 k_tokcount_sl (TFIDF_K1=sl) — cross-checks and A/B timing;
+                               round 3's k_tokcount_st was retired in round 5 (git history) */
     bool stamps_on = false; /* env TFIDF_STAMPS=1 with the diagnostic library build */
     int xfail_rank = -1;    /* env TFIDF_TEST_XFAIL_RANK (tests): this rank fails inside the exchange of
                                its first run, right after the key all-gather (the abort path of
@@ -125,7 +125,6 @@ struct tfidf_ctx {
                                of its first exchange fails (the agreed path: no abort) */
     DevBuf stamps;
     bool k1_vs = false;     /* last run used the slot-keyed kernel (default) */
-    bool k1_st = false;     /* ... and of those the LDS-staged tokcount_st */
     bool k1_sl = false;     /* ... or tokcount_sl (else tokcount_vs) */
     K1Out* k1out_host = nullptr;   /* pinned: tokcount_sl's output block, copied to k1out_dev per run */
     DevBuf k1out_dev;
@@ -296,7 +295,6 @@ int tfidf_open(int device, tfidf_ctx** out) {
     const char* km = getenv("TFIDF_K1");
     if (km && !strcmp(km, "general")) ctx->k1_mode = 2;
     if (km && !strcmp(km, "vs")) ctx->k1_mode = 1;
-    if (km && !strcmp(km, "st")) ctx->k1_mode = 4;
     if (km && !strcmp(km, "sl")) ctx->k1_mode = 3;
     const char* ks = getenv("TFIDF_STAMPS");
     ctx->stamps_on = ks && ks[0] == '1';
@@ -738,9 +736,8 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     const bool aligned = (((uintptr_t)c.bytes & 15u) == 0);
     ctx->k1_vs = aligned && ctx->k1_mode != 2;
     if (ctx->k1_vs && ctx->vcap > K1_VS_MAX_CAP) return TFIDF_E_CAPACITY;
-    ctx->k1_st = ctx->k1_vs && ctx->k1_mode == 4 && ctx->vcap <= K1_ST_MAX_CAP;
     ctx->k1_sl = ctx->k1_vs && (ctx->k1_mode == 0 || ctx->k1_mode == 3) && ctx->vcap <= K1_ST_MAX_CAP;
-    const uint32_t cb = (ctx->k1_st || ctx->k1_sl) ? CHUNK_BYTES_ST : CHUNK_BYTES;
+    const uint32_t cb = ctx->k1_sl ? CHUNK_BYTES_ST : CHUNK_BYTES;
     const uint64_t nchunks = span ? (span + cb - 1) / cb : 0;
     if (ctx->rec_cap == 0) ctx->rec_cap = span / 6 + 4096;
     if (ctx->part_cap == 0) ctx->part_cap = span / 64 + 4096;
@@ -801,9 +798,7 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
         HIPCHK(hipMemcpyAsync(ctx->k1out_dev.p, ctx->k1out_host, sizeof(K1Out), hipMemcpyHostToDevice, s));
         LCHK(launch_tokcount_sl(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd,
                                 ctx->k1out_dev.as<K1Out>(), s));
-    } else if (nchunks && ctx->k1_st)
-        LCHK(launch_tokcount_st(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
-    else if (nchunks && ctx->k1_vs)
+    } else if (nchunks && ctx->k1_vs)
         LCHK(launch_tokcount_vs(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
     else if (nchunks)
         LCHK(launch_tokcount(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
@@ -829,6 +824,10 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     ctx->nchunks = nchunks;
     ctx->nrec_part = Q;
     if (st & (ST_VOCAB_SPIN | ST_TERM_LONG)) return TFIDF_E_CAPACITY;
+    if (st & ST_LONG_COLLIDE) {   /* dev_vocab.h: reported, never merged */
+        fprintf(stderr, "tfidf: two distinct terms of 16 bytes or more share their 120-bit identity key\n");
+        return TFIDF_E_CAPACITY;
+    }
     bool retry = false;
     if (st & ST_BOUNDS) {
         fprintf(stderr, "tfidf: internal bounds check tripped in K1 (status 0x%x)\n", st);
@@ -1434,7 +1433,7 @@ extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* out) {
     info->ms_tokcount = ctx->ms_stage[S_TOKCOUNT];
     for (int i = 0; i < S_NSTAGES; ++i) info->ms_stage[i] = ctx->ms_stage[i];
     info->nstages = S_NSTAGES;
-    info->flags = (ctx->k1_vs ? TFIDF_RUN_K1_VS : 0u) | (ctx->k1_st ? TFIDF_RUN_K1_ST : 0u) | (ctx->k1_sl ? TFIDF_RUN_K1_SL : 0u) |
+    info->flags = (ctx->k1_vs ? TFIDF_RUN_K1_VS : 0u) | (ctx->k1_sl ? TFIDF_RUN_K1_SL : 0u) |
                   (ctx->xp && ctx->last_dense ? TFIDF_RUN_XCHG_DENSE : 0u);
     info->device_allocs = g_dev_allocs.load(std::memory_order_relaxed);
     info->device_alloc_bytes = g_dev_alloc_bytes.load(std::memory_order_relaxed);

@@ -426,6 +426,13 @@ int rccl_init_rank(const void* unique_id, int rank, int nranks, int device, Xpor
     }
     std::vector<ncclComm_t> one{comm};
     const int rc = comms_ready(one, tmo);
+    if (rc == TFIDF_E_PEER) {
+        /* a peer never joined: the communicator is abandoned, not aborted — RCCL 2.27's
+         * ncclCommAbort joins the init thread, which waits for the absent peer forever */
+        fprintf(stderr, "tfidf: rank %d of %d: the other ranks did not join within %lld s (TFIDF_COMM_TIMEOUT_S)\n",
+                rank, nranks, (long long)(tmo / 1000));
+        return rc;
+    }
     if (rc) {
         (void)ncclCommAbort(comm);
         return rc;
@@ -506,7 +513,9 @@ int tfidf_group_open(int nranks, const int* devices, uint32_t flags, tfidf_group
             (void)hipSetDevice(cur);
             if (bad) rc = TFIDF_E_RCCL;
             else rc = comms_ready(cl->comms, cl->timeout_ms);
-            if (rc) {   /* nothing usable: abort what was created */
+            if (rc == TFIDF_E_PEER) {   /* timed out: abandoned, not aborted (rccl_init_rank) */
+                for (ncclComm_t& c : cl->comms) c = nullptr;
+            } else if (rc) {   /* nothing usable: abort what was created */
                 for (ncclComm_t& c : cl->comms)
                     if (c) { (void)ncclCommAbort(c); c = nullptr; }
             }

@@ -40,6 +40,7 @@
 #define ST_BOUNDS      16u   /* internal consistency guard tripped (a bug, reported as an error) */
 #define ST_HAS_LONG    64u   /* the vocabulary holds terms of >= 16 bytes (their order needs vocab_long_fixup) */
 #define ST_TERM_LONG   32u   /* a term of >= 16 MiB: beyond the 24-bit length of a long key's rep */
+#define ST_LONG_COLLIDE 128u /* two distinct terms of >= 16 bytes share their 120-bit key (dev_vocab.h) */
 
 /* doc flags */
 #define DF_PARTIAL     1u
@@ -94,18 +95,13 @@ int launch_plan_chunks(const CorpusDev& c, uint64_t nchunks, uint32_t chunk_byte
 int launch_tokcount(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc,
                     uint64_t c0, uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s);
 
-/* K1 main path (tokcount_st.hip, LDS-staged walk; tokcount_vs.hip: the round-1 kernel,
- * TFIDF_K1=vs): 16-byte aligned corpus base; return -3 when the vocabulary capacity
- * exceeds the LDS entry's slot field */
-int launch_tokcount_st(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc, uint64_t c0,
-                       uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s);
 /* K1 round-1 path (tokcount_vs.hip): 16-byte aligned corpus base; returns -3 when the
  * vocabulary capacity exceeds the LDS entry's slot field */
 int launch_tokcount_vs(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc, uint64_t c0,
                        uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s);
 #define K1_VS_MAX_CAP (1ull << 28)
 
-#define K1_ST_MAX_CAP (1ull << 22)   /* tokcount_st up to this vocabulary capacity, tokcount_vs beyond */
+#define K1_ST_MAX_CAP (1ull << 22)   /* tokcount_sl up to this vocabulary capacity, tokcount_vs beyond */
 /* K1 default (tokcount_sl.hip): one workgroup per chunk, straight-line rounds; the output
  * block is read from device memory (o_dev: a K1Out the engine copies there per run).
  * 16-byte aligned corpus base; -3 when the vocabulary exceeds K1_ST_MAX_CAP slots */

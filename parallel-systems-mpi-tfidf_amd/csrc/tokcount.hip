@@ -420,7 +420,7 @@ __global__ __launch_bounds__(NT, 2) void k_tokcount(CorpusDev c, const uint64_t*
                         make_long_key(c.bytes + p0, n, &klo, &khi);
                         if (n >= 0xFFFFFFull) atomicOr(o.status, ST_TERM_LONG); /* rep holds 24 length bits */
                         uint64_t rep = ((n < 0xFFFFFFull ? n : 0xFFFFFFull) << 40) | p0;
-                        uint32_t g = vocab_insert(v, klo, khi, rep, o.status);
+                        uint32_t g = vocab_insert(v, klo, khi, rep, o.status, c.bytes);
                         klo = g;
                         khi = KEY_GSLOT_TAG;
                     }

@@ -47,6 +47,14 @@
 #include "dev_vocab.h"
 #include "kernels.h"
 
+/* timing ablations (diagnostic builds only, wrong output by design): every record write of
+ * K1 is suppressed so the stages after it see an empty, consistent record set */
+#if defined(SL_ABL_NOVOCAB) || defined(SL_ABL_NOCOUNT) || defined(SL_ABL_NOROUNDS) || defined(SL_ABL_NOWRITE)
+#define SL_ABL 1
+#else
+#define SL_ABL 0
+#endif
+
 namespace {
 
 constexpr int NT = 256;                 /* threads per workgroup */
@@ -190,6 +198,7 @@ __device__ __noinline__ void overflow_record(const K1Out* o, uint32_t doc, uint3
     if (rank == 0u) b = gatomic_add(o->part_alloc, (unsigned long long)__popcll(am));
     const unsigned long long q = (((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(b >> 32)) << 32) |
                                   (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b)) + rank;
+    if (SL_ABL) return;
     if (q < o->part_cap) { gmem(o->part_doc)[q] = doc; gmem(o->part_slot)[q] = slot; gmem(o->part_cnt)[q] = 1u; }
     else atomicOr(o->status, ST_PART_FULL);
 }
@@ -249,7 +258,7 @@ __device__ __noinline__ uint32_t resolve_slow(const uint8_t* __restrict__ bytes,
     /* rep = (length << 40) | offset holds 24 length bits (TFIDF_E_CAPACITY beyond) */
     if (n >= 0xFFFFFFull) atomicOr(status, ST_TERM_LONG);
     const uint64_t rep = ((n < 0xFFFFFFull ? n : 0xFFFFFFull) << 40) | p0;
-    return vocab_insert_s(keys, reps, mask, klo, khi, rep, status);
+    return vocab_insert_s(keys, reps, mask, klo, khi, rep, status, bytes);
 }
 
 __device__ __forceinline__ void wave_agg_add(uint32_t* ctr, uint32_t idx) {
@@ -310,7 +319,7 @@ __device__ __forceinline__ void sl_flush(SlShared& S, const K1Out* o, uint32_t g
             st = complete ? 2 : 1;
             packed = complete ? cnt : (cnt << 16);
         }
-        if (st == 1 || part) gmem(o->doc_flags)[gd0 + tid] = DF_PARTIAL;
+        if ((st == 1 || part) && !SL_ABL) gmem(o->doc_flags)[gd0 + tid] = DF_PARTIAL;
         S.f.dstate[tid] = st;
     }
     uint32_t tot;
@@ -318,11 +327,11 @@ __device__ __forceinline__ void sl_flush(SlShared& S, const K1Out* o, uint32_t g
     if ((uint32_t)tid < ng) S.f.doff[tid] = off;
     const uint32_t nrec = tot & 0xFFFFu, npart = tot >> 16;
     if (tid == 0) {
-        const unsigned long long rb = nrec ? gatomic_add(o->rec_alloc, (unsigned long long)nrec) : 0ull;
+        const unsigned long long rb = (nrec && !SL_ABL) ? gatomic_add(o->rec_alloc, (unsigned long long)nrec) : 0ull;
         if (rb + nrec > o->rec_cap) atomicOr(o->status, ST_REC_FULL);
         S.rec_base = rb;
     } else if (tid == 64) {
-        const unsigned long long pb = npart ? gatomic_add(o->part_alloc, (unsigned long long)npart) : 0ull;
+        const unsigned long long pb = (npart && !SL_ABL) ? gatomic_add(o->part_alloc, (unsigned long long)npart) : 0ull;
         if (pb + npart > o->part_cap) atomicOr(o->status, ST_PART_FULL);
         S.part_base = pb;
     }
@@ -331,7 +340,7 @@ __device__ __forceinline__ void sl_flush(SlShared& S, const K1Out* o, uint32_t g
     const bool rec_ok = rb + nrec <= o->rec_cap, part_ok = pb + npart <= o->part_cap;
     if ((uint32_t)tid < ng && S.f.dstate[tid] == 2) {
         gmem(o->doc_recoff)[gd0 + tid] = rb + (off & 0xFFFFu);
-        gmem(o->doc_npairs)[gd0 + tid] = S.f.dcnt[tid];
+        gmem(o->doc_npairs)[gd0 + tid] = SL_ABL ? 0u : S.f.dcnt[tid];
     }
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
@@ -342,10 +351,10 @@ __device__ __forceinline__ void sl_flush(SlShared& S, const K1Out* o, uint32_t g
             const uint32_t dof = S.f.doff[rel];
             if (S.f.dstate[rel] == 2) {
                 const uint64_t q = rb + (dof & 0xFFFFu) + k;
-                if (rec_ok) { gmem(rec_slot)[q] = key & smask; gmem(rec_cnt)[q] = ec[j]; }
+                if (rec_ok && !SL_ABL) { gmem(rec_slot)[q] = key & smask; gmem(rec_cnt)[q] = ec[j]; }
             } else {
                 const uint64_t q = pb + (dof >> 16) + k;
-                if (part_ok) { gmem(part_doc)[q] = gd0 + rel; gmem(part_slot)[q] = key & smask; gmem(part_cnt)[q] = ec[j]; }
+                if (part_ok && !SL_ABL) { gmem(part_doc)[q] = gd0 + rel; gmem(part_slot)[q] = key & smask; gmem(part_cnt)[q] = ec[j]; }
             }
             S.TK[j * NT + tid] = 0u;
             S.TC[j * NT + tid] = 0u;
@@ -428,15 +437,15 @@ __device__ __forceinline__ void sl_flush_few(SlShared& S, const K1Out* o, uint32
                 st = complete ? 2 : 1;
                 packed = complete ? cnt : (cnt << 16);
             }
-            if (st == 1 || part) gmem(o->doc_flags)[gd0 + d] = DF_PARTIAL;
+            if ((st == 1 || part) && !SL_ABL) gmem(o->doc_flags)[gd0 + d] = DF_PARTIAL;
         }
         const uint32_t incl = wave_incl_scan(packed);
         const uint32_t all = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         const uint32_t off = incl - packed;
         const uint32_t nrec = all & 0xFFFFu, npart = all >> 16;
         unsigned long long a0 = 0, a1 = 0;
-        if (lane == 0 && nrec) a0 = gatomic_add(o->rec_alloc, (unsigned long long)nrec);
-        if (lane == 32 && npart) a1 = gatomic_add(o->part_alloc, (unsigned long long)npart);
+        if (lane == 0 && nrec && !SL_ABL) a0 = gatomic_add(o->rec_alloc, (unsigned long long)nrec);
+        if (lane == 32 && npart && !SL_ABL) a1 = gatomic_add(o->part_alloc, (unsigned long long)npart);
         const unsigned long long rb = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(a0 >> 32), 0) << 32) |
                                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a0, 0);
         const unsigned long long pb = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(a1 >> 32), 32) << 32) |
@@ -449,7 +458,7 @@ __device__ __forceinline__ void sl_flush_few(SlShared& S, const K1Out* o, uint32
             if (st == 2) {
                 fb = rec_ok ? rb + (off & 0xFFFFu) : ~0ull;
                 gmem(o->doc_recoff)[gd0 + d] = rb + (off & 0xFFFFu);
-                gmem(o->doc_npairs)[gd0 + d] = cnt;
+                gmem(o->doc_npairs)[gd0 + d] = SL_ABL ? 0u : cnt;
             } else if (st == 1) {
                 fb = part_ok ? pb + (off >> 16) : ~0ull;
             }
@@ -472,7 +481,7 @@ __device__ __forceinline__ void sl_flush_few(SlShared& S, const K1Out* o, uint32
                     rank[q] += 1u << (16 * (rel & 1u));
                 }
             const uint64_t fb = S.fbase[rel];
-            if (fb != ~0ull) {
+            if (fb != ~0ull && !SL_ABL) {
                 const uint64_t qq = fb + r;
                 if (S.f.dstate[rel] == 2) { gmem(rec_slot)[qq] = key & smask; gmem(rec_cnt)[qq] = ec[j]; }
                 else { gmem(part_doc)[qq] = gd0 + rel; gmem(part_slot)[qq] = key & smask; gmem(part_cnt)[qq] = ec[j]; }
@@ -630,8 +639,13 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
 #ifdef SL_DEBUG
             p.ent = a.ent;
 #endif
+#ifdef SL_ABL_NOVOCAB   /* timing ablation (wrong output): no vocabulary loads, slot = home */
+            p.s0 = make_uint4(p.k0, p.k1, p.k2, p.k3);
+            p.s1 = p.s0;
+#else
             p.s0 = bload16<0>(vrs, (int32_t)(p.h << 4));
             p.s1 = bload16<0>(vrs, (int32_t)(p.h << 4) + 16);
+#endif
         };
         auto finish = [&](const Round& r) {
 #ifdef SL_STAMPS
@@ -644,7 +658,11 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
             const bool h0 = ((r.s0.x ^ r.k0) | (r.s0.y ^ r.k1) | (r.s0.z ^ r.k2) | (r.s0.w ^ r.k3)) == 0u;
             const bool h1 = ((r.s1.x ^ r.k0) | (r.s1.y ^ r.k1) | (r.s1.z ^ r.k2) | (r.s1.w ^ r.k3)) == 0u;
             uint32_t slot = r.h + (h0 ? 0u : 1u);
+#ifdef SL_ABL_NOVOCAB
+            const bool need = false;
+#else
             const bool need = (r.kind == 2u) | ((r.kind == 1u) & !(h0 | h1));
+#endif
             if (__ballot(need) != 0ull) {
                 if (need) {
                     const uint64_t p0 = b0 + (uint64_t)(int64_t)r.ap;
@@ -665,6 +683,10 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
                     d[3] = ((unsigned long long)key << 32) | slot;
                 }
             }
+#endif
+#ifdef SL_ABL_NOCOUNT   /* timing ablation (wrong output): no LDS count */
+            wclaims += (uint32_t)__popcll(__ballot(key == 0x12345u));
+            return;
 #endif
             /* The LDS count, straight-line: ONE bucket read (two ds_read_b128), then one CAS
              * and one add per lane whatever the case — a match CASes its own key over itself,
@@ -811,6 +833,10 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
                 SL_STAMP(1);
                 if (ntok == 0) continue;
                 tokens_w += ntok;
+#ifdef SL_ABL_NOROUNDS   /* timing ablation (wrong output): tokenize only */
+                if (!multi && lane == 0) atomicAdd(&S.dsz[wr], ntok);
+                continue;
+#endif
                 if (!multi && lane == 0) atomicAdd(&S.dsz[wr], ntok);   /* the whole step is in document wr */
                 for (uint32_t tb = 0; tb < ntok; tb += TLW) {
                     {

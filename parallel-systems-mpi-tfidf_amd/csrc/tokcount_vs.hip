@@ -158,7 +158,7 @@ __device__ __forceinline__ uint32_t slow_slot(const uint8_t* __restrict__ bytes,
      * emitted truncated, so the run fails with TFIDF_E_CAPACITY instead */
     if (n >= 0xFFFFFFull) atomicOr(status, ST_TERM_LONG);
     const uint64_t rep = ((n < 0xFFFFFFull ? n : 0xFFFFFFull) << 40) | p0;
-    return vocab_insert<VS_HOME>(v, klo, khi, rep, status);
+    return vocab_insert<VS_HOME>(v, klo, khi, rep, status, bytes);
 }
 
 /* A (document, term) pair met after the table reached FILL_LIMIT and not in it: one

@@ -20,7 +20,7 @@ import statistics
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SOURCES = {"k_tokcount_sl": "tokcount_sl.hip", "k_tokcount_st": "tokcount_st.hip", "k_tokcount_vs": "tokcount_vs.hip", "k_tokcount": "tokcount.hip"}
+SOURCES = {"k_tokcount_sl": "tokcount_sl.hip", "k_tokcount_vs": "tokcount_vs.hip", "k_tokcount": "tokcount.hip"}
 
 
 def k1_source_sha(kernel) -> str:
@@ -29,8 +29,8 @@ def k1_source_sha(kernel) -> str:
 
 
 def kernel_of(name):
-    """k_tokcount_st / k_tokcount_vs / k_tokcount from a demangled kernel name"""
-    for k in ("k_tokcount_sl", "k_tokcount_st", "k_tokcount_vs"):
+    """k_tokcount_sl / k_tokcount_vs / k_tokcount from a demangled kernel name"""
+    for k in ("k_tokcount_sl", "k_tokcount_vs"):
         if k in name:
             return k
     return "k_tokcount" if "k_tokcount(" in name else None
@@ -58,7 +58,7 @@ def main():
     prof_dir, key, table, copies = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4:]
     fetch, kern = per_launch(prof_dir, "FETCH_SIZE")
     write, _ = per_launch(prof_dir, "WRITE_SIZE")
-    kern = kern or "k_tokcount_st"
+    kern = kern or "k_tokcount_sl"
     e = {"kernel": kern, "k1_source_sha": k1_source_sha(kern), "fetch_size_kb": fetch, "write_size_kb": write,
          "hbm_bytes_per_launch": None, "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes ({key})",
          "formula": "2*FETCH_SIZE + WRITE_SIZE (KB*1024); x2 on reads per MI355X_MICROARCH.md §HBM "

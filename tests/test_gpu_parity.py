@@ -84,7 +84,7 @@ def test_long_tokens_and_shared_prefixes(engine):
 
 def test_tokens_across_windows_and_chunks(engine):
     # one big document (> BIG_DOC, split across chunks) whose tokens straddle the 4 KiB
-    # windows and chunk boundaries (24 KiB for tokcount_st, 16 KiB for the other K1
+    # windows and chunk boundaries (24 KiB for tokcount_sl, 12 KiB for the other K1
     # kernels) at every offset
     rng = np.random.default_rng(3)
     parts = []
@@ -235,12 +235,12 @@ def test_full_config_properties(cfg):
 @pytest.mark.parametrize("cfg,scale", [("c2", 0.002), ("c5", 0.0005), ("c4", 0.001)])
 def test_k1_variants_agree(cfg, scale):
     """The default K1 (k_tokcount_sl up to 4M vocabulary slots, k_tokcount_vs beyond), the
-    persistent LDS-staged K1 (TFIDF_K1=st), the round-1 slot-keyed K1 (TFIDF_K1=vs) and the
-    general K1 (unaligned corpora) give identical results, equal to the oracle."""
+    round-1 slot-keyed K1 (TFIDF_K1=vs) and the general K1 (unaligned corpora) give identical
+    results, equal to the oracle."""
     p = tfidf_configs.plan(cfg, scale=scale)
     data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
     outs = []
-    modes = [("auto", 2), ("sl", 2), ("st", 2), ("vs", 2), ("general", 0)]
+    modes = [("auto", 2), ("sl", 2), ("vs", 2), ("general", 0)]
     for mode, flag in modes:
         os.environ["TFIDF_K1"] = mode
         try:
@@ -250,8 +250,6 @@ def test_k1_variants_agree(cfg, scale):
                 assert (f & 3) == flag
                 if mode in ("auto", "sl") and cfg != "c4":
                     assert f & tfidf_abi.RUN_K1_SL
-                if mode == "st" and cfg != "c4":
-                    assert f & tfidf_abi.RUN_K1_ST
                 outs.append(e.fetch())
         finally:
             os.environ.pop("TFIDF_K1", None)
@@ -491,3 +489,62 @@ def test_term_of_16_mib_is_a_capacity_error(engine):
     g = load_golden("g1_whitespace")
     engine.run_host(g["data"], g["off"])
     assert engine.fetch()["output_txt"] == g["output"]
+
+
+def _long_term_corpus(nterms, ndocs, seed):
+    """documents of distinct terms of 18-30 bytes (long keys: 120-bit hashes), each term in
+    several documents, with a few short words between them"""
+    rng = np.random.default_rng(seed)
+    terms = sorted({bytes(rng.integers(97, 123, int(rng.integers(18, 31)), dtype=np.uint8)) for _ in range(nterms)})
+    docs = []
+    for d in range(ndocs):
+        pick = rng.choice(len(terms), size=min(len(terms), 40))
+        docs.append(b" ".join(terms[j] + b" w%d" % (j % 7) for j in pick) + b"\n")
+    return docs_to_arrays(docs)
+
+
+_LONGTAG_CHILD = r"""
+import sys
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2]); sys.path.insert(0, sys.argv[3])
+import numpy as np, tfidf_abi, test_gpu_parity as t, oracle_py
+from helpers import assert_same_result
+with tfidf_abi.Engine(0) as e:
+    # few distinct long terms: no 16-bit collision among them, each repeated in many
+    # documents at different offsets -> the byte verification must accept every match
+    data, off = t._long_term_corpus(4, 300, 5)
+    e.run_host(data, off)
+    ora = oracle_py.run(data, off)
+    assert_same_result(e.fetch(), ora)
+    print("RESULT few ok")
+    # thousands of distinct long terms: ~70 pairs share a 16-bit key
+    data, off = t._long_term_corpus(3000, 400, 6)
+    try:
+        e.run_host(data, off)
+        print("RESULT many merged")
+    except tfidf_abi.TfidfError as ex:
+        print("RESULT many rc=%d" % ex.rc)
+"""
+
+
+def test_long_term_hash_collisions_are_reported():
+    """Identity of terms of >= 16 bytes is exact (dev_vocab.h): their 120-bit key only picks the
+    vocabulary slot; every match is verified byte by byte against the incumbent's first
+    occurrence, as TFIDF.c:152,172's strcmp would.  The test library lib/libtfidf_hip_longtag16.so
+    truncates the key to 16 bits so distinct long terms DO collide: a corpus of a few long terms
+    (no collision) still matches the oracle exactly, and one of 3000 long terms fails with
+    TFIDF_E_CAPACITY instead of merging counts.  The product library runs the 3000-term corpus
+    against the oracle."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    pydir = os.path.join(os.path.dirname(here), "parallel-systems-mpi-tfidf_amd", "python")
+    env = dict(os.environ, TFIDF_LIB="longtag16")
+    import sys
+    r = subprocess.run([sys.executable, "-c", _LONGTAG_CHILD, pydir, here, os.path.join(os.path.dirname(here), "oracle")],
+                       env=env,
+                       capture_output=True, text=True, timeout=240, cwd=here)
+    out = [l for l in r.stdout.splitlines() if l.startswith("RESULT")]
+    assert out == ["RESULT few ok", "RESULT many rc=-9"], r.stdout + r.stderr[-3000:]
+    assert "share their 120-bit identity key" in r.stderr
+
+
+def test_many_distinct_long_terms_vs_oracle(engine):
+    check_vs_oracle(engine, *_long_term_corpus(3000, 400, 6))
