@@ -403,6 +403,9 @@ def main():
     ap.add_argument("--plan-only", action="store_true",
                     help="print what would be measured (shards per rank, and the c3 strong follow-up of a "
                          "multi-GPU c2 run) as JSON and exit, without touching a GPU")
+    ap.add_argument("--shard-of", default="",
+                    help="R/N: diagnostics only (K1 PMC traffic of a multi-GPU plan, scripts/r05_final.sh): run rank R's "
+                         "shard of the N-GPU plan alone on one GPU, no exchange (idf over the global N)")
     ap.add_argument("--no-c3", action="store_true",
                     help="--gpus N >= 2: skip the c3 strong (BASELINE config 3) measurement after the c2 line")
     ap.add_argument("--shards", type=int, default=0,
@@ -444,8 +447,13 @@ def main():
         dist.broadcast(uid, 0)
         eng.comm_init(bytes(uid.numpy().tobytes()), rank, world)
 
-    p = tfidf_configs.plan(args.config, scale=args.scale, rank=rank, nranks=world, weak=not args.strong,
-                           vocab=args.vocab)
+    if args.shard_of and world == 1:
+        sr, sn = (int(x) for x in args.shard_of.split("/"))
+        p = tfidf_configs.plan(args.config, scale=args.scale, rank=sr, nranks=sn, weak=not args.strong,
+                               vocab=args.vocab)
+    else:
+        p = tfidf_configs.plan(args.config, scale=args.scale, rank=rank, nranks=world, weak=not args.strong,
+                               vocab=args.vocab)
     corpus = eng.synth_device(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"], p["ndocs_total"])
     eng.set_timing(True)
 

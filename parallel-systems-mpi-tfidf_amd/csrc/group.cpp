@@ -420,12 +420,17 @@ int rccl_init_rank(const void* unique_id, int rank, int nranks, int device, Xpor
     ncclComm_t comm = nullptr;
     if (hipSetDevice(device) != hipSuccess) return TFIDF_E_HIP;
     const int64_t tmo = comm_timeout_ms_from_env();
-    if (nccl_issue(ncclCommInitRankConfig(&comm, nranks, u, rank, &cfg)) < 0 || !comm) {
+    const bool dbg = getenv("TFIDF_DEBUG_COMM") != nullptr;
+    if (dbg) fprintf(stderr, "tfidf: rccl_init_rank %d/%d: ncclCommInitRankConfig...\n", rank, nranks);
+    const ncclResult_t ir = ncclCommInitRankConfig(&comm, nranks, u, rank, &cfg);
+    if (dbg) fprintf(stderr, "tfidf: rccl_init_rank: returned %d, comm %p; polling (timeout %lld ms)\n", (int)ir, (void*)comm, (long long)tmo);
+    if (nccl_issue(ir) < 0 || !comm) {
         if (comm) (void)ncclCommAbort(comm);
         return TFIDF_E_RCCL;
     }
     std::vector<ncclComm_t> one{comm};
     const int rc = comms_ready(one, tmo);
+    if (dbg) fprintf(stderr, "tfidf: rccl_init_rank: polled, rc %d\n", rc);
     if (rc == TFIDF_E_PEER) {
         /* a peer never joined: the communicator is abandoned, not aborted — RCCL 2.27's
          * ncclCommAbort joins the init thread, which waits for the absent peer forever */

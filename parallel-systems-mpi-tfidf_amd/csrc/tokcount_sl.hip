@@ -57,7 +57,10 @@
 
 namespace {
 
-constexpr int NT = 256;                 /* threads per workgroup */
+#ifndef SL_NT
+#define SL_NT 256
+#endif
+constexpr int NT = SL_NT;               /* threads per workgroup (SL_NT=320: five waves, A/B) */
 constexpr int NWAVE = NT / 64;
 #ifndef SL_WGCU
 #define SL_WGCU 4
@@ -101,7 +104,8 @@ struct SlShared {
         } f;
     };
     uint4 sel[16];                      /* v_perm selectors of a term of length n */
-    uint64_t fbase[8];
+    uint32_t lbase[8];                  /* few-document flush: a document's first staging index */
+    uint32_t fl_nrec, fl_npart;         /* flush: records and partial records of the group */
     uint8_t dpart[GCAP];                /* document has overflow records */
     uint8_t dfull[GCAP];                /* document lies wholly inside the chunk */
     uint32_t wsum[NWAVE];
@@ -180,14 +184,27 @@ __device__ __forceinline__ uint32_t bkt_match(const BktK& kk, uint32_t key) {
     if (j == 8u) j = kk.b.x == key ? 4u : kk.b.y == key ? 5u : kk.b.z == key ? 6u : kk.b.w == key ? 7u : 8u;
     return j;
 }
-/* Buckets fill from slot 0 up and are never emptied during a group (a claim always takes
- * the first empty slot, a lost claim re-reads the bucket), so a bucket is hole-free: slots
- * [0, n) hold keys, [n, 8) are empty.  Occupancy n from the keys' top bits (every key has
- * bit 31 set): the top bytes of four slots gathered by two v_perm, their bit 7 counted. */
-__device__ __forceinline__ uint32_t bkt_fill(const BktK& kk) {
+/* A claim starts at a slot derived from the key and takes the first empty slot from there
+ * on, cyclically in the bucket, so different keys of one round rarely aim at the same slot
+ * (round 4's claims all took the bucket's first empty slot: 1.52 lost claims per round, 70 %
+ * of rounds retried; this form: c2 K1 1.72 -> 1.65 ms, profiles/r05_k1_ab_c2.txt).  Every claimer
+ * of a key walks the same cyclic order from the same start and slots are never emptied
+ * during a group, so a key is never claimed twice: a walker meets the key's slot (its CAS
+ * returns the key) before any slot that was empty when the key was placed.  Occupancy from
+ * the keys' top bits (every key has bit 31 set): the top bytes of four slots gathered by two
+ * v_perm, their bit 7 moved to one bit each by a multiply. */
+__device__ __forceinline__ uint32_t bkt_occ(const BktK& kk) {   /* bit i: slot i holds a key */
     const uint32_t ta = __builtin_amdgcn_perm(kk.a.y, kk.a.x, 0x0C0C0703u) | __builtin_amdgcn_perm(kk.a.w, kk.a.z, 0x07030C0Cu);
     const uint32_t tb = __builtin_amdgcn_perm(kk.b.y, kk.b.x, 0x0C0C0703u) | __builtin_amdgcn_perm(kk.b.w, kk.b.z, 0x07030C0Cu);
-    return (uint32_t)__popc(ta & 0x80808080u) + (uint32_t)__popc(tb & 0x80808080u);
+    /* bits 7, 15, 23, 31 -> bits 28..31 (no carries: the partial products do not overlap) */
+    return (((ta & 0x80808080u) * 0x00204081u) >> 28) | ((((tb & 0x80808080u) * 0x00204081u) >> 28) << 4);
+}
+__device__ __forceinline__ uint32_t bkt_pref(uint32_t key) { return (key * 0x85EBCA77u) >> 29; }
+/* the first slot at or after p (cyclically) that `occ` marks empty; BW when none */
+__device__ __forceinline__ uint32_t bkt_pick(uint32_t occ, uint32_t p) {
+    const uint32_t e = ~occ & 0xFFu;
+    const uint32_t r = ((e | (e << 8)) >> p) & 0xFFu;
+    return r ? ((p + (uint32_t)__builtin_ctz(r)) & (BW - 1u)) : BW;
 }
 
 /* one partial record of count 1 (overflow mode / no room): one device atomic per wave */
@@ -213,7 +230,7 @@ __device__ __noinline__ uint32_t bkt_slow(uint32_t* TK, uint32_t* TC, uint8_t* d
         const BktK kk = bkt_read(TK, b);
         const uint32_t j = bkt_match(kk, key);
         if (j < BW) { atomicAdd(&TC[bkt_slot(b, j)], 1u); return 0u; }
-        const uint32_t e = bkt_fill(kk);   /* the first empty slot (hole-free bucket) */
+        const uint32_t e = bkt_pick(bkt_occ(kk), bkt_pref(key));   /* the key's first empty slot */
         if (e < BW) {
             if (over) break;
             const uint32_t old = atomicCAS(&TK[bkt_slot(b, e)], 0u, key);
@@ -286,21 +303,50 @@ __device__ __forceinline__ uint32_t wave_agg_add_rtn(uint32_t* ctr, uint32_t idx
     return k;
 }
 
+/* The flush's second half: every entry has been placed in the staging area (the table's own
+ * TK/TC words: records [0, nrec), partial records [nrec, nrec + npart), key and count), so the
+ * group's records leave as ONE contiguous run from rb and its partial records as one from pb
+ * — consecutive lanes store consecutive words (round 4 stored each entry at its document's
+ * base + rank from the lane that held it: scattered partial lines, 0.33 ms of c2's K1 for
+ * 0.5 GB, profiles/r05_k1_ablations_c2.txt).  Then the whole table is cleared. */
+__device__ __forceinline__ void sl_write_staged(SlShared& S, const K1Out* o, uint32_t gd0, uint32_t sb, uint32_t nrec,
+                                                uint32_t npart, unsigned long long rb, unsigned long long pb,
+                                                bool rec_ok, bool part_ok) {
+    const int tid = threadIdx.x;
+    uint32_t* const rec_slot = o->rec_slot;   /* read once (see sl_flush_few) */
+    uint32_t* const rec_cnt = o->rec_cnt;
+    uint32_t* const part_doc = o->part_doc;
+    uint32_t* const part_slot = o->part_slot;
+    uint32_t* const part_cnt = o->part_cnt;
+    const uint32_t smask = (1u << sb) - 1u;
+    lds_barrier();
+    if (rec_ok && !SL_ABL)
+        for (uint32_t i = (uint32_t)tid; i < nrec; i += NT) {
+            gmem(rec_slot)[rb + i] = S.TK[i] & smask;
+            gmem(rec_cnt)[rb + i] = S.TC[i];
+        }
+    if (part_ok && !SL_ABL)
+        for (uint32_t i = (uint32_t)tid; i < npart; i += NT) {
+            const uint32_t k = S.TK[nrec + i];
+            gmem(part_doc)[pb + i] = gd0 + ((k & 0x7FFFFFFFu) >> sb);
+            gmem(part_slot)[pb + i] = k & smask;
+            gmem(part_cnt)[pb + i] = S.TC[nrec + i];
+        }
+    lds_barrier();
+    uint4* t = reinterpret_cast<uint4*>(S.TK);
+#pragma unroll
+    for (int j = tid; j < 2 * TB / 4; j += NT) t[j] = make_uint4(0, 0, 0, 0);   /* TK and TC are adjacent */
+}
+
 /* Emits the group's table entries as records (complete documents: the record stream;
  * documents crossing the chunk, over K5's in-LDS sort size or with overflow records: the
  * partial stream) — any number of documents: per-document counts by wave-aggregated LDS
  * adds, a block scan, every entry written at its document's base + its rank. */
 __device__ __forceinline__ void sl_flush(SlShared& S, const K1Out* o, uint32_t gd0, uint32_t ng, uint32_t sb) {
     const int tid = threadIdx.x;
-    uint32_t* const rec_slot = o->rec_slot;   /* read once: see sl_flush_few */
-    uint32_t* const rec_cnt = o->rec_cnt;
-    uint32_t* const part_doc = o->part_doc;
-    uint32_t* const part_slot = o->part_slot;
-    uint32_t* const part_cnt = o->part_cnt;
     lds_barrier();
     if (tid < GCAP) { S.f.dcnt[tid] = 0; S.f.drun[tid] = 0; }
     lds_barrier();
-    const uint32_t smask = (1u << sb) - 1u;
     uint32_t ek[EPT], ec[EPT];
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
@@ -342,6 +388,9 @@ __device__ __forceinline__ void sl_flush(SlShared& S, const K1Out* o, uint32_t g
         gmem(o->doc_recoff)[gd0 + tid] = rb + (off & 0xFFFFu);
         gmem(o->doc_npairs)[gd0 + tid] = SL_ABL ? 0u : S.f.dcnt[tid];
     }
+    /* every entry to its staging index: its document's base in the record or partial run
+     * + its rank among the document's entries (all entries are in registers: the table's
+     * words are free) */
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
         const uint32_t key = ek[j];
@@ -349,17 +398,12 @@ __device__ __forceinline__ void sl_flush(SlShared& S, const K1Out* o, uint32_t g
             const uint32_t rel = (key & 0x7FFFFFFFu) >> sb;
             const uint32_t k = wave_agg_add_rtn(&S.f.drun[0], rel);
             const uint32_t dof = S.f.doff[rel];
-            if (S.f.dstate[rel] == 2) {
-                const uint64_t q = rb + (dof & 0xFFFFu) + k;
-                if (rec_ok && !SL_ABL) { gmem(rec_slot)[q] = key & smask; gmem(rec_cnt)[q] = ec[j]; }
-            } else {
-                const uint64_t q = pb + (dof >> 16) + k;
-                if (part_ok && !SL_ABL) { gmem(part_doc)[q] = gd0 + rel; gmem(part_slot)[q] = key & smask; gmem(part_cnt)[q] = ec[j]; }
-            }
-            S.TK[j * NT + tid] = 0u;
-            S.TC[j * NT + tid] = 0u;
+            const uint32_t loc = (S.f.dstate[rel] == 2 ? (dof & 0xFFFFu) : nrec + (dof >> 16)) + k;
+            S.TK[loc] = key;
+            S.TC[loc] = ec[j];
         }
     }
+    sl_write_staged(S, o, gd0, sb, nrec, npart, rb, pb, rec_ok, part_ok);
 }
 
 /* The flush of a group of at most FEW documents (most chunks hold one or two): per-thread
@@ -380,16 +424,7 @@ constexpr uint32_t FEW = 8;
 __device__ __forceinline__ void sl_flush_few(SlShared& S, const K1Out* o, uint32_t gd0, uint32_t ng, uint32_t sb SLF_ARGS) {
     const int tid = threadIdx.x;
     const int lane = tid & 63, w = tid >> 6;
-    /* the output arrays' addresses read once (scalar loads): read at the stores, the
-     * per-lane choice between the two streams made the compiler load them per entry with
-     * vector loads and wait for each */
-    uint32_t* const rec_slot = o->rec_slot;
-    uint32_t* const rec_cnt = o->rec_cnt;
-    uint32_t* const part_doc = o->part_doc;
-    uint32_t* const part_slot = o->part_slot;
-    uint32_t* const part_cnt = o->part_cnt;
     lds_barrier();
-    const uint32_t smask = (1u << sb) - 1u;
     uint32_t ek[EPT], ec[EPT];
     uint32_t pk[FEW / 2] = {0, 0, 0, 0};
 #pragma unroll
@@ -454,20 +489,22 @@ __device__ __forceinline__ void sl_flush_few(SlShared& S, const K1Out* o, uint32
         if (lane == 0 && !rec_ok) atomicOr(o->status, ST_REC_FULL);
         if (lane == 0 && !part_ok) atomicOr(o->status, ST_PART_FULL);
         if (d < ng) {
-            uint64_t fb = ~0ull;
             if (st == 2) {
-                fb = rec_ok ? rb + (off & 0xFFFFu) : ~0ull;
                 gmem(o->doc_recoff)[gd0 + d] = rb + (off & 0xFFFFu);
                 gmem(o->doc_npairs)[gd0 + d] = SL_ABL ? 0u : cnt;
-            } else if (st == 1) {
-                fb = part_ok ? pb + (off >> 16) : ~0ull;
             }
-            S.fbase[d] = fb;
-            S.f.dstate[d] = st;
+            S.lbase[d] = st == 2 ? (off & 0xFFFFu) : nrec + (off >> 16);   /* staging index */
+        }
+        if (lane == 0) {
+            S.fl_nrec = nrec;
+            S.fl_npart = npart;
+            S.rec_base = rec_ok ? rb : ~0ull;
+            S.part_base = part_ok ? pb : ~0ull;
         }
     }
     lds_barrier();
     SLF_STAMP(10);
+    /* every entry to its staging index (sl_write_staged): its document's base + its rank */
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
         const uint32_t key = ek[j];
@@ -480,16 +517,13 @@ __device__ __forceinline__ void sl_flush_few(SlShared& S, const K1Out* o, uint32
                     r = (rank[q] >> (16 * (rel & 1u))) & 0xFFFFu;
                     rank[q] += 1u << (16 * (rel & 1u));
                 }
-            const uint64_t fb = S.fbase[rel];
-            if (fb != ~0ull && !SL_ABL) {
-                const uint64_t qq = fb + r;
-                if (S.f.dstate[rel] == 2) { gmem(rec_slot)[qq] = key & smask; gmem(rec_cnt)[qq] = ec[j]; }
-                else { gmem(part_doc)[qq] = gd0 + rel; gmem(part_slot)[qq] = key & smask; gmem(part_cnt)[qq] = ec[j]; }
-            }
-            S.TK[j * NT + tid] = 0u;
-            S.TC[j * NT + tid] = 0u;
+            const uint32_t loc = S.lbase[rel] + r;
+            S.TK[loc] = key;
+            S.TC[loc] = ec[j];
         }
     }
+    const unsigned long long rb = S.rec_base, pb = S.part_base;
+    sl_write_staged(S, o, gd0, sb, S.fl_nrec, S.fl_npart, rb, pb, rb != ~0ull, pb != ~0ull);
 }
 
 __device__ __forceinline__ uint32_t perm_sel(uint32_t n, uint32_t k) {
@@ -516,7 +550,7 @@ struct Round {
 
 }  // namespace
 
-__global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, const uint64_t* __restrict__ chunk_start,
+__global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_tokcount_sl(CorpusDev c, const uint64_t* __restrict__ chunk_start,
                                                                const uint32_t* __restrict__ chunk_doc, uint64_t c0,
                                                                uint64_t c1, VocabDev v, const K1Out* __restrict__ o,
                                                                uint32_t sb, uint32_t gcap) {
@@ -702,7 +736,9 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
             const uint32_t j = (m1 ? 1u : 0u) | (m2 ? 2u : 0u) | (m3 ? 3u : 0u) | (m4 ? 4u : 0u) | (m5 ? 5u : 0u) |
                                (m6 ? 6u : 0u) | (m7 ? 7u : 0u);
             const bool found = m0 | m1 | m2 | m3 | m4 | m5 | m6 | m7;
-            const uint32_t n = bkt_fill(kk);
+            const uint32_t pref = bkt_pref(key);
+            uint32_t occ = bkt_occ(kk);
+            const uint32_t n = bkt_pick(occ, pref);   /* the key's first empty slot (BW: full) */
             const bool hit = key != 0u && found;
             const bool claim = key != 0u && !found && n < BW && !over;
             const uint32_t idx = bkt_slot(b, found ? j : (n & (BW - 1u)));
@@ -718,17 +754,20 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
             st_cnt[2] += (uint32_t)__popcll(__ballot(claim && !ok));
             ++st_cnt[4];
 #endif
-            /* claims lost to other lanes of this round (every lane read the bucket before any
-             * claimed, so the k-th winner took slot n + k - 1): inline claims of slots n + 1,
-             * then n + 2, without re-reading the bucket (a lost CAS returns the slot's key:
-             * the same key counts there) */
+            /* claims lost to other lanes (of this round: every lane read the bucket before any
+             * claimed): inline claims of the key's next empty slots of the snapshot, without
+             * re-reading the bucket (a lost CAS returns the slot's key: the same key counts
+             * there) */
             uint32_t nn = n;
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
-                const bool lost = claim && slow && nn + 1u < BW;
+                if (claim && slow) {
+                    occ |= 1u << (nn & (BW - 1u));
+                    nn = bkt_pick(occ, pref);
+                }
+                const bool lost = claim && slow && nn < BW;
                 if (__ballot(lost) == 0ull) break;
                 if (lost) {
-                    ++nn;
                     const uint32_t i2 = bkt_slot(b, nn);
                     const uint32_t o2 = atomicCAS(&S.TK[i2], 0u, key);
                     if (o2 == 0u || o2 == key) {
@@ -750,7 +789,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU) void k_tokcount_sl(CorpusDev c, cons
                         uint32_t e2 = j2;
                         bool ok2 = j2 < BW;
                         if (!ok2) {
-                            e2 = bkt_fill(k2);
+                            e2 = bkt_pick(bkt_occ(k2), pref);
                             if (e2 < BW) {
                                 const uint32_t o2 = atomicCAS(&S.TK[bkt_slot(b2, e2)], 0u, key);
                                 ok2 = o2 == 0u || o2 == key;
