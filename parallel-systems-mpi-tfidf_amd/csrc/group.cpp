@@ -409,41 +409,59 @@ struct LocalXport final : Xport {
 
 }  // namespace
 
-/* one rank of a process-per-GPU job (tfidf_comm_init): a non-blocking ncclCommInitRankConfig,
- * polled until every rank joined (or the deadline: TFIDF_E_PEER) */
+/* one rank of a process-per-GPU job (tfidf_comm_init).  RCCL 2.27's ncclCommInitRankConfig
+ * blocks its caller in the bootstrap until every rank has joined, even for a non-blocking
+ * communicator (measured on the GPU box: a 2-rank init whose peer never starts did not
+ * return within 40 s).  So the init runs on a helper thread and this call waits for it at
+ * most TFIDF_COMM_TIMEOUT_S: a peer that never joins gives TFIDF_E_PEER instead of a hang.
+ * The helper then stays blocked in RCCL's bootstrap (it cannot be interrupted); if the peers
+ * ever do join, it aborts the communicator nobody will use. */
+struct InitJob {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false, abandoned = false;
+    int rc = TFIDF_OK;
+    ncclComm_t comm = nullptr;
+};
 int rccl_init_rank(const void* unique_id, int rank, int nranks, int device, Xport** out) {
     *out = nullptr;
     ncclUniqueId u;
     memcpy(&u, unique_id, sizeof(u));
-    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-    cfg.blocking = 0;
-    ncclComm_t comm = nullptr;
-    if (hipSetDevice(device) != hipSuccess) return TFIDF_E_HIP;
     const int64_t tmo = comm_timeout_ms_from_env();
-    const bool dbg = getenv("TFIDF_DEBUG_COMM") != nullptr;
-    if (dbg) fprintf(stderr, "tfidf: rccl_init_rank %d/%d: ncclCommInitRankConfig...\n", rank, nranks);
-    const ncclResult_t ir = ncclCommInitRankConfig(&comm, nranks, u, rank, &cfg);
-    if (dbg) fprintf(stderr, "tfidf: rccl_init_rank: returned %d, comm %p; polling (timeout %lld ms)\n", (int)ir, (void*)comm, (long long)tmo);
-    if (nccl_issue(ir) < 0 || !comm) {
-        if (comm) (void)ncclCommAbort(comm);
-        return TFIDF_E_RCCL;
-    }
-    std::vector<ncclComm_t> one{comm};
-    const int rc = comms_ready(one, tmo);
-    if (dbg) fprintf(stderr, "tfidf: rccl_init_rank: polled, rc %d\n", rc);
-    if (rc == TFIDF_E_PEER) {
-        /* a peer never joined: the communicator is abandoned, not aborted — RCCL 2.27's
-         * ncclCommAbort joins the init thread, which waits for the absent peer forever */
+    auto job = std::make_shared<InitJob>();
+    std::thread([job, u, rank, nranks, device, tmo] {
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;
+        ncclComm_t comm = nullptr;
+        int rc = TFIDF_OK;
+        if (hipSetDevice(device) != hipSuccess) rc = TFIDF_E_HIP;
+        if (!rc && (nccl_issue(ncclCommInitRankConfig(&comm, nranks, u, rank, &cfg)) < 0 || !comm)) rc = TFIDF_E_RCCL;
+        if (!rc) {
+            std::vector<ncclComm_t> one{comm};
+            rc = comms_ready(one, tmo);
+        }
+        std::lock_guard<std::mutex> lk(job->mu);
+        if (job->abandoned || rc) {   /* nobody takes it: abort what was made */
+            if (comm) (void)ncclCommAbort(comm);
+            comm = nullptr;
+        }
+        job->rc = rc;
+        job->comm = comm;
+        job->done = true;
+        job->cv.notify_all();
+    }).detach();
+    std::unique_lock<std::mutex> lk(job->mu);
+    const bool done = tmo > 0 ? job->cv.wait_for(lk, std::chrono::milliseconds(tmo), [&] { return job->done; })
+                              : (job->cv.wait(lk, [&] { return job->done; }), true);
+    if (!done) {
+        job->abandoned = true;
         fprintf(stderr, "tfidf: rank %d of %d: the other ranks did not join within %lld s (TFIDF_COMM_TIMEOUT_S)\n",
                 rank, nranks, (long long)(tmo / 1000));
-        return rc;
+        return TFIDF_E_PEER;
     }
-    if (rc) {
-        (void)ncclCommAbort(comm);
-        return rc;
-    }
+    if (job->rc) return job->rc;
     RcclXport* x = new RcclXport();
-    x->cr.comm = comm;
+    x->cr.comm = job->comm;
     x->cr.timeout_ms = tmo;
     x->rank = rank;
     x->nranks = nranks;

@@ -49,10 +49,18 @@
 
 /* timing ablations (diagnostic builds only, wrong output by design): every record write of
  * K1 is suppressed so the stages after it see an empty, consistent record set */
-#if defined(SL_ABL_NOVOCAB) || defined(SL_ABL_NOCOUNT) || defined(SL_ABL_NOROUNDS) || defined(SL_ABL_NOWRITE)
+#if defined(SL_ABL_NOVOCAB) || defined(SL_ABL_NOCOUNT) || defined(SL_ABL_NOROUNDS) || defined(SL_ABL_NOWRITE) || \
+    defined(SL_ABL_NOALLOC)
 #define SL_ABL 1
 #else
 #define SL_ABL 0
+#endif
+/* SL_ABL_NOALLOC: the records are stored, all at the start of the arrays (no allocation
+ * atomics); the stage after K1 still sees an empty record set */
+#ifdef SL_ABL_NOALLOC
+#define SL_ABL_ST 0
+#else
+#define SL_ABL_ST SL_ABL
 #endif
 
 namespace {
@@ -320,12 +328,12 @@ __device__ __forceinline__ void sl_write_staged(SlShared& S, const K1Out* o, uin
     uint32_t* const part_cnt = o->part_cnt;
     const uint32_t smask = (1u << sb) - 1u;
     lds_barrier();
-    if (rec_ok && !SL_ABL)
+    if (rec_ok && !SL_ABL_ST)
         for (uint32_t i = (uint32_t)tid; i < nrec; i += NT) {
             gmem(rec_slot)[rb + i] = S.TK[i] & smask;
             gmem(rec_cnt)[rb + i] = S.TC[i];
         }
-    if (part_ok && !SL_ABL)
+    if (part_ok && !SL_ABL_ST)
         for (uint32_t i = (uint32_t)tid; i < npart; i += NT) {
             const uint32_t k = S.TK[nrec + i];
             gmem(part_doc)[pb + i] = gd0 + ((k & 0x7FFFFFFFu) >> sb);

@@ -18,6 +18,6 @@ for r in $(seq 1 ${ROUNDS:-2}); do
   done
 done
 if [ "${DIAG:-0}" = 1 ]; then
-  TFIDF_COMM_TIMEOUT_S=3 timeout -k 5 40 python3 -u scripts/r05_diag_init.py > $OUT/diag_init.log 2>&1
+  TFIDF_DEBUG_COMM=1 TFIDF_COMM_TIMEOUT_S=3 timeout -k 5 40 python3 -u scripts/r05_diag_init.py > $OUT/diag_init.log 2>&1
   echo "diag_init rc=$?"; grep -E "^ *[0-9]+\.[0-9]+ |tfidf:" $OUT/diag_init.log | tail -8
 fi
