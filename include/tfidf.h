@@ -188,9 +188,10 @@ typedef struct tfidf_run_info {
      * steady-state runs reads them before and after and expects no change */
     uint64_t device_allocs;
     uint64_t device_alloc_bytes;
-    /* the run's idf table, log(N/df) on the host's libm (TFIDF.c:243): up to 2^24 documents
-     * every df = 1..N is tabulated on host threads while the device runs the stages before
-     * the score (beyond that only the distinct df values, after the DF stage) */
+    /* the run's idf table, log(N/df) on the host's libm (TFIDF.c:243): up to 2^18 documents
+     * every df = 1..N is tabulated by the context's host worker threads while the device runs
+     * the stages before the score; beyond that only the run's distinct df values, after the DF
+     * stage (one host round trip) */
     uint64_t idf_logs;        /* libm log() calls made for this run's table (0: the table of
                                  the previous run's N was kept, TFIDF_IDF_CACHE=1) */
     double   ms_idf_host;     /* wall time of those calls (host threads) */

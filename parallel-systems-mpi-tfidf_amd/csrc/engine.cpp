@@ -126,6 +126,7 @@ struct tfidf_ctx {
     DevBuf stamps;
     bool k1_vs = false;     /* last run used the slot-keyed kernel (default) */
     bool k1_sl = false;     /* ... or tokcount_sl (else tokcount_vs) */
+    uint64_t sl_maxcap = K1_ST_MAX_CAP;   /* env TFIDF_SL_MAXCAP: tokcount_sl up to this many vocabulary slots */
     K1Out* k1out_host = nullptr;   /* pinned: tokcount_sl's output block, copied to k1out_dev per run */
     DevBuf k1out_dev;
     hipEvent_t ev[S_NSTAGES + 1];
@@ -148,7 +149,8 @@ struct tfidf_ctx {
      * the two slots it loads per token): 1M slots (16 MB) to start, x4 past 12 % load */
     uint64_t vcap = 1ull << 20;
 #define VOCAB_LOW_LOAD_CAP (1ull << 24)
-#define IDF_FULL_MAX (1ull << 24)   /* documents up to which the idf table covers every df */
+#define IDF_FULL_MAX (1ull << 18)   /* documents up to which the idf table covers every df (beyond:
+                                       the distinct df values of the run, one host round trip) */
     uint32_t vload_pct = 12;
     uint32_t vload_big_pct = 45;   /* load limit of tables of VOCAB_LOW_LOAD_CAP slots and more */
     DevBuf rec_slot, rec_cnt;
@@ -174,9 +176,18 @@ struct tfidf_ctx {
     double* idf_pin = nullptr;
     size_t idf_pin_n = 0;
     hipEvent_t ev_idf = nullptr;          /* the table's upload (idf_pin reusable after it) */
-    std::vector<std::thread> idf_th;
-    std::vector<int64_t> idf_end_ns;      /* per thread: when it finished */
-    std::chrono::steady_clock::time_point idf_t0;
+    struct IdfPool {                      /* persistent workers: no thread start per run */
+        std::mutex mu;
+        std::condition_variable go, done;
+        std::vector<std::thread> th;
+        uint64_t gen = 0;
+        bool stop = false, busy = false;
+        unsigned active = 0, left = 0;
+        double* lut = nullptr;
+        uint64_t Nt = 0;
+        std::chrono::steady_clock::time_point t0;
+        int64_t end_ns = 0;
+    } idf_pool;
     uint64_t idf_logs = 0;                /* log() calls of the last run */
     double ms_idf_host = 0, ms_idf_wait = 0;
     DevBuf dkey0, dkey1, dseq0, dseq1, npairs_ord, out_off, doc_meta;
@@ -225,6 +236,7 @@ struct tfidf_ctx {
     double ms_total = 0;
     hipError_t last_err = hipSuccess;
 };
+static void idf_pool_stop(tfidf_ctx* ctx);   /* the per-run idf table's workers (idf_start) */
 
 #define HIPCHK(x)                                                                          \
     do {                                                                                   \
@@ -296,6 +308,11 @@ int tfidf_open(int device, tfidf_ctx** out) {
     if (km && !strcmp(km, "general")) ctx->k1_mode = 2;
     if (km && !strcmp(km, "vs")) ctx->k1_mode = 1;
     if (km && !strcmp(km, "sl")) ctx->k1_mode = 3;
+    {
+        const char* sm = getenv("TFIDF_SL_MAXCAP");
+        const unsigned long long v = sm ? strtoull(sm, nullptr, 0) : 0ull;
+        if (v >= 1024 && v <= K1_SL_MAX_CAP) ctx->sl_maxcap = v;
+    }
     const char* ks = getenv("TFIDF_STAMPS");
     ctx->stamps_on = ks && ks[0] == '1';
     const char* kx = getenv("TFIDF_TEST_XFAIL_RANK");
@@ -353,7 +370,7 @@ void tfidf_close(tfidf_ctx* ctx) {
     if (ctx->stream2) { (void)hipStreamSynchronize(ctx->stream2); (void)hipStreamDestroy(ctx->stream2); }
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_order) (void)hipEventDestroy(ctx->ev_order);
-    for (auto& t : ctx->idf_th) t.join();
+    idf_pool_stop(ctx);
     if (ctx->ev_idf) { (void)hipEventSynchronize(ctx->ev_idf); (void)hipEventDestroy(ctx->ev_idf); }
     if (ctx->idf_pin) (void)hipHostFree(ctx->idf_pin);
     for (int i = 0; i < WR_NBUF; ++i) {
@@ -736,8 +753,10 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     const bool aligned = (((uintptr_t)c.bytes & 15u) == 0);
     ctx->k1_vs = aligned && ctx->k1_mode != 2;
     if (ctx->k1_vs && ctx->vcap > K1_VS_MAX_CAP) return TFIDF_E_CAPACITY;
-    ctx->k1_sl = ctx->k1_vs && (ctx->k1_mode == 0 || ctx->k1_mode == 3) && ctx->vcap <= K1_ST_MAX_CAP;
-    const uint32_t cb = ctx->k1_sl ? CHUNK_BYTES_ST : CHUNK_BYTES;
+    ctx->k1_sl = ctx->k1_vs && (ctx->k1_mode == 0 || ctx->k1_mode == 3) && ctx->vcap <= ctx->sl_maxcap;
+    /* tokcount_sl over a high-cardinality table (TFIDF_SL_MAXCAP): half-size chunks, as
+     * tokcount_vs, since nearly every token is a new pair for its LDS table */
+    const uint32_t cb = ctx->k1_sl ? (ctx->vcap > K1_ST_MAX_CAP ? CHUNK_BYTES : CHUNK_BYTES_ST) : CHUNK_BYTES;
     const uint64_t nchunks = span ? (span + cb - 1) / cb : 0;
     if (ctx->rec_cap == 0) ctx->rec_cap = span / 6 + 4096;
     if (ctx->part_cap == 0) ctx->part_cap = span / 64 + 4096;
@@ -1046,6 +1065,37 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
  * (TFIDF.c:243 evaluates log(1.0*N/df) per pair; the table holds the same doubles), on up to
  * eight host threads started when the run starts, so the logs run beside K1 .. DF on the
  * device.  run_post waits for them (ms_idf_wait: normally 0) and uploads the table. */
+#define IDF_POOL 8
+static void idf_worker(tfidf_ctx::IdfPool* P, unsigned i) {
+    uint64_t seen = 0;
+    for (;;) {
+        std::unique_lock<std::mutex> lk(P->mu);
+        P->go.wait(lk, [&] { return P->stop || P->gen != seen; });
+        if (P->stop) return;
+        seen = P->gen;
+        if (i >= P->active) continue;
+        double* lut = P->lut;
+        const uint64_t Nt = P->Nt, lo = 1 + (Nt * i) / P->active, hi = 1 + (Nt * (i + 1)) / P->active;
+        const auto t0 = P->t0;
+        lk.unlock();
+        for (uint64_t d = lo; d < hi; ++d) lut[d] = log(1.0 * (double)Nt / (double)d);
+        const int64_t e = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+        lk.lock();
+        P->end_ns = e > P->end_ns ? e : P->end_ns;
+        if (--P->left == 0) P->done.notify_all();
+    }
+}
+static void idf_pool_stop(tfidf_ctx* ctx) {
+    tfidf_ctx::IdfPool& P = ctx->idf_pool;
+    {
+        std::unique_lock<std::mutex> lk(P.mu);
+        P.done.wait(lk, [&] { return P.left == 0; });
+        P.stop = true;
+    }
+    P.go.notify_all();
+    for (auto& t : P.th) t.join();
+    P.th.clear();
+}
 static int idf_start(tfidf_ctx* ctx, uint64_t Nt) {
     ctx->idf_logs = 0;
     ctx->ms_idf_host = ctx->ms_idf_wait = 0;
@@ -1060,33 +1110,36 @@ static int idf_start(tfidf_ctx* ctx, uint64_t Nt) {
         if (hipHostMalloc((void**)&ctx->idf_pin, n * 8, hipHostMallocDefault) != hipSuccess) return TFIDF_E_NOMEM;
         ctx->idf_pin_n = n;
     }
+    tfidf_ctx::IdfPool& P = ctx->idf_pool;
+    if (P.th.empty())
+        for (unsigned i = 0; i < IDF_POOL; ++i) P.th.emplace_back(idf_worker, &P, i);
     ctx->idf_full_n = 0;   /* idf_vals is rewritten by this run */
-    const unsigned nt = (unsigned)(n / 8192 < 1 ? 1 : (n / 8192 > 8 ? 8 : n / 8192));
-    ctx->idf_end_ns.assign(nt, 0);
-    ctx->idf_t0 = std::chrono::steady_clock::now();
-    double* lut = ctx->idf_pin;
-    lut[0] = 0.0;   /* df >= 1 for every term that occurs */
-    for (unsigned t = 0; t < nt; ++t) {
-        const uint64_t lo = 1 + (Nt * t) / nt, hi = 1 + (Nt * (t + 1)) / nt;
-        ctx->idf_th.emplace_back([ctx, lut, lo, hi, Nt, t] {
-            for (uint64_t d = lo; d < hi; ++d) lut[d] = log(1.0 * (double)Nt / (double)d);
-            ctx->idf_end_ns[t] = std::chrono::duration_cast<std::chrono::nanoseconds>(
-                                     std::chrono::steady_clock::now() - ctx->idf_t0).count();
-        });
+    ctx->idf_pin[0] = 0.0;   /* df >= 1 for every term that occurs */
+    {
+        std::lock_guard<std::mutex> lk(P.mu);
+        P.active = (unsigned)(n / 16384 < 1 ? 1 : (n / 16384 > IDF_POOL ? IDF_POOL : n / 16384));
+        P.left = P.active;
+        P.lut = ctx->idf_pin;
+        P.Nt = Nt;
+        P.t0 = std::chrono::steady_clock::now();
+        P.end_ns = 0;
+        P.busy = true;
+        ++P.gen;
     }
+    P.go.notify_all();
     ctx->idf_logs = Nt;
     return TFIDF_OK;
 }
-/* joins the table's threads (also on every error path of tfidf_run) */
+/* waits for the table's workers (also on every error path of tfidf_run) */
 static void idf_join(tfidf_ctx* ctx) {
-    if (ctx->idf_th.empty()) return;
+    tfidf_ctx::IdfPool& P = ctx->idf_pool;
+    if (!P.busy) return;
     const auto w0 = std::chrono::steady_clock::now();
-    for (auto& t : ctx->idf_th) t.join();
-    ctx->idf_th.clear();
+    std::unique_lock<std::mutex> lk(P.mu);
+    P.done.wait(lk, [&] { return P.left == 0; });
+    P.busy = false;
     ctx->ms_idf_wait = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
-    int64_t e = 0;
-    for (int64_t x : ctx->idf_end_ns) e = x > e ? x : e;
-    ctx->ms_idf_host = (double)e * 1e-6;
+    ctx->ms_idf_host = (double)P.end_ns * 1e-6;
 }
 struct IdfJoin {
     tfidf_ctx* c;
@@ -1115,7 +1168,7 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
     constexpr uint32_t IDF_SPEC = 16384;
     std::vector<uint32_t> vals;
     if (full_lut) {
-        if (!ctx->idf_th.empty()) {   /* this run's table (idf_start): join, upload */
+        if (ctx->idf_pool.busy) {   /* this run's table (idf_start): join, upload */
             ENSURE(ctx->idf_vals, (size_t)(Nt + 1) * 8);
             idf_join(ctx);
             HIPCHK(hipMemcpyAsync(ctx->idf_vals.p, ctx->idf_pin, (size_t)(Nt + 1) * 8, hipMemcpyHostToDevice, s));
@@ -1158,6 +1211,7 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
         ENSURE(ctx->idf_vals, (size_t)K * 8 + 8);
         std::vector<double> idf(K);
         for (uint32_t k = 0; k < K; ++k) idf[k] = log(1.0 * (double)Nt / (double)vals[k]);
+        ctx->idf_logs = K;   /* this run's distinct df values */
         if (K) HIPCHK(hipMemcpyAsync(ctx->idf_vals.p, idf.data(), (size_t)K * 8, hipMemcpyHostToDevice, s));
     }
     /* the output arrays are sized by the record bound (pairs <= records): the pair total P

@@ -102,6 +102,7 @@ int launch_tokcount_vs(const CorpusDev& c, const uint64_t* chunk_start, const ui
 #define K1_VS_MAX_CAP (1ull << 28)
 
 #define K1_ST_MAX_CAP (1ull << 22)   /* tokcount_sl up to this vocabulary capacity, tokcount_vs beyond */
+#define K1_SL_MAX_CAP (1ull << 25)   /* the largest table tokcount_sl can address (TFIDF_SL_MAXCAP, A/B) */
 /* K1 default (tokcount_sl.hip): one workgroup per chunk, straight-line rounds; the output
  * block is read from device memory (o_dev: a K1Out the engine copies there per run).
  * 16-byte aligned corpus base; -3 when the vocabulary exceeds K1_ST_MAX_CAP slots */

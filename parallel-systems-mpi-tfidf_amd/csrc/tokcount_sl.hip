@@ -88,7 +88,8 @@ constexpr uint32_t WAVE_CLAIMS = (TB - 2 * NT - 64) / NWAVE;   /* claims per wav
 constexpr int GCAP = 256;               /* documents per group at most */
 constexpr int TLW = 192;                /* token entries per wave and pass */
 constexpr uint32_t LEN_LONG = 31u;
-constexpr uint32_t SLOT_BITS = 22;      /* vocabulary slots < 2^22 (K1_ST_MAX_CAP) */
+constexpr uint32_t SLOT_BITS = 25;      /* vocabulary slots < 2^25 (K1_SL_MAX_CAP; the LDS key's document
+                                           field shrinks as the slot field grows: gcap below) */
 constexpr int PMAX = 16;
 #ifdef SL_STAMPS
 constexpr int SL_NPH = 12;              /* diagnostic phases (SL_STAMPS) */
