@@ -185,6 +185,8 @@ struct tfidf_ctx {
         unsigned active = 0, left = 0;
         double* lut = nullptr;
         uint64_t Nt = 0;
+        const uint32_t* vals = nullptr;   /* null: lut[d] for every df d = 1..Nt; else lut[k] for df vals[k], k < n */
+        uint64_t n = 0;
         std::chrono::steady_clock::time_point t0;
         int64_t end_ns = 0;
     } idf_pool;
@@ -1075,10 +1077,14 @@ static void idf_worker(tfidf_ctx::IdfPool* P, unsigned i) {
         seen = P->gen;
         if (i >= P->active) continue;
         double* lut = P->lut;
-        const uint64_t Nt = P->Nt, lo = 1 + (Nt * i) / P->active, hi = 1 + (Nt * (i + 1)) / P->active;
+        const uint32_t* vals = P->vals;
+        const uint64_t Nt = P->Nt, n = P->n, lo = (n * i) / P->active, hi = (n * (i + 1)) / P->active;
         const auto t0 = P->t0;
         lk.unlock();
-        for (uint64_t d = lo; d < hi; ++d) lut[d] = log(1.0 * (double)Nt / (double)d);
+        if (vals)
+            for (uint64_t k = lo; k < hi; ++k) lut[k] = log(1.0 * (double)Nt / (double)vals[k]);
+        else
+            for (uint64_t d = lo + 1; d < hi + 1; ++d) lut[d] = log(1.0 * (double)Nt / (double)d);
         const int64_t e = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
         lk.lock();
         P->end_ns = e > P->end_ns ? e : P->end_ns;
@@ -1096,6 +1102,26 @@ static void idf_pool_stop(tfidf_ctx* ctx) {
     for (auto& t : P.th) t.join();
     P.th.clear();
 }
+/* posts a table job to the context's workers (lut: n values; vals null = every df 1..n) */
+static void idf_post(tfidf_ctx* ctx, double* lut, uint64_t Nt, const uint32_t* vals, uint64_t n) {
+    tfidf_ctx::IdfPool& P = ctx->idf_pool;
+    if (P.th.empty())
+        for (unsigned i = 0; i < IDF_POOL; ++i) P.th.emplace_back(idf_worker, &P, i);
+    {
+        std::lock_guard<std::mutex> lk(P.mu);
+        P.active = (unsigned)(n / 16384 < 1 ? 1 : (n / 16384 > IDF_POOL ? IDF_POOL : n / 16384));
+        P.left = P.active;
+        P.lut = lut;
+        P.Nt = Nt;
+        P.vals = vals;
+        P.n = n;
+        P.t0 = std::chrono::steady_clock::now();
+        P.end_ns = 0;
+        P.busy = true;
+        ++P.gen;
+    }
+    P.go.notify_all();
+}
 static int idf_start(tfidf_ctx* ctx, uint64_t Nt) {
     ctx->idf_logs = 0;
     ctx->ms_idf_host = ctx->ms_idf_wait = 0;
@@ -1110,23 +1136,9 @@ static int idf_start(tfidf_ctx* ctx, uint64_t Nt) {
         if (hipHostMalloc((void**)&ctx->idf_pin, n * 8, hipHostMallocDefault) != hipSuccess) return TFIDF_E_NOMEM;
         ctx->idf_pin_n = n;
     }
-    tfidf_ctx::IdfPool& P = ctx->idf_pool;
-    if (P.th.empty())
-        for (unsigned i = 0; i < IDF_POOL; ++i) P.th.emplace_back(idf_worker, &P, i);
     ctx->idf_full_n = 0;   /* idf_vals is rewritten by this run */
     ctx->idf_pin[0] = 0.0;   /* df >= 1 for every term that occurs */
-    {
-        std::lock_guard<std::mutex> lk(P.mu);
-        P.active = (unsigned)(n / 16384 < 1 ? 1 : (n / 16384 > IDF_POOL ? IDF_POOL : n / 16384));
-        P.left = P.active;
-        P.lut = ctx->idf_pin;
-        P.Nt = Nt;
-        P.t0 = std::chrono::steady_clock::now();
-        P.end_ns = 0;
-        P.busy = true;
-        ++P.gen;
-    }
-    P.go.notify_all();
+    idf_post(ctx, ctx->idf_pin, Nt, nullptr, Nt);
     ctx->idf_logs = Nt;
     return TFIDF_OK;
 }
@@ -1209,10 +1221,23 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
             HIPCHK(hipMemcpy(vals.data() + spec, vals_dev + spec, (size_t)(K - spec) * 4, hipMemcpyDeviceToHost));
         }
         ENSURE(ctx->idf_vals, (size_t)K * 8 + 8);
-        std::vector<double> idf(K);
-        for (uint32_t k = 0; k < K; ++k) idf[k] = log(1.0 * (double)Nt / (double)vals[k]);
+        /* the distinct df values' logs on the context's workers, into pinned memory */
+        HIPCHK(hipEventSynchronize(ctx->ev_idf));   /* the previous upload has read idf_pin */
+        if (ctx->idf_pin_n < (size_t)K + 1) {
+            if (ctx->idf_pin) (void)hipHostFree(ctx->idf_pin);
+            ctx->idf_pin = nullptr;
+            ctx->idf_pin_n = 0;
+            if (hipHostMalloc((void**)&ctx->idf_pin, ((size_t)K + 1) * 8, hipHostMallocDefault) != hipSuccess)
+                return TFIDF_E_NOMEM;
+            ctx->idf_pin_n = (size_t)K + 1;
+        }
+        if (K) {
+            idf_post(ctx, ctx->idf_pin, Nt, vals.data(), K);
+            idf_join(ctx);
+            HIPCHK(hipMemcpyAsync(ctx->idf_vals.p, ctx->idf_pin, (size_t)K * 8, hipMemcpyHostToDevice, s));
+            HIPCHK(hipEventRecord(ctx->ev_idf, s));
+        }
         ctx->idf_logs = K;   /* this run's distinct df values */
-        if (K) HIPCHK(hipMemcpyAsync(ctx->idf_vals.p, idf.data(), (size_t)K * 8, hipMemcpyHostToDevice, s));
     }
     /* the output arrays are sized by the record bound (pairs <= records): the pair total P
      * comes back with the final status word */

@@ -16,4 +16,4 @@ for c in c5 c3; do
 done
 timeout -k 10 600 python3 bench.py --no-cpu-baseline --no-probe --no-emit --config c3 --steps 5 --warmup 2 > $OUT/c3.json 2> $OUT/c3.err || { tail -20 $OUT/c3.err; exit 1; }
 python3 -c "import json; d=json.load(open('$OUT/c3.json')); print('c3', d['value'], d['ms_per_step'], d['device_ms_per_step'], d['stage_ms_mean']['idf'], d['idf'])"
-CFG=c4 VARIANTS="base env:TFIDF_SL_MAXCAP=33554432" ROUNDS=2 bash scripts/r05_c.sh
+[ -n "$TESTK" ] && { timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$TESTK" > $OUT/gpu_tests.log 2>&1 || { echo "TESTS FAILED"; grep -E "FAIL|Error" $OUT/gpu_tests.log | tail -20; exit 1; }; echo "tests: $(tail -1 $OUT/gpu_tests.log)"; }
