@@ -127,10 +127,6 @@ struct tfidf_ctx {
     bool k1_vs = false;     /* last run used the slot-keyed kernel (default) */
     bool k1_sl = false;     /* ... or tokcount_sl (else tokcount_vs) */
     uint64_t sl_maxcap = K1_ST_MAX_CAP;   /* env TFIDF_SL_MAXCAP: tokcount_sl up to this many vocabulary slots */
-    bool df_k1 = false;                   /* env TFIDF_DF_K1=1: K1 counts df in slot space (A/B) */
-    bool run_df_k1 = false;               /* ... and the last run did (K5 maps K1's records' slots) */
-    uint64_t run_R_main = 0;
-    DevBuf df_slot;
     K1Out* k1out_host = nullptr;   /* pinned: tokcount_sl's output block, copied to k1out_dev per run */
     DevBuf k1out_dev;
     hipEvent_t ev[S_NSTAGES + 1];
@@ -319,10 +315,6 @@ int tfidf_open(int device, tfidf_ctx** out) {
         const unsigned long long v = sm ? strtoull(sm, nullptr, 0) : 0ull;
         if (v >= 1024 && v <= K1_SL_MAX_CAP) ctx->sl_maxcap = v;
     }
-    {
-        const char* dk = getenv("TFIDF_DF_K1");
-        ctx->df_k1 = dk && dk[0] == '1';
-    }
     const char* ks = getenv("TFIDF_STAMPS");
     ctx->stamps_on = ks && ks[0] == '1';
     const char* kx = getenv("TFIDF_TEST_XFAIL_RANK");
@@ -404,7 +396,7 @@ void tfidf_close(tfidf_ctx* ctx) {
                       &ctx->x_sidx, &ctx->x_back, &ctx->x_cnt, &ctx->x_rrec, &ctx->x_rslot, &ctx->x_reply, &ctx->x_gkeys,
                       &ctx->x_pos, &ctx->x_dense,
                       &ctx->x_tkey, &ctx->x_tdf, &ctx->stamps, &ctx->big_list, &ctx->big_idx, &ctx->dense_cnt, &ctx->kcnt,
-                      &ctx->tile_cnt, &ctx->df_slot};
+                      &ctx->tile_cnt};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i <= S_NSTAGES; ++i) (void)hipEventDestroy(ctx->ev[i]);
     if (ctx->hpin) (void)hipHostFree(ctx->hpin);
@@ -815,12 +807,6 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     o.chunk_shard = cnt + 16;
     o.status = (uint32_t*)(cnt + 3);
     o.stamps = nullptr;
-    o.df_slot = nullptr;
-    if (ctx->df_k1 && ctx->k1_sl) {
-        ENSURE(ctx->df_slot, ctx->vcap * 4);
-        HIPCHK(hipMemsetAsync(ctx->df_slot.p, 0, ctx->vcap * 4, s));
-        o.df_slot = ctx->df_slot.as<uint32_t>();
-    }
     if (ctx->stamps_on) {
         ENSURE(ctx->stamps, 8 * K1_DEBUG_WORDS);
         HIPCHK(hipMemsetAsync(ctx->stamps.p, 0, 8 * K1_DEBUG_WORDS, s));
@@ -1058,23 +1044,11 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     mark(ctx, S_DF);
     ENSURE(ctx->df_local, (size_t)V * 4 + 4);
     ENSURE(ctx->df_global, (size_t)V * 4 + 4);
-    ctx->run_df_k1 = ctx->df_k1 && ctx->k1_sl;
-    if (ctx->run_df_k1) {
-        /* K1 counted the complete documents' records per slot: the DF pass counts only the
-         * merged records (ranks, after R_main), then the slot counts join by rank */
-        LCHK(launch_df_hist(ctx->rec_slot.as<uint32_t>() + R_main, 0, merged_count, R_total - R_main,
-                            ctx->rank_of_slot.as<uint32_t>(), V <= 65536u ? ctx->rank16.as<uint16_t>() : nullptr, V,
-                            cap, (uint32_t*)(cnt + 3), ctx->df_local.as<uint32_t>(), ar, s));
-        LCHK(launch_df_add_slot(ctx->df_local.as<uint32_t>(), ctx->df_slot.as<uint32_t>(),
-                                ctx->slot_of_rank.as<uint32_t>(), V, s));
-    } else {
-        /* also rewrites every record's slot as its term rank (K5 then needs no rank gather) */
-        LCHK(launch_df_hist(ctx->rec_slot.as<uint32_t>(), R_main, merged_count, R_total,
-                            ctx->rank_of_slot.as<uint32_t>(),
-                            V <= 65536u ? ctx->rank16.as<uint16_t>() : nullptr, V, cap,
-                            (uint32_t*)(cnt + 3), ctx->df_local.as<uint32_t>(), ar, s));
-    }
-    ctx->run_R_main = R_main;
+    /* also rewrites every record's slot as its term rank (K5 then needs no rank gather) */
+    LCHK(launch_df_hist(ctx->rec_slot.as<uint32_t>(), R_main, merged_count, R_total,
+                        ctx->rank_of_slot.as<uint32_t>(),
+                        V <= 65536u ? ctx->rank16.as<uint16_t>() : nullptr, V, cap,
+                        (uint32_t*)(cnt + 3), ctx->df_local.as<uint32_t>(), ar, s));
     ctx->run_V = V;
     ctx->run_cap = cap;
     ctx->run_R_total = R_total;
@@ -1309,9 +1283,6 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
     a.nterms = V;
     a.rank_bits = V > 1 ? 32u - (uint32_t)__builtin_clz(V - 1) : 1u;
     a.rec_total = R_total;
-    a.slot_recs = ctx->run_df_k1 ? 1u : 0u;
-    a.ranked_from = ctx->run_R_main;
-    a.rank16 = V <= 65536u ? ctx->rank16.as<uint16_t>() : nullptr;
     a.slot_cap = cap;
     a.status = (uint32_t*)(cnt + 3);
     a.out_term = ctx->out_term.as<uint32_t>();

@@ -896,19 +896,6 @@ __global__ __launch_bounds__(DFS_NT) void k_dfs_slice(const uint32_t* __restrict
     for (uint32_t j = threadIdx.x; j < sw; j += DFS_NT) df[s0 + j] = sbins[j];
 }
 
-/* df[r] += df_slot[slot_of_rank[r]]: K1's df in slot space (the complete documents' records)
- * joined to the term ranks, after the DF pass counted the merged records */
-__global__ void k_df_add_slot(uint32_t* __restrict__ df, const uint32_t* __restrict__ df_slot,
-                              const uint32_t* __restrict__ slot_of_rank, uint32_t V) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r < V) df[r] += df_slot[slot_of_rank[r]];
-}
-int launch_df_add_slot(uint32_t* df, const uint32_t* df_slot, const uint32_t* slot_of_rank, uint32_t V, hipStream_t s) {
-    if (!V) return 0;
-    k_df_add_slot<<<grid_for(V), NT, 0, s>>>(df, df_slot, slot_of_rank, V);
-    return ok();
-}
-
 int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra, uint64_t nrec_max,
                    const uint32_t* rank_of_slot, const uint16_t* rank16, uint32_t V, uint64_t slot_cap,
                    uint32_t* status, uint32_t* df, Arena& ar, hipStream_t s) {
@@ -1093,14 +1080,8 @@ __device__ __forceinline__ void k5_emit(const K5Args& a, uint64_t o, double ds, 
     sto(&a.out_score[o], (double)(tf * k5_idf(a, rank))); /* TFIDF.c:243-244 (idf from the host-libm LUT) */
 }
 
-/* records hold term ranks once the DF pass has run (k_df_hist_* rewrite them in place); with
- * slot_recs, K1's records (those below ranked_from: a document's records all lie on one side)
- * still hold vocabulary slots and are mapped here */
-__device__ __forceinline__ uint32_t k5_rank(const K5Args& a, uint32_t r, uint64_t rb) {
-    if (a.slot_recs && rb < a.ranked_from) {
-        if (r >= a.slot_cap) { atomicOr(a.status, ST_BOUNDS); return 0u; }
-        r = a.rank16 ? (uint32_t)G(a.rank16)[r] : G(a.rank_of_slot)[r];
-    }
+/* records hold term ranks once the DF pass has run (k_df_hist_* rewrite them in place) */
+__device__ __forceinline__ uint32_t k5_rank(const K5Args& a, uint32_t r) {
     if (r >= a.nterms) { atomicOr(a.status, ST_BOUNDS); r = 0; }
     return r;
 }
@@ -1268,7 +1249,7 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
 #pragma unroll
         for (int q = 0; q < K5_PF; ++q) {
             const uint32_t j = 64u * q + lane;
-            r[q] = (small_doc && j < n) ? k5_rank(a, s_cur[q], rb) : 0xFFFFFFFFu;
+            r[q] = (small_doc && j < n) ? k5_rank(a, s_cur[q]) : 0xFFFFFFFFu;
             if (small_doc && j < n) buf0[j] = c_cur[q]; /* counts by record index */
         }
         if (small_doc && n > 64u * K5_PF) { /* beyond the prefetch: loaded here */
@@ -1282,7 +1263,7 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
 #pragma unroll
             for (int q = K5_PF; q < K5_RQ; ++q) {
                 const uint32_t j = 64u * q + lane;
-                r[q] = j < n ? k5_rank(a, sx[q - K5_PF], rb) : 0xFFFFFFFFu;
+                r[q] = j < n ? k5_rank(a, sx[q - K5_PF]) : 0xFFFFFFFFu;
             }
         } else {
 #pragma unroll
@@ -1590,7 +1571,7 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
 #pragma unroll
             for (int e = 0; e < K5L_EB; ++e) {
                 const uint32_t j = j0 + NT * e + tid;
-                if (j < n) rk[e] = k5_rank(a, rk[e], rb);
+                if (j < n) rk[e] = k5_rank(a, rk[e]);
                 f[e] = j < n ? k5_idf(a, rk[e]) : 0.0;
             }
 #pragma unroll
@@ -1617,7 +1598,7 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
         for (int e = 0; e < K5L_EB; ++e) {
             const uint32_t j = j0 + NT * e + tid;
             if (j < n) {
-                kbuf[0][j] = k5_rank(a, sl[e], rb);
+                kbuf[0][j] = k5_rank(a, sl[e]);
                 vbuf[0][j] = cn[e];
             }
         }
@@ -1885,7 +1866,7 @@ __global__ __launch_bounds__(256, K5S_OCC) void k_score_small(K5Args a) {
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const bool v = 64u * q + lane < d.n;
-            if (v) r[q] = k5_rank(a, r[q], d.rb);
+            if (v) r[q] = k5_rank(a, r[q]);
             f[q] = v ? k5_idf(a, r[q]) : 0.0;
         }
     };
@@ -1979,7 +1960,7 @@ __global__ __launch_bounds__(256) void k_emit_split(K5Args a) {
 #pragma unroll
             for (int e = 0; e < K5L_EB; ++e) {
                 const uint32_t j = j0 + 256u * e + threadIdx.x;
-                if (j < j1) rk[e] = k5_rank(a, rk[e], rb);
+                if (j < j1) rk[e] = k5_rank(a, rk[e]);
                 f[e] = j < j1 ? k5_idf(a, rk[e]) : 0.0;
             }
 #pragma unroll

@@ -82,8 +82,6 @@ struct K1Out {
     unsigned long long* chunk_shard; /* tokcount_st: 8 sharded chunk counters (zeroed per run) */
     unsigned long long* stamps;  /* diagnostic build only: K1_NSTAMP phase cycle sums, WG count,
                                     then K1_NCOUNT event counters */
-    uint32_t* df_slot;           /* non-null (tokcount_sl): complete documents' records also counted
-                                    per vocabulary slot, df in slot space */
 };
 #define K1_NSTAMP 17
 #define K1_NCOUNT 4   /* segments, flushes, tokens taking the full probe, probe iterations */
@@ -150,7 +148,6 @@ int launch_dense_emit(const uint32_t* dense, uint32_t nb, uint32_t V, const uint
                       uint8_t* doc_flags, Arena& ar, hipStream_t s);
 
 /* DF */
-int launch_df_add_slot(uint32_t* df, const uint32_t* df_slot, const uint32_t* slot_of_rank, uint32_t V, hipStream_t s);
 int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra, uint64_t nrec_max,
                    const uint32_t* rank_of_slot, const uint16_t* rank16, uint32_t V, uint64_t slot_cap,
                    uint32_t* status, uint32_t* df, Arena& ar, hipStream_t s);
@@ -195,10 +192,6 @@ struct K5Args {
                                     table: a 4-byte gather into V words + an L2-resident table instead of
                                     an 8-byte gather into V doubles; idf_rank is not built) */
     uint64_t rec_total;          /* bounds guard: records in rec_slot/rec_cnt */
-    uint32_t slot_recs;          /* 1: records below ranked_from still hold vocabulary slots (K1 counted df
-                                    in slot space, no DF pass rewrote them): K5 maps them to ranks */
-    uint64_t ranked_from;
-    const uint16_t* rank16;      /* slot -> rank as u16 (V <= 65536), else rank_of_slot */
     uint64_t slot_cap;           /* bounds guard: vocabulary capacity */
     uint32_t* status;            /* ST_BOUNDS set instead of faulting */
     uint32_t* out_term;          /* output order: term rank */

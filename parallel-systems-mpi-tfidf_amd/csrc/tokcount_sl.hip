@@ -329,21 +329,11 @@ __device__ __forceinline__ void sl_write_staged(SlShared& S, const K1Out* o, uin
     uint32_t* const part_cnt = o->part_cnt;
     const uint32_t smask = (1u << sb) - 1u;
     lds_barrier();
-    uint32_t* const df_slot = o->df_slot;
-    if (rec_ok && !SL_ABL_ST) {
-        if (df_slot)   /* df in slot space: one atomic per record (every record is a distinct (document, term)) */
-            for (uint32_t i = (uint32_t)tid; i < nrec; i += NT) {
-                const uint32_t sl = S.TK[i] & smask;
-                gmem(rec_slot)[rb + i] = sl;
-                gmem(rec_cnt)[rb + i] = S.TC[i];
-                atomicAdd(&df_slot[sl], 1u);
-            }
-        else
-            for (uint32_t i = (uint32_t)tid; i < nrec; i += NT) {
-                gmem(rec_slot)[rb + i] = S.TK[i] & smask;
-                gmem(rec_cnt)[rb + i] = S.TC[i];
-            }
-    }
+    if (rec_ok && !SL_ABL_ST)
+        for (uint32_t i = (uint32_t)tid; i < nrec; i += NT) {
+            gmem(rec_slot)[rb + i] = S.TK[i] & smask;
+            gmem(rec_cnt)[rb + i] = S.TC[i];
+        }
     if (part_ok && !SL_ABL_ST)
         for (uint32_t i = (uint32_t)tid; i < npart; i += NT) {
             const uint32_t k = S.TK[nrec + i];
