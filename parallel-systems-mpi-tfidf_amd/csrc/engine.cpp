@@ -536,12 +536,14 @@ static int exchange_owner(tfidf_ctx* ctx, uint32_t V, const std::vector<uint64_t
     ens(ctx->x_sidx, (size_t)V * 4 + 4);
     ens(ctx->x_back, ((size_t)V + R) * 4 + 4);
     ens(ctx->x_rrec, sumv * 20 + 20);
-    ens(ctx->x_rslot, sumv * 4 + 4);
     ens(ctx->x_reply, (sumv + R) * 4 + 4);
-    ens(ctx->x_tkey, table_cap(sumv) * 16);
-    /* the table form's df column, or the bucketed form's spread counters */
-    const size_t xb_cnt = ((size_t)owner_buckets(sumv) + 1) * 128;
-    ens(ctx->x_tdf, table_cap(sumv) * 4 > xb_cnt ? table_cap(sumv) * 4 : xb_cnt);
+    if (ctx->xagg_table) {   /* TFIDF_XAGG=table: the HBM table and its df column */
+        ens(ctx->x_tkey, table_cap(sumv) * 16);
+        ens(ctx->x_tdf, table_cap(sumv) * 4);
+        ens(ctx->x_rslot, sumv * 4 + 4);
+    } else {                 /* the bucketed form's sort scratch */
+        ens(ctx->x_tkey, owner_bucket_scratch(sumv));
+    }
     if (ctx->xnomem_rank == me) {   /* tests: an agreed allocation failure (once) */
         ctx->xnomem_rank = -1;
         arc = TFIDF_E_NOMEM;
@@ -597,12 +599,9 @@ static int exchange_owner(tfidf_ctx* ctx, uint32_t V, const std::vector<uint64_t
         XCHK(launch_owner_aggregate(ctx->x_rrec.as<uint32_t>(), nrecv, roff, (uint32_t)R, ctx->x_tkey.as<uint4>(),
                                     table_cap(nrecv), ctx->x_tdf.as<uint32_t>(), ctx->x_rslot.as<uint32_t>(),
                                     ctx->x_reply.as<uint32_t>(), used, (uint32_t*)(cnt + 3), s));
-    } else {   /* bucketed: x_tkey (24 B per received record) and x_tdf are its scratch */
-        uint4* bkey = ctx->x_tkey.as<uint4>();
-        uint32_t* bdf = (uint32_t*)(bkey + nrecv);
-        XCHK(launch_owner_aggregate_buckets(ctx->x_rrec.as<uint32_t>(), nrecv, roff, (uint32_t)R, bkey, bdf,
-                                            bdf + nrecv, ctx->x_rslot.as<uint32_t>(), ctx->x_tdf.as<uint32_t>(),
-                                            ctx->x_reply.as<uint32_t>(), used, (uint32_t*)(cnt + 3), s));
+    } else {   /* bucketed: x_tkey is its scratch */
+        XCHK(launch_owner_aggregate_buckets(ctx->x_rrec.as<uint32_t>(), nrecv, roff, (uint32_t)R, ctx->x_tkey.p,
+                                            ctx->x_tkey.cap, ctx->x_reply.as<uint32_t>(), used, (uint32_t*)(cnt + 3), s));
     }
     rc = xp->alltoallv(ctx->x_reply.p, rcnt1.data(), ctx->x_back.p, scnt1.data(), 4, s);
     if (rc) return rc;

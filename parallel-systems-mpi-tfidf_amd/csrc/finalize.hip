@@ -2279,150 +2279,213 @@ int launch_owner_aggregate(const uint32_t* rrec, uint64_t n, const uint32_t* rof
     k_owner_reply<<<grid_for(m), NT, 0, s>>>(rslot, n, roff, R, tdf, used, reply);
     return ok();
 }
-/* ---- the owner's aggregation, bucketed (round 4): the received records are partitioned by
- * the top bits of their key hash into buckets of ~XB_MEAN records (every copy of a key in
- * one bucket), then one workgroup per bucket sums the df of equal keys in an LDS table of
- * record indices (claim = a 32-bit CAS of the index: the key itself is already in memory,
- * so no pending state) and answers each record.  Sequential passes over the records
- * instead of random probes into a table of 1.5x the records in HBM (c4 at 8 shards: 128 MB
- * of keys per owner) and no table clears. */
-constexpr uint32_t XB_MEAN = 1024;   /* mean records per bucket */
-constexpr uint32_t XB_T = 4096;      /* LDS slots of the largest table (4x the mean; a bucket's table is
+/* ---- the owner's aggregation, bucketed: the received records are grouped by the top bits
+ * of their key hash into buckets of ~XB_MEAN records (every copy of a key in one bucket), then
+ * one workgroup per bucket sums the df of equal keys in an LDS table and answers each record.
+ * The grouping is an LSD radix sort of (bucket, record index) pairs (prims.hip: LDS-staged,
+ * each tile's runs stored contiguously; 2 digit passes up to 2^16 buckets), not a scatter of
+ * the records: round 4's per-record returning atomic for the bucket rank and its scattered
+ * 24-byte stores (c4 at 8 shards: 1.2 ms of the owner's 2.1 ms) are gone, and the bucket
+ * workgroups read the records in place through the sorted indices. */
+constexpr uint32_t XB_MEAN = 512;    /* mean records per bucket (at most) */
+constexpr uint32_t XB_T = 2048;      /* LDS slots of the largest table (4x the mean; a bucket's table is
                                         the power of two >= 2x its records, cleared per bucket) */
-constexpr uint32_t XB_CS = 32;       /* bucket counters 128 bytes apart: the count pass's atomics
-                                        spread over as many L2 lines as buckets */
-constexpr uint32_t XB_SCAN_NT = 1024;
 /* bucket = the top bits of a 64-bit mix (key_hash is 32-bit; its low bits pick the LDS slot),
  * independent of owner_of's mix */
 __device__ __forceinline__ uint64_t xb_hash(const uint32_t* r) {
     const uint64_t lo = ((uint64_t)r[1] << 32) | r[0], hi = ((uint64_t)r[3] << 32) | r[2];
     return mix64(hi ^ (lo * 0xD6E8FEB86659FD93ull) ^ 0x2545F4914F6CDD1Dull);
 }
-/* rank[i] = the record's place in its bucket; cnt[b] = the bucket's records */
-__global__ void k_xb_count(const uint32_t* __restrict__ rrec, uint64_t n, uint32_t shift, uint32_t* __restrict__ cnt,
-                           uint32_t* __restrict__ rank) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) rank[i] = atomicAdd(&cnt[(uint32_t)(xb_hash(rrec + 5 * i) >> shift) * XB_CS], 1u);
-}
-/* exclusive scan of nb counts in place, one workgroup; off[nb] = total */
-__global__ void __launch_bounds__(XB_SCAN_NT) k_xb_scan(uint32_t* __restrict__ off, uint32_t nb) {
-    __shared__ uint32_t ws[XB_SCAN_NT / 64];
-    const uint32_t per = (nb + XB_SCAN_NT - 1) / XB_SCAN_NT, a = threadIdx.x * per, e = a + per < nb ? a + per : nb;
-    uint32_t t = 0;
-    for (uint32_t b = a; b < e; ++b) t += off[b * XB_CS];
-    /* exclusive scan of the per-thread totals */
-    uint32_t inc = t;
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(inc, d, 64);
-        if ((threadIdx.x & 63) >= (uint32_t)d) inc += y;
-    }
-    if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = inc;
-    __syncthreads();
-    uint32_t base = 0;
-    for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) base += ws[w];
-    uint32_t acc = base + inc - t;
-    for (uint32_t b = a; b < e; ++b) {
-        const uint32_t c = off[b * XB_CS];
-        off[b * XB_CS] = acc;
-        acc += c;
-    }
-    if (threadIdx.x == XB_SCAN_NT - 1) off[nb * XB_CS] = acc;
-}
-__global__ void k_xb_scatter(const uint32_t* __restrict__ rrec, uint64_t n, uint32_t shift, const uint32_t* __restrict__ off,
-                             const uint32_t* __restrict__ rank, uint4* __restrict__ bkey, uint32_t* __restrict__ bdf,
-                             uint32_t* __restrict__ bidx) {
+/* (bucket, record index) pairs, the radix sort's input */
+__global__ void k_xb_keys(const uint32_t* __restrict__ rrec, uint64_t n, uint32_t shift, uint64_t* __restrict__ key,
+                          uint32_t* __restrict__ idx) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const uint32_t* r = rrec + 5 * i;
-    const uint32_t p = off[(uint32_t)(xb_hash(r) >> shift) * XB_CS] + rank[i];
-    bkey[p] = make_uint4(r[0], r[1], r[2], r[3]);
-    bdf[p] = r[4];
-    bidx[p] = (uint32_t)i;
+    key[i] = xb_hash(rrec + 5 * i) >> shift;
+    idx[i] = (uint32_t)i;
 }
-/* one workgroup per bucket (grid-stride over buckets): LDS slot -> the bucket's first
- * record of the key + the summed df; then every record answered (reply[i + sender]) */
-__global__ void __launch_bounds__(NT) k_xb_bucket(const uint4* __restrict__ bkey, const uint32_t* __restrict__ bdf,
-                                                  const uint32_t* __restrict__ bidx, const uint32_t* __restrict__ off,
-                                                  uint32_t nb, const uint32_t* __restrict__ roff, uint32_t R,
-                                                  uint32_t* __restrict__ reply, unsigned long long* __restrict__ used,
-                                                  uint32_t* __restrict__ status) {
+/* off[b] = the first sorted position of bucket b (off[nb] = n) from the sorted bucket ids */
+__global__ void k_xb_bounds(const uint64_t* __restrict__ key, uint64_t n, uint32_t nb, uint32_t* __restrict__ off) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t b = (uint32_t)key[p];
+    const uint32_t prev = p ? (uint32_t)key[p - 1] : 0xFFFFFFFFu;
+    for (uint32_t q = prev + 1; q <= b; ++q) off[q] = (uint32_t)p;   /* prev + 1 wraps to 0 at p = 0 */
+    if (p == n - 1)
+        for (uint32_t q = b + 1; q <= nb; ++q) off[q] = (uint32_t)n;
+}
+__device__ __forceinline__ uint4 xb_key_at(const uint32_t* __restrict__ rrec, uint32_t i) {
+    const uint32_t* r = rrec + 5ull * i;
+    return make_uint4(r[0], r[1], r[2], r[3]);
+}
+/* one workgroup per bucket (grid-stride over buckets).  Each thread loads its records (up to
+ * XB_PER: index, key, df) once, in independent loads, and keeps them in registers; the keys
+ * are also staged in LDS, so the find-or-claim probes compare keys without waiting on
+ * memory: LDS slot -> the bucket-local index of the key's first copy + the summed df, and
+ * each record is answered from the slot it found (reply[i + sender]).  A bucket of more
+ * than XB_MAXREC records (not expected: the mean is <= XB_MEAN) takes the same steps with
+ * the keys compared in memory. */
+constexpr uint32_t XB_NT = 256;
+constexpr uint32_t XB_MAXREC = 1024;
+constexpr uint32_t XB_PER = XB_MAXREC / XB_NT;
+__device__ __forceinline__ uint32_t xb_seg(const uint32_t* sroff, const uint32_t* __restrict__ roff, uint32_t R,
+                                           uint32_t i) {
+    uint32_t lo = 0, hi = R;
+    if (R <= XO_MAXR) {
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (sroff[mid] <= i) lo = mid; else hi = mid;
+        }
+        return lo;
+    }
+    return seg_of(roff, R, i);
+}
+__device__ __forceinline__ bool xb_eq(const uint4& a, const uint4& b) {
+    return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
+}
+__device__ __forceinline__ uint32_t xb_home(const uint4& k, uint32_t tm) {
+    return (uint32_t)key_hash(((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z) & tm;
+}
+__global__ void __launch_bounds__(XB_NT) k_xb_bucket(const uint32_t* __restrict__ rrec, const uint32_t* __restrict__ sidx,
+                                                     const uint32_t* __restrict__ off, uint32_t nb,
+                                                     const uint32_t* __restrict__ roff, uint32_t R,
+                                                     uint32_t* __restrict__ reply, unsigned long long* __restrict__ used,
+                                                     uint32_t* __restrict__ status) {
+    __shared__ uint4 skey[XB_MAXREC];
     __shared__ uint32_t tix[XB_T], tdf[XB_T];
+    __shared__ uint32_t sroff[XO_MAXR + 1];
+    for (uint32_t p = threadIdx.x; p <= R && p <= XO_MAXR; p += XB_NT) sroff[p] = roff[p];
+    uint32_t claims = 0;
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
-        const uint32_t b0 = off[b * XB_CS], nrec = off[(b + 1) * XB_CS] - b0;
+        const uint32_t b0 = off[b], nrec = off[b + 1] - b0;
         uint32_t T = 256;
         while (T < 2 * nrec && T < XB_T) T *= 2;
         const uint32_t tm = T - 1;
-        for (uint32_t t = threadIdx.x; t < T; t += NT) { tix[t] = 0xFFFFFFFFu; tdf[t] = 0; }
-        __syncthreads();
-        uint32_t claims = 0;
-        for (uint32_t j0 = 0; j0 < nrec; j0 += NT) {   /* find-or-claim, df added */
-            const uint32_t j = j0 + threadIdx.x;
-            if (j < nrec) {
-                const uint4 k = bkey[b0 + j];
-                uint32_t h = (uint32_t)key_hash(((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z) & tm;
-                uint32_t probe = 0;
+        for (uint32_t t = threadIdx.x; t < T; t += XB_NT) { tix[t] = 0xFFFFFFFFu; tdf[t] = 0; }
+        if (nrec <= XB_MAXREC) {
+            uint32_t ii[XB_PER], dd[XB_PER], hh[XB_PER];
+            uint4 kk[XB_PER];
+#pragma unroll
+            for (uint32_t q = 0; q < XB_PER; ++q) {
+                const uint32_t j = threadIdx.x + q * XB_NT;
+                ii[q] = j < nrec ? sidx[b0 + j] : 0u;
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < XB_PER; ++q) {
+                const uint32_t j = threadIdx.x + q * XB_NT;
+                if (j < nrec) {
+                    kk[q] = xb_key_at(rrec, ii[q]);
+                    dd[q] = rrec[5ull * ii[q] + 4];
+                    skey[j] = kk[q];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (uint32_t q = 0; q < XB_PER; ++q) {   /* find-or-claim, df added */
+                const uint32_t j = threadIdx.x + q * XB_NT;
+                hh[q] = 0xFFFFFFFFu;
+                if (j >= nrec) continue;
+                uint32_t h = xb_home(kk[q], tm);
+                for (uint32_t probe = 0; probe < T; ++probe, h = (h + 1) & tm) {
+                    uint32_t x = tix[h];
+                    if (x == 0xFFFFFFFFu) {
+                        x = atomicCAS(&tix[h], 0xFFFFFFFFu, j);
+                        if (x == 0xFFFFFFFFu) { ++claims; hh[q] = h; break; }
+                    }
+                    if (xb_eq(skey[x], kk[q])) { hh[q] = h; break; }
+                }
+                if (hh[q] != 0xFFFFFFFFu) atomicAdd(&tdf[hh[q]], dd[q]);
+                else atomicOr(status, ST_BOUNDS);   /* more distinct keys than slots in one bucket */
+            }
+            __syncthreads();
+#pragma unroll
+            for (uint32_t q = 0; q < XB_PER; ++q) {   /* the answers */
+                const uint32_t j = threadIdx.x + q * XB_NT;
+                if (j < nrec) reply[ii[q] + xb_seg(sroff, roff, R, ii[q])] = hh[q] != 0xFFFFFFFFu ? tdf[hh[q]] : 0u;
+            }
+        } else {
+            __syncthreads();
+            for (uint32_t j0 = 0; j0 < nrec; j0 += XB_NT) {   /* find-or-claim, df added */
+                const uint32_t j = j0 + threadIdx.x;
+                if (j >= nrec) continue;
+                const uint32_t i = sidx[b0 + j];
+                const uint4 k = xb_key_at(rrec, i);
+                uint32_t h = xb_home(k, tm), probe = 0;
                 for (; probe < T; ++probe, h = (h + 1) & tm) {
                     uint32_t x = tix[h];
                     if (x == 0xFFFFFFFFu) {
                         x = atomicCAS(&tix[h], 0xFFFFFFFFu, j);
                         if (x == 0xFFFFFFFFu) { ++claims; break; }
                     }
-                    const uint4 o = bkey[b0 + x];
-                    if (o.x == k.x && o.y == k.y && o.z == k.z && o.w == k.w) break;
+                    if (xb_eq(xb_key_at(rrec, sidx[b0 + x]), k)) break;
                 }
-                if (probe < T) atomicAdd(&tdf[h], bdf[b0 + j]);
-                else atomicOr(status, ST_BOUNDS);   /* more distinct keys than slots in one bucket */
+                if (probe < T) atomicAdd(&tdf[h], rrec[5ull * i + 4]);
+                else atomicOr(status, ST_BOUNDS);
             }
-        }
-        __syncthreads();
-        for (uint32_t j0 = 0; j0 < nrec; j0 += NT) {   /* the answers */
-            const uint32_t j = j0 + threadIdx.x;
-            if (j < nrec) {
-                const uint4 k = bkey[b0 + j];
-                uint32_t h = (uint32_t)key_hash(((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z) & tm;
-                uint32_t d = 0;
+            __syncthreads();
+            for (uint32_t j0 = 0; j0 < nrec; j0 += XB_NT) {   /* the answers */
+                const uint32_t j = j0 + threadIdx.x;
+                if (j >= nrec) continue;
+                const uint32_t i = sidx[b0 + j];
+                const uint4 k = xb_key_at(rrec, i);
+                uint32_t h = xb_home(k, tm), d = 0;
                 for (uint32_t probe = 0; probe < T; ++probe, h = (h + 1) & tm) {
                     const uint32_t x = tix[h];
                     if (x == 0xFFFFFFFFu) break;
-                    const uint4 o = bkey[b0 + x];
-                    if (o.x == k.x && o.y == k.y && o.z == k.z && o.w == k.w) { d = tdf[h]; break; }
+                    if (xb_eq(xb_key_at(rrec, sidx[b0 + x]), k)) { d = tdf[h]; break; }
                 }
-                const uint32_t i = bidx[b0 + j];
-                reply[i + seg_of(roff, R, i)] = d;
+                reply[i + xb_seg(sroff, roff, R, i)] = d;
             }
         }
-        const uint32_t c = wave_sum(claims);
-        if ((threadIdx.x & 63) == 0 && c) atomicAdd(used, (unsigned long long)c);
         __syncthreads();   /* the table is cleared for the next bucket only after every lookup */
     }
+    const uint32_t c = wave_sum(claims);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(used, (unsigned long long)c);
 }
 __global__ void k_xb_trailer(const uint32_t* __restrict__ roff, uint32_t R, const unsigned long long* __restrict__ used,
                              uint32_t* __restrict__ reply) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p < R) reply[(uint64_t)roff[p + 1] + p] = (uint32_t)*used;
 }
-/* scratch: bkey n x 16 B + bdf, rank n x 4 B (keys), bidx n x 4 B, cnt nb + 1 words */
-uint32_t owner_buckets(uint64_t n) {   /* >= 2: the bucket is hash >> (64 - lg), lg >= 1 */
+static uint32_t owner_buckets(uint64_t n) {   /* >= 2: the bucket is hash >> (64 - lg), lg >= 1 */
     uint32_t nb = 2;
     while ((uint64_t)nb * XB_MEAN < n && nb < (1u << 24)) nb *= 2;
     return nb;
 }
-int launch_owner_aggregate_buckets(const uint32_t* rrec, uint64_t n, const uint32_t* roff, uint32_t R, uint4* bkey,
-                                   uint32_t* bdf, uint32_t* rank, uint32_t* bidx, uint32_t* cnt, uint32_t* reply,
-                                   unsigned long long* used, uint32_t* status, hipStream_t s) {
+static size_t xb_al(size_t b) { return (b + 255) & ~(size_t)255; }
+size_t owner_bucket_scratch(uint64_t n) {
+    /* sort keys 2 x 8n, indices 2 x 4n, bucket offsets, the sort's histograms + scan scratch */
+    return 2 * xb_al(n * 8 + 8) + 2 * xb_al(n * 4 + 4) + xb_al(((size_t)owner_buckets(n) + 1) * 4) + n / 2 + (2u << 20);
+}
+int launch_owner_aggregate_buckets(const uint32_t* rrec, uint64_t n, const uint32_t* roff, uint32_t R, void* scratch,
+                                   size_t scratch_bytes, uint32_t* reply, unsigned long long* used, uint32_t* status,
+                                   hipStream_t s) {
     const uint32_t nb = owner_buckets(n);
     uint32_t lg = 0;
     while ((1u << lg) < nb) ++lg;
     const uint32_t shift = 64 - lg;
-    if (hipMemsetAsync(used, 0, 8, s) != hipSuccess || hipMemsetAsync(cnt, 0, ((size_t)nb + 1) * XB_CS * 4, s) != hipSuccess)
-        return -1;
+    if (hipMemsetAsync(used, 0, 8, s) != hipSuccess) return -1;
     if (n) {
         if (n >= 0xFFFFFFFFull) return -2;
+        if (scratch_bytes < owner_bucket_scratch(n)) return -2;
+        uint8_t* p = (uint8_t*)scratch;
+        uint64_t* k0 = (uint64_t*)p;  p += xb_al(n * 8 + 8);
+        uint64_t* k1 = (uint64_t*)p;  p += xb_al(n * 8 + 8);
+        uint32_t* v0 = (uint32_t*)p;  p += xb_al(n * 4 + 4);
+        uint32_t* v1 = (uint32_t*)p;  p += xb_al(n * 4 + 4);
+        uint32_t* off = (uint32_t*)p; p += xb_al(((size_t)nb + 1) * 4);
+        Arena ar;
+        ar.base = p;
+        ar.cap = scratch_bytes - (size_t)(p - (uint8_t*)scratch);
         const unsigned g = (unsigned)((n + NT - 1) / NT);
-        k_xb_count<<<g, NT, 0, s>>>(rrec, n, shift, cnt, rank);
-        k_xb_scan<<<1, XB_SCAN_NT, 0, s>>>(cnt, nb);
-        k_xb_scatter<<<g, NT, 0, s>>>(rrec, n, shift, cnt, rank, bkey, bdf, bidx);
-        k_xb_bucket<<<nb < 8192 ? nb : 8192, NT, 0, s>>>(bkey, bdf, bidx, cnt, nb, roff, R, reply, used, status);
+        k_xb_keys<<<g, NT, 0, s>>>(rrec, n, shift, k0, v0);
+        const uint32_t mask = lg <= 8 ? 0x1u : lg <= 16 ? 0x3u : 0x7u;
+        const int cur = radix_sort_u64(k0, v0, k1, v1, n, mask, ar, s);
+        if (cur < 0) return cur == -2 ? -2 : -1;
+        const uint64_t* ks = cur ? k1 : k0;
+        const uint32_t* vs = cur ? v1 : v0;
+        k_xb_bounds<<<g, NT, 0, s>>>(ks, n, nb, off);
+        k_xb_bucket<<<nb < 8192 ? nb : 8192, XB_NT, 0, s>>>(rrec, vs, off, nb, roff, R, reply, used, status);
     }
     k_xb_trailer<<<(R + NT - 1) / NT, NT, 0, s>>>(roff, R, used, reply);
     return ok();

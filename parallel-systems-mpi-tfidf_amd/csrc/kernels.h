@@ -215,12 +215,13 @@ int launch_owner_offsets(const uint32_t* m, uint32_t R, uint32_t me, uint32_t* s
 int launch_owner_aggregate(const uint32_t* rrec, uint64_t n, const uint32_t* roff, uint32_t R, uint4* tkey, uint64_t tcap,
                            uint32_t* tdf, uint32_t* rslot, uint32_t* reply, unsigned long long* used, uint32_t* status,
                            hipStream_t s);
-/* the same, bucketed: records partitioned by key hash into owner_buckets(n) buckets, each
- * aggregated in LDS (scratch: bkey n x 16 B; bdf, rank, bidx n x 4 B; cnt (nb + 1) x 128 B) */
-uint32_t owner_buckets(uint64_t n);
-int launch_owner_aggregate_buckets(const uint32_t* rrec, uint64_t n, const uint32_t* roff, uint32_t R, uint4* bkey,
-                                   uint32_t* bdf, uint32_t* rank, uint32_t* bidx, uint32_t* cnt, uint32_t* reply,
-                                   unsigned long long* used, uint32_t* status, hipStream_t s);
+/* the same, bucketed: records grouped by key hash into buckets of <= 512 on average (a radix sort of
+ * (bucket, record index) pairs), each bucket aggregated in LDS; scratch of
+ * owner_bucket_scratch(n) bytes */
+size_t owner_bucket_scratch(uint64_t n);
+int launch_owner_aggregate_buckets(const uint32_t* rrec, uint64_t n, const uint32_t* roff, uint32_t R, void* scratch,
+                                   size_t scratch_bytes, uint32_t* reply, unsigned long long* used, uint32_t* status,
+                                   hipStream_t s);
 int launch_owner_back(const uint32_t* back, const uint32_t* soff, uint32_t R, const uint32_t* sidx, uint32_t V,
                       uint32_t* df_global, uint32_t* vg, hipStream_t s);
 /* out[i] = sum of rows[r * n + i] over r < nrows (the in-process transport's all-reduce) */
