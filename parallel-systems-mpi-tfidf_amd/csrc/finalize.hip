@@ -717,13 +717,17 @@ __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ r
     const uint64_t r0 = (uint64_t)blockIdx.x * per;
     const uint64_t r1 = r0 + per < nrec ? r0 + per : nrec;
     for (uint64_t i = r0 + threadIdx.x; i < r1; i += (uint64_t)DFH_B * DFH_NT) {
-        uint32_t sl[DFH_B], r[DFH_B];
+        uint32_t sl[DFH_B], r[DFH_B], g[DFH_B];
 #pragma unroll
         for (int q = 0; q < DFH_B; ++q) {
             const uint64_t k = i + (uint64_t)q * DFH_NT;
             sl[q] = k < r1 ? __builtin_nontemporal_load(&rec_slot[k]) : 0xFFFFFFFFu;
         }
-        uint32_t miss = 0;   /* bit q: record q's rank came from global memory */
+        /* classify without branches around loads: every lane reads its cache entry; a
+         * miss's rank gather is one unconditional load per record (lanes that need none
+         * read entry 0), all DFH_B of them in flight before the first is used (a gather
+         * inside the miss branch made the compiler wait for each before the next) */
+        uint32_t miss = 0;   /* bit q: record q's rank comes from global memory */
 #pragma unroll
         for (int q = 0; q < DFH_B; ++q) {
             const bool ranked = i + (uint64_t)q * DFH_NT >= ranked_from;   /* merged records hold ranks */
@@ -731,15 +735,26 @@ __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ r
                 atomicOr(status, ST_BOUNDS);
                 sl[q] = 0xFFFFFFFFu;
             }
-            if (sl[q] == 0xFFFFFFFFu || ranked) { r[q] = ranked ? sl[q] : 0u; continue; }
             const unsigned long long e = cache[dfh_cslot(sl[q])];
-            if ((uint32_t)(e >> 32) == sl[q] + 1u) { r[q] = (uint32_t)e; continue; }
-            miss |= 1u << q;
-            r[q] = rank16 ? (uint32_t)rank16[sl[q]] : rank_of_slot[sl[q]];
+            const bool hit = (uint32_t)(e >> 32) == sl[q] + 1u;
+            const bool need = sl[q] != 0xFFFFFFFFu && !ranked && !hit;
+            miss |= need ? 1u << q : 0u;
+            r[q] = ranked ? sl[q] : (uint32_t)e;
+        }
+        if (rank16) {
+#pragma unroll
+            for (int q = 0; q < DFH_B; ++q) g[q] = rank16[((miss >> q) & 1u) ? sl[q] : 0u];
+        } else {
+#pragma unroll
+            for (int q = 0; q < DFH_B; ++q) g[q] = rank_of_slot[((miss >> q) & 1u) ? sl[q] : 0u];
         }
 #pragma unroll
-        for (int q = 0; q < DFH_B; ++q)
-            if ((miss >> q) & 1u) cache[dfh_cslot(sl[q])] = ((unsigned long long)(sl[q] + 1u) << 32) | r[q];
+        for (int q = 0; q < DFH_B; ++q) {
+            if ((miss >> q) & 1u) {
+                r[q] = g[q];
+                cache[dfh_cslot(sl[q])] = ((unsigned long long)(sl[q] + 1u) << 32) | r[q];
+            }
+        }
 #pragma unroll
         for (int q = 0; q < DFH_B; ++q) {
             if (sl[q] == 0xFFFFFFFFu) continue;
