@@ -239,6 +239,9 @@ struct tfidf_ctx {
     hipError_t last_err = hipSuccess;
 };
 static void idf_pool_stop(tfidf_ctx* ctx);   /* the per-run idf table's workers (idf_start) */
+/* open contexts in this process: the idf workers of all of them share IDF_POOL threads' worth
+ * of work (a group of K shards in one process would otherwise start 8 K of them) */
+static std::atomic<int> g_live_ctx{0};
 
 #define HIPCHK(x)                                                                          \
     do {                                                                                   \
@@ -360,6 +363,7 @@ int tfidf_open(int device, tfidf_ctx** out) {
     if (hipHostMalloc((void**)&ctx->hpin, 256, hipHostMallocDefault) != hipSuccess) { delete ctx; return TFIDF_E_NOMEM; }
     if (hipHostMalloc((void**)&ctx->k1out_host, sizeof(K1Out), hipHostMallocDefault) != hipSuccess ||
         ctx->k1out_dev.ensure(sizeof(K1Out)) != 0) { delete ctx; return TFIDF_E_NOMEM; }
+    g_live_ctx.fetch_add(1);
     *out = ctx;
     return TFIDF_OK;
 }
@@ -373,6 +377,7 @@ void tfidf_close(tfidf_ctx* ctx) {
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_order) (void)hipEventDestroy(ctx->ev_order);
     idf_pool_stop(ctx);
+    g_live_ctx.fetch_sub(1);
     if (ctx->ev_idf) { (void)hipEventSynchronize(ctx->ev_idf); (void)hipEventDestroy(ctx->ev_idf); }
     if (ctx->idf_pin) (void)hipHostFree(ctx->idf_pin);
     for (int i = 0; i < WR_NBUF; ++i) {
@@ -1064,8 +1069,8 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
 
 /* ---- the per-run idf table: log(N/df) for every df = 0..N on the host's libm
  * (TFIDF.c:243 evaluates log(1.0*N/df) per pair; the table holds the same doubles), on up to
- * eight host threads started when the run starts, so the logs run beside K1 .. DF on the
- * device.  run_post waits for them (ms_idf_wait: normally 0) and uploads the table. */
+ * eight host threads per process (shared out over its open contexts) posted when the run
+ * starts, so the logs run beside K1 .. DF on the device.  run_post waits for them (ms_idf_wait: normally 0) and uploads the table. */
 #define IDF_POOL 8
 static void idf_worker(tfidf_ctx::IdfPool* P, unsigned i) {
     uint64_t seen = 0;
@@ -1104,11 +1109,13 @@ static void idf_pool_stop(tfidf_ctx* ctx) {
 /* posts a table job to the context's workers (lut: n values; vals null = every df 1..n) */
 static void idf_post(tfidf_ctx* ctx, double* lut, uint64_t Nt, const uint32_t* vals, uint64_t n) {
     tfidf_ctx::IdfPool& P = ctx->idf_pool;
-    if (P.th.empty())
-        for (unsigned i = 0; i < IDF_POOL; ++i) P.th.emplace_back(idf_worker, &P, i);
+    const int live = g_live_ctx.load();
+    const unsigned share = live > 1 ? (unsigned)(IDF_POOL / live > 1 ? IDF_POOL / live : 1) : IDF_POOL;
+    const unsigned want = (unsigned)(n / 16384 < 1 ? 1 : (n / 16384 > share ? share : n / 16384));
+    while (P.th.size() < want) P.th.emplace_back(idf_worker, &P, (unsigned)P.th.size());   /* started once, as needed */
     {
         std::lock_guard<std::mutex> lk(P.mu);
-        P.active = (unsigned)(n / 16384 < 1 ? 1 : (n / 16384 > IDF_POOL ? IDF_POOL : n / 16384));
+        P.active = want;
         P.left = P.active;
         P.lut = lut;
         P.Nt = Nt;
