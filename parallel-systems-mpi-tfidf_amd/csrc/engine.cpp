@@ -263,9 +263,22 @@ static std::atomic<int> g_live_ctx{0};
             HIPCHK(hipStreamSynchronize(s_));                                              \
         }                                                                                  \
     } while (0)
+/* TFIDF_DEBUG_ALLOC=1: every (re)allocation of a stage buffer is named on stderr (which
+ * buffer still grows after the warm-up runs) */
+static int debug_alloc() {
+    static const int on = [] { const char* e = getenv("TFIDF_DEBUG_ALLOC"); return e && e[0] == '1'; }();
+    return on;
+}
+static int ensure_named(DevBuf& b, size_t bytes, const char* name) {
+    const void* p0 = b.p;
+    const int rc = b.ensure(bytes);
+    if (debug_alloc() && (b.p != p0 || rc))
+        fprintf(stderr, "tfidf: alloc %s %zu bytes (asked %zu)%s\n", name, b.cap, bytes, rc ? " FAILED" : "");
+    return rc;
+}
 #define ENSURE(buf, bytes)                                   \
     do {                                                     \
-        if ((buf).ensure((size_t)(bytes)) != 0) return TFIDF_E_NOMEM; \
+        if (ensure_named((buf), (size_t)(bytes), #buf) != 0) return TFIDF_E_NOMEM; \
     } while (0)
 #define LCHK(x)                                              \
     do {                                                     \
@@ -956,12 +969,20 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     mark(ctx, S_MERGE);
     uint64_t R_total = R_main;
     const uint32_t* merged_count = nullptr;   /* device: merged + dense records beyond R_main */
+    {
+        /* Q follows K1's overflow records, which vary from run to run (the order of the LDS
+         * claims): at least 2^20 entries (28 MB in all), also when this run has none, so that
+         * a shard with few or no partial records does not allocate in steady state (c5 at 8
+         * shards: 0 -> 28 K -> 90 K, ten device allocations in its timed steps,
+         * TFIDF_DEBUG_ALLOC=1) */
+        const uint64_t Qc = Q < (1ull << 20) ? (1ull << 20) : Q;
+        ENSURE(ctx->pkey0, Qc * 8);
+        ENSURE(ctx->pkey1, Qc * 8);
+        ENSURE(ctx->pseq0, Qc * 4);
+        ENSURE(ctx->pseq1, Qc * 4);
+        ENSURE(ctx->phead, (Qc + 1) * 4);
+    }
     if (Q) {
-        ENSURE(ctx->pkey0, Q * 8);
-        ENSURE(ctx->pkey1, Q * 8);
-        ENSURE(ctx->pseq0, Q * 4);
-        ENSURE(ctx->pseq1, Q * 4);
-        ENSURE(ctx->phead, (Q + 1) * 4);
         /* merged (and dense) records land in [R_main, R_main + Q): size for the worst case */
         if (R_main + Q > ctx->rec_cap) {
             uint64_t ncap = R_main + Q + (R_main + Q) / 8 + 4096;
@@ -1238,8 +1259,14 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
             ctx->idf_pin_n = (size_t)K + 1;
         }
         if (K) {
-            idf_post(ctx, ctx->idf_pin, Nt, vals.data(), K);
-            idf_join(ctx);
+            if (K < 2 * 16384) {   /* one worker's share: on this thread, no hand-off and wake-up */
+                const auto t0 = std::chrono::steady_clock::now();
+                for (uint32_t k = 0; k < K; ++k) ctx->idf_pin[k] = log(1.0 * (double)Nt / (double)vals[k]);
+                ctx->ms_idf_host = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            } else {
+                idf_post(ctx, ctx->idf_pin, Nt, vals.data(), K);
+                idf_join(ctx);
+            }
             HIPCHK(hipMemcpyAsync(ctx->idf_vals.p, ctx->idf_pin, (size_t)K * 8, hipMemcpyHostToDevice, s));
             HIPCHK(hipEventRecord(ctx->ev_idf, s));
         }
