@@ -204,8 +204,9 @@ struct tfidf_ctx {
     int xchg_mode = 0;      /* env TFIDF_XCHG: 0 auto (dense up to DENSE_XCHG_MAXV terms per rank), 1 owner, 2 dense,
                                3 dense with table numbering */
     bool last_dense = false;   /* the last exchange used the dense form */
-    bool local_long = false;
-    bool xagg_table = false;   /* env TFIDF_XAGG=table: the owner aggregates in an HBM table (A/B) */   /* this rank's vocabulary holds terms of >= 16 bytes (K1 status) */
+    bool local_long = false;   /* this rank's vocabulary holds terms of >= 16 bytes (K1 status) */
+    bool xagg_table = false;   /* env TFIDF_XAGG=table: the owner aggregates in an HBM table (A/B) */
+    uint32_t xb_stage_max = ~0u;   /* env TFIDF_XB_STAGE_MAX (tests): the owner's largest bucket staged in LDS */
     /* sizes the local part of a run hands to the exchange and the stages after it */
     uint32_t run_N = 0, run_V = 0;
     uint64_t run_cap = 0, run_R_total = 0;
@@ -341,6 +342,8 @@ int tfidf_open(int device, tfidf_ctx** out) {
     if (kxm && !strcmp(kxm, "dense_table")) ctx->xchg_mode = 3;
     const char* kxa = getenv("TFIDF_XAGG");
     ctx->xagg_table = kxa && !strcmp(kxa, "table");
+    const char* kxb = getenv("TFIDF_XB_STAGE_MAX");
+    ctx->xb_stage_max = kxb ? (uint32_t)atoi(kxb) : ~0u;
     const char* kn = getenv("TFIDF_TEST_XNOMEM_RANK");
     ctx->xnomem_rank = kn ? atoi(kn) : -1;
     /* diagnostics: initial vocabulary capacity (power of two) and the loads it may reach
@@ -619,7 +622,8 @@ static int exchange_owner(tfidf_ctx* ctx, uint32_t V, const std::vector<uint64_t
                                     ctx->x_reply.as<uint32_t>(), used, (uint32_t*)(cnt + 3), s));
     } else {   /* bucketed: x_tkey is its scratch */
         XCHK(launch_owner_aggregate_buckets(ctx->x_rrec.as<uint32_t>(), nrecv, roff, (uint32_t)R, ctx->x_tkey.p,
-                                            ctx->x_tkey.cap, ctx->x_reply.as<uint32_t>(), used, (uint32_t*)(cnt + 3), s));
+                                            ctx->x_tkey.cap, ctx->x_reply.as<uint32_t>(), used, (uint32_t*)(cnt + 3),
+                                            ctx->xb_stage_max, s));
     }
     rc = xp->alltoallv(ctx->x_reply.p, rcnt1.data(), ctx->x_back.p, scnt1.data(), 4, s);
     if (rc) return rc;

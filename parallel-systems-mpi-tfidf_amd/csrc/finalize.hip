@@ -2365,7 +2365,7 @@ __global__ void __launch_bounds__(XB_NT) k_xb_bucket(const uint32_t* __restrict_
                                                      const uint32_t* __restrict__ off, uint32_t nb,
                                                      const uint32_t* __restrict__ roff, uint32_t R,
                                                      uint32_t* __restrict__ reply, unsigned long long* __restrict__ used,
-                                                     uint32_t* __restrict__ status) {
+                                                     uint32_t* __restrict__ status, uint32_t stage_max) {
     __shared__ uint4 skey[XB_MAXREC];
     __shared__ uint32_t tix[XB_T], tdf[XB_T];
     __shared__ uint32_t sroff[XO_MAXR + 1];
@@ -2377,7 +2377,7 @@ __global__ void __launch_bounds__(XB_NT) k_xb_bucket(const uint32_t* __restrict_
         while (T < 2 * nrec && T < XB_T) T *= 2;
         const uint32_t tm = T - 1;
         for (uint32_t t = threadIdx.x; t < T; t += XB_NT) { tix[t] = 0xFFFFFFFFu; tdf[t] = 0; }
-        if (nrec <= XB_MAXREC) {
+        if (nrec <= stage_max) {
             uint32_t ii[XB_PER], dd[XB_PER], hh[XB_PER];
             uint4 kk[XB_PER];
 #pragma unroll
@@ -2474,7 +2474,10 @@ size_t owner_bucket_scratch(uint64_t n) {
 }
 int launch_owner_aggregate_buckets(const uint32_t* rrec, uint64_t n, const uint32_t* roff, uint32_t R, void* scratch,
                                    size_t scratch_bytes, uint32_t* reply, unsigned long long* used, uint32_t* status,
-                                   hipStream_t s) {
+                                   uint32_t stage_max, hipStream_t s) {
+    /* stage_max: buckets of up to this many records (<= XB_MAXREC) are staged in LDS; the
+     * tests set 0 so that every bucket takes the path that compares keys in memory */
+    if (stage_max > XB_MAXREC) stage_max = XB_MAXREC;
     const uint32_t nb = owner_buckets(n);
     uint32_t lg = 0;
     while ((1u << lg) < nb) ++lg;
@@ -2500,7 +2503,7 @@ int launch_owner_aggregate_buckets(const uint32_t* rrec, uint64_t n, const uint3
         const uint64_t* ks = cur ? k1 : k0;
         const uint32_t* vs = cur ? v1 : v0;
         k_xb_bounds<<<g, NT, 0, s>>>(ks, n, nb, off);
-        k_xb_bucket<<<nb < 8192 ? nb : 8192, XB_NT, 0, s>>>(rrec, vs, off, nb, roff, R, reply, used, status);
+        k_xb_bucket<<<nb < 8192 ? nb : 8192, XB_NT, 0, s>>>(rrec, vs, off, nb, roff, R, reply, used, status, stage_max);
     }
     k_xb_trailer<<<(R + NT - 1) / NT, NT, 0, s>>>(roff, R, used, reply);
     return ok();

@@ -221,7 +221,7 @@ int launch_owner_aggregate(const uint32_t* rrec, uint64_t n, const uint32_t* rof
 size_t owner_bucket_scratch(uint64_t n);
 int launch_owner_aggregate_buckets(const uint32_t* rrec, uint64_t n, const uint32_t* roff, uint32_t R, void* scratch,
                                    size_t scratch_bytes, uint32_t* reply, unsigned long long* used, uint32_t* status,
-                                   hipStream_t s);
+                                   uint32_t stage_max, hipStream_t s);
 int launch_owner_back(const uint32_t* back, const uint32_t* soff, uint32_t R, const uint32_t* sidx, uint32_t V,
                       uint32_t* df_global, uint32_t* vg, hipStream_t s);
 /* out[i] = sum of rows[r * n + i] over r < nrows (the in-process transport's all-reduce) */

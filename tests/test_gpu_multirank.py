@@ -88,6 +88,21 @@ def test_group_shards_equal_single_rank_oracle(cfg, scale, K, xchg, monkeypatch)
     assert len({i["nterms"] for i in infos}) > 1
 
 
+@pytest.mark.parametrize("cfg,scale,K", [("c4", 0.01, 4), ("c2", 0.003, 3)])
+def test_owner_buckets_compared_in_memory(cfg, scale, K, monkeypatch):
+    """The owner form's path for a bucket too large to stage in LDS (more than 1024 records:
+    not expected at a mean of <= 512, so TFIDF_XB_STAGE_MAX=0 sends every bucket there):
+    keys compared in memory (finalize.hip k_xb_bucket), the same result."""
+    monkeypatch.setenv("TFIDF_XCHG", "owner")
+    monkeypatch.setenv("TFIDF_XB_STAGE_MAX", "0")
+    shards = _shards(cfg, scale, K)
+    ora = _full(cfg, scale)
+    texts, res, infos = _run_group(shards, K)
+    assert b"".join(texts) == ora["output_txt"]
+    assert_same_result(_concat(res), ora)
+    assert all(i["nterms_global"] == ora["nterms"] for i in infos)
+
+
 @pytest.mark.parametrize("xchg", ["dense", "dense_table", "owner"])
 def test_group_long_terms(xchg, monkeypatch):
     """Terms of >= 16 bytes (hash-tagged identity keys, not in term order) on the ranks: the
