@@ -797,11 +797,22 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     ENSURE(ctx->doc_size, (size_t)N * 4 + 4);
     ENSURE(ctx->doc_flags, (size_t)N + 1);
     unsigned long long* cnt = ctx->counters.as<unsigned long long>(); /* rec, part, ntok, status */
-    HIPCHK(hipMemsetAsync(ctx->vkeys.p, 0xEE, ctx->vcap * 16, s));
-    HIPCHK(hipMemsetAsync(cnt, 0, 256, s));   /* K1 counters, status, the sharded chunk counters */
-    HIPCHK(hipMemsetAsync(ctx->doc_npairs.p, 0, (size_t)N * 4 + 4, s));
-    HIPCHK(hipMemsetAsync(ctx->doc_size.p, 0, (size_t)N * 4 + 4, s));
-    HIPCHK(hipMemsetAsync(ctx->doc_flags.p, 0, (size_t)N + 1, s));
+    {   /* the run's clears in one launch: the vocabulary table (EMPTY keys), K1's counters,
+         * status and sharded chunk counters, the per-document pairs / sizes / flags */
+        FillList fl{};
+        auto add = [&](void* p, uint64_t bytes, uint32_t byte) {
+            fl.p[fl.n] = p;
+            fl.bytes[fl.n] = bytes;
+            fl.val[fl.n] = byte * 0x01010101u;
+            ++fl.n;
+        };
+        add(ctx->vkeys.p, ctx->vcap * 16, 0xEEu);
+        add(cnt, 256, 0u);
+        add(ctx->doc_npairs.p, (size_t)N * 4 + 4, 0u);
+        add(ctx->doc_size.p, (size_t)N * 4 + 4, 0u);
+        add(ctx->doc_flags.p, (size_t)N + 1, 0u);
+        LCHK(launch_fill_multi(fl, s));
+    }
     ENSURE(ctx->big_list, (size_t)BIG_LIST_CAP * 4);
     if (nchunks)
         LCHK(launch_plan_chunks(c, nchunks, cb, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(),

@@ -116,6 +116,44 @@ __global__ void k_gather_u128(const uint4* __restrict__ k, const uint32_t* __res
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = k[seq[i]];
 }
+/* one grid-stride pass over all segments' 16-byte blocks (off: their prefix counts, in
+ * 16-byte units), then each segment's tail bytes */
+struct FillRun {
+    FillList l;
+    uint64_t off[FILL_MAX + 1];
+};
+__global__ void k_fill_multi(const FillRun f) {
+    const uint64_t total = f.off[f.l.n];
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        uint32_t g = 0;
+        while (i >= f.off[g + 1]) ++g;
+        const uint32_t v = f.l.val[g];
+        reinterpret_cast<uint4*>(f.l.p[g])[i - f.off[g]] = make_uint4(v, v, v, v);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 16u * f.l.n) {
+        const uint32_t g = threadIdx.x / 16u, t = threadIdx.x % 16u;
+        const uint64_t nb = f.l.bytes[g];
+        if (t < (nb & 15u)) ((uint8_t*)f.l.p[g])[(nb & ~15ull) + t] = (uint8_t)f.l.val[g];
+    }
+}
+int launch_fill_multi(const FillList& l, hipStream_t s) {
+    if (l.n == 0) return 0;
+    if (l.n > (uint32_t)FILL_MAX) return -3;
+    FillRun f;
+    f.l = l;
+    f.off[0] = 0;
+    for (uint32_t g = 0; g < l.n; ++g) {
+        if (((uintptr_t)l.p[g] & 15u) != 0) return -3;
+        f.off[g + 1] = f.off[g] + l.bytes[g] / 16;
+    }
+    uint64_t nbx = (f.off[l.n] + NT - 1) / NT;
+    if (nbx < 1) nbx = 1;
+    if (nbx > 2048) nbx = 2048;
+    k_fill_multi<<<(unsigned)nbx, NT, 0, s>>>(f);
+    return ok();
+}
+
 int launch_gather_u128(const uint4* k, const uint32_t* seq, uint64_t n, uint4* out, hipStream_t s) {
     if (!n) return 0;
     k_gather_u128<<<grid_for(n), NT, 0, s>>>(k, seq, n, out);
@@ -1998,8 +2036,18 @@ static void launch_score_large(const K5Args& a, uint32_t grid, hipStream_t s) {
 int launch_score_order(const K5Args& a, Arena& ar, hipStream_t s, hipStream_t s2, hipEvent_t ev_fork,
                        hipEvent_t ev_join) {
     if (!a.ndocs) return 0;
-    if (hipMemsetAsync(a.large_count, 0, 4, s) != hipSuccess) return -1;
-    if (a.split_count && hipMemsetAsync(a.split_count, 0, 4, s) != hipSuccess) return -1;
+    {   /* the handed-off list's and the chunk tasks' counters, one launch */
+        FillList fl{};
+        fl.p[0] = a.large_count;
+        fl.bytes[0] = 4;
+        fl.n = 1;
+        if (a.split_count) {
+            fl.p[1] = a.split_count;
+            fl.bytes[1] = 4;
+            fl.n = 2;
+        }
+        if (launch_fill_multi(fl, s)) return -1;
+    }
     if (!a.idf_by_df)
         k_idf_of_rank<<<grid_for(a.nterms ? a.nterms : 1), NT, 0, s>>>(a.df_of_rank, a.idf_idx, a.idf, a.nterms,
                                                                       a.idf_rank);

@@ -118,6 +118,16 @@ int launch_vocab_compact(const VocabDev& v, uint64_t cap, const uint32_t* dense_
  * the sorted keys gathered back (long-term fix-up only) */
 int launch_sortkey_half(const uint4* k, uint64_t n, const uint32_t* seq, int hi, uint64_t* out, hipStream_t s);
 int launch_gather_u128(const uint4* k, const uint32_t* seq, uint64_t n, uint4* out, hipStream_t s);
+/* several byte fills in one launch (a run's clears: one kernel instead of one per buffer);
+ * each segment's base 16-byte aligned (device allocations are) */
+constexpr int FILL_MAX = 8;
+struct FillList {
+    void* p[FILL_MAX];
+    uint64_t bytes[FILL_MAX];
+    uint32_t val[FILL_MAX];   /* the byte value, replicated */
+    uint32_t n;
+};
+int launch_fill_multi(const FillList& l, hipStream_t s);
 int launch_vocab_rank(const uint32_t* sorted_dense, const uint32_t* vslot, uint32_t V, uint32_t* rank_of_slot,
                       uint32_t* slot_of_rank, uint16_t* rank16, hipStream_t s);
 /* long terms tied on their first 16 bytes: ordered by iterated segmented sorts (host loop,
