@@ -76,6 +76,34 @@ __global__ __launch_bounds__(SC_NT) void k_scan_apply(const T* in, T* out, uint6
     }
 }
 
+/* the apply pass that sums the block totals before it itself (up to SC_FUSED_MAXNB blocks:
+ * each block reads at most that many words), instead of a separate scan launch over them */
+constexpr uint64_t SC_FUSED_MAXNB = 1024;
+template <typename T>
+__global__ __launch_bounds__(SC_NT) void k_scan_apply_fused(const T* in, T* out, uint64_t n, const T* __restrict__ bsum) {
+    __shared__ T wsum[SC_NT / 64];
+    T pre = 0;
+    for (uint32_t k = threadIdx.x; k < blockIdx.x; k += SC_NT) pre += bsum[k];
+    T boff;
+    (void)block_excl_scan_t<T>(pre, wsum, &boff);
+    const uint64_t base = (uint64_t)blockIdx.x * SC_TILE + (uint64_t)threadIdx.x * SC_IT;
+    T v[SC_IT];
+    T s = 0;
+#pragma unroll
+    for (int j = 0; j < SC_IT; ++j) {
+        v[j] = (base + j < n) ? in[base + j] : (T)0;
+        s += v[j];
+    }
+    T tot;
+    T run = block_excl_scan_t<T>(s, wsum, &tot) + boff;
+#pragma unroll
+    for (int j = 0; j < SC_IT; ++j) {
+        if (base + j < n) out[base + j] = run;
+        run += v[j];
+        if (base + j + 1 == n) out[n] = run;
+    }
+}
+
 template <typename T>
 int scan_excl_t(const T* in, T* out, uint64_t n, Arena& ar, hipStream_t s) {
     if (n == 0) return hipMemsetAsync(out, 0, sizeof(T), s) == hipSuccess ? 0 : -1;
@@ -88,6 +116,11 @@ int scan_excl_t(const T* in, T* out, uint64_t n, Arena& ar, hipStream_t s) {
     T* bsum = (T*)ar.get((nb + 1) * sizeof(T));
     if (!bsum) return -2;
     k_scan_reduce<T><<<(unsigned)nb, SC_NT, 0, s>>>(in, n, bsum);
+    if (nb <= SC_FUSED_MAXNB) {   /* two launches instead of three */
+        k_scan_apply_fused<T><<<(unsigned)nb, SC_NT, 0, s>>>(in, out, n, bsum);
+        ar.release(m);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     int rc = scan_excl_t<T>(bsum, bsum, nb, ar, s);
     if (rc) return rc;
     k_scan_apply<T><<<(unsigned)nb, SC_NT, 0, s>>>(in, out, n, bsum);
