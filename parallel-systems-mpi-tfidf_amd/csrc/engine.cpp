@@ -163,6 +163,7 @@ struct tfidf_ctx {
      * final status): asynchronous copies on the stream and one synchronisation each, instead
      * of pageable or synchronous copies (two round trips per run saved) */
     uint64_t* hpin = nullptr;
+    uint64_t* hpin_dev = nullptr;   /* hpin as the device addresses it (status words written by kernels) */
     DevBuf dense, vslot, skey0, skey1, seq0, seq1, rank_of_slot, slot_of_rank, rank16;
     DevBuf pkey0, pkey1, pseq0, pseq1, phead;
     DevBuf big_list, big_idx, dense_cnt, kcnt, tile_cnt;   /* dense merge of long documents */
@@ -377,6 +378,10 @@ int tfidf_open(int device, tfidf_ctx** out) {
     if (arena_reset(ctx, 64ull << 20) != 0) { delete ctx; return TFIDF_E_NOMEM; }
     if (ctx->counters.ensure(256) != 0) { delete ctx; return TFIDF_E_NOMEM; }
     if (hipHostMalloc((void**)&ctx->hpin, 256, hipHostMallocDefault) != hipSuccess) { delete ctx; return TFIDF_E_NOMEM; }
+    if (hipHostGetDevicePointer((void**)&ctx->hpin_dev, ctx->hpin, 0) != hipSuccess || !ctx->hpin_dev) {
+        delete ctx;
+        return TFIDF_E_NOMEM;
+    }
     if (hipHostMalloc((void**)&ctx->k1out_host, sizeof(K1Out), hipHostMallocDefault) != hipSuccess ||
         ctx->k1out_dev.ensure(sizeof(K1Out)) != 0) { delete ctx; return TFIDF_E_NOMEM; }
     g_live_ctx.fetch_add(1);
@@ -863,9 +868,14 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     LCHK(launch_vocab_flags(vd, cap, ctx->dense.as<uint32_t>(), s));
     LCHK(scan_excl_u32(ctx->dense.as<uint32_t>(), ctx->dense.as<uint32_t>(), cap, ar, s));
     uint64_t* hp = ctx->hpin;
-    HIPCHK(hipMemcpyAsync(hp, cnt, 64, hipMemcpyDeviceToHost, s));
-    hp[8] = 0;
-    HIPCHK(hipMemcpyAsync(hp + 8, ctx->dense.as<uint32_t>() + cap, 4, hipMemcpyDeviceToHost, s));
+    {   /* K1's counters (hp[0..7]) and the vocabulary size (hp[8]): one launch */
+        WordList wl{};
+        for (int i = 0; i < 8; ++i) { wl.src[i] = cnt + i; wl.bytes[i] = 8; }
+        wl.src[8] = ctx->dense.as<uint32_t>() + cap;
+        wl.bytes[8] = 4;
+        wl.n = 9;
+        LCHK(launch_words_to_host(wl, ctx->hpin_dev, s));
+    }
     HIPCHK(hipStreamSynchronize(s));
     const uint32_t V = (uint32_t)hp[8];
     unsigned long long hc[8];
@@ -1338,16 +1348,22 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
     a.out_score = ctx->out_score.as<double>();
     XCHK(launch_score_order(a, ar, s, ctx->stream2, ctx->ev_fork, ctx->ev_order));
     mark(ctx, S_NSTAGES);
-    ctx->hpin[10] = 0;
-    ctx->hpin[14] = 0;
-    HIPCHK(hipMemcpyAsync(ctx->hpin + 10, cnt + 3, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(ctx->hpin + 11, ctx->out_off.as<uint64_t>() + N, 8, hipMemcpyDeviceToHost, s));
-    if (ctx->xp) HIPCHK(hipMemcpyAsync(ctx->hpin + 14, cnt + 12, 4, hipMemcpyDeviceToHost, s));   /* global V */
+    {   /* the final status, the pair total and (with a transport) global V: one launch */
+        WordList wl{};
+        wl.src[0] = cnt + 3;
+        wl.bytes[0] = 4;
+        wl.src[1] = ctx->out_off.as<uint64_t>() + N;
+        wl.bytes[1] = 8;
+        wl.src[2] = cnt + 12;
+        wl.bytes[2] = 4;
+        wl.n = ctx->xp ? 3 : 2;
+        XCHK(launch_words_to_host(wl, ctx->hpin_dev + 24, s));
+    }
     XSYNC(s);
-    const uint32_t st_end = (uint32_t)ctx->hpin[10];
-    const uint64_t P = ctx->hpin[11];
+    const uint32_t st_end = (uint32_t)ctx->hpin[24];
+    const uint64_t P = ctx->hpin[25];
     ctx->npairs = P;
-    if (ctx->xp) ctx->Vg = (uint32_t)ctx->hpin[14];
+    if (ctx->xp) ctx->Vg = (uint32_t)ctx->hpin[26];
     if (st_end & ST_BOUNDS) {
         fprintf(stderr, "tfidf: internal bounds check tripped (status 0x%x)\n", st_end);
         return TFIDF_E_STATE;

@@ -154,6 +154,20 @@ int launch_fill_multi(const FillList& l, hipStream_t s) {
     return ok();
 }
 
+/* dst[i] = the i-th word, zero-extended; dst is pinned host memory (visible to the host
+ * after the stream synchronises) */
+__global__ void k_words_to_host(const WordList l, uint64_t* dst) {
+    const uint32_t i = threadIdx.x;
+    if (i >= l.n) return;
+    dst[i] = l.bytes[i] == 8 ? *(const volatile uint64_t*)l.src[i] : (uint64_t) * (const volatile uint32_t*)l.src[i];
+}
+int launch_words_to_host(const WordList& l, uint64_t* host_dst, hipStream_t s) {
+    if (l.n == 0) return 0;
+    if (l.n > (uint32_t)WORDS_MAX) return -3;
+    k_words_to_host<<<1, 64, 0, s>>>(l, host_dst);
+    return ok();
+}
+
 int launch_gather_u128(const uint4* k, const uint32_t* seq, uint64_t n, uint4* out, hipStream_t s) {
     if (!n) return 0;
     k_gather_u128<<<grid_for(n), NT, 0, s>>>(k, seq, n, out);

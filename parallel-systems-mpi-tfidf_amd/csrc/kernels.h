@@ -128,6 +128,15 @@ struct FillList {
     uint32_t n;
 };
 int launch_fill_multi(const FillList& l, hipStream_t s);
+/* a few device words (4 or 8 bytes each) into pinned host memory in one launch (the run's
+ * status reads: one small kernel instead of one copy per word) */
+constexpr int WORDS_MAX = 16;
+struct WordList {
+    const void* src[WORDS_MAX];
+    uint32_t bytes[WORDS_MAX];   /* 4 or 8 */
+    uint32_t n;
+};
+int launch_words_to_host(const WordList& l, uint64_t* host_dst, hipStream_t s);
 int launch_vocab_rank(const uint32_t* sorted_dense, const uint32_t* vslot, uint32_t V, uint32_t* rank_of_slot,
                       uint32_t* slot_of_rank, uint16_t* rank16, hipStream_t s);
 /* long terms tied on their first 16 bytes: ordered by iterated segmented sorts (host loop,
