@@ -129,6 +129,7 @@ struct tfidf_ctx {
     uint64_t sl_maxcap = K1_ST_MAX_CAP;   /* env TFIDF_SL_MAXCAP: tokcount_sl up to this many vocabulary slots */
     K1Out* k1out_host = nullptr;   /* pinned: tokcount_sl's output block, copied to k1out_dev per run */
     DevBuf k1out_dev;
+    bool k1out_valid = false;      /* k1out_dev holds *k1out_host (the copy is skipped when a run's block is the same) */
     hipEvent_t ev[S_NSTAGES + 1];
     Arena arena;
     DevBuf arena_buf;
@@ -852,8 +853,11 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     if (nchunks && ctx->k1_sl) {
         /* pinned source: the copy is stream-ordered before the launch, and the block is not
          * rewritten before the next run (every run synchronises with the host after K1) */
-        *ctx->k1out_host = o;
-        HIPCHK(hipMemcpyAsync(ctx->k1out_dev.p, ctx->k1out_host, sizeof(K1Out), hipMemcpyHostToDevice, s));
+        if (!ctx->k1out_valid || memcmp(ctx->k1out_host, &o, sizeof(K1Out)) != 0) {   /* steady state: unchanged */
+            *ctx->k1out_host = o;
+            HIPCHK(hipMemcpyAsync(ctx->k1out_dev.p, ctx->k1out_host, sizeof(K1Out), hipMemcpyHostToDevice, s));
+            ctx->k1out_valid = true;
+        }
         LCHK(launch_tokcount_sl(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd,
                                 ctx->k1out_dev.as<K1Out>(), s));
     } else if (nchunks && ctx->k1_vs)
