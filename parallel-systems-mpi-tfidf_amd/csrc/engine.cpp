@@ -137,6 +137,7 @@ struct tfidf_ctx {
      * vocabulary / merge / DF stages, after K1 (K1's persistent grid wants every CU) */
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_order = nullptr;
+    hipEvent_t ev_spin = nullptr;   /* the run's host waits (spin_sync) */
     Arena arena2;
     DevBuf arena2_buf;
     /* host-input staging */
@@ -263,7 +264,7 @@ static std::atomic<int> g_live_ctx{0};
             const int w_ = ctx->xp->wait(s_);                                              \
             if (w_) return w_;                                                             \
         } else {                                                                           \
-            HIPCHK(hipStreamSynchronize(s_));                                              \
+            HIPCHK(spin_sync(ctx, s_));                                                    \
         }                                                                                  \
     } while (0)
 /* TFIDF_DEBUG_ALLOC=1: every (re)allocation of a stage buffer is named on stderr (which
@@ -302,6 +303,18 @@ static int arena_reset(tfidf_ctx* ctx, size_t want) {
 
 static void mark(tfidf_ctx* ctx, int stage) {
     if (ctx->timing) (void)hipEventRecord(ctx->ev[stage], ctx->stream);
+}
+
+/* The run's waits for its own stream (K1's counters, the final status): the host polls an
+ * event instead of blocking in hipStreamSynchronize, whose wake-up after a millisecond-long
+ * kernel left the device idle for tens of microseconds before the next launches. */
+static hipError_t spin_sync(tfidf_ctx* ctx, hipStream_t s) {
+    if (g_live_ctx.load() > 1) return hipStreamSynchronize(s);   /* several ranks' threads in this process */
+    hipError_t e = hipEventRecord(ctx->ev_spin, s);
+    if (e != hipSuccess) return e;
+    while ((e = hipEventQuery(ctx->ev_spin)) == hipErrorNotReady) {
+    }
+    return e;
 }
 
 extern "C" {
@@ -371,6 +384,7 @@ int tfidf_open(int device, tfidf_ctx** out) {
     HIPCHK(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ctx->ev_order, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ctx->ev_idf, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ctx->ev_spin, hipEventDisableTiming));
     {
         const char* ic = getenv("TFIDF_IDF_CACHE");
         ctx->idf_cache = ic && ic[0] == '1';
@@ -397,6 +411,7 @@ void tfidf_close(tfidf_ctx* ctx) {
     delete ctx->xp;
     if (ctx->stream2) { (void)hipStreamSynchronize(ctx->stream2); (void)hipStreamDestroy(ctx->stream2); }
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    if (ctx->ev_spin) (void)hipEventDestroy(ctx->ev_spin);
     if (ctx->ev_order) (void)hipEventDestroy(ctx->ev_order);
     idf_pool_stop(ctx);
     g_live_ctx.fetch_sub(1);
@@ -880,7 +895,7 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
         wl.n = 9;
         LCHK(launch_words_to_host(wl, ctx->hpin_dev, s));
     }
-    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(spin_sync(ctx, s));
     const uint32_t V = (uint32_t)hp[8];
     unsigned long long hc[8];
     for (int i = 0; i < 8; ++i) hc[i] = hp[i];
