@@ -399,6 +399,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the measured HBM read/copy peak probe")
     ap.add_argument("--no-emit", action="store_true", help="skip the (untimed) output-emission measurement")
+    ap.add_argument("--stage-steps", type=int, default=3,
+                    help="untimed steps after the timed ones with per-stage HIP events (stage_ms_*)")
     ap.add_argument("--vocab", type=int, default=0, help="diagnostics only: override the config's vocabulary size")
     ap.add_argument("--plan-only", action="store_true",
                     help="print what would be measured (shards per rank, and the c3 strong follow-up of a "
@@ -455,7 +457,11 @@ def main():
         p = tfidf_configs.plan(args.config, scale=args.scale, rank=rank, nranks=world, weak=not args.strong,
                                vocab=args.vocab)
     corpus = eng.synth_device(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"], p["ndocs_total"])
-    eng.set_timing(True)
+    # the timed steps record HIP events around K1 and the whole run only (the roofline's K1
+    # time, device_ms_per_step); the per-stage breakdown comes from --stage-steps extra steps
+    # after the timed region (each event record costs the stream ~5 us: ten of them are ~2 %
+    # of a c2 step)
+    eng.set_timing(2)
 
     # cold run: the first tfidf_run of this fresh context (table growth retries, the idf LUT
     # of this N, every first device allocation), timed on its own and reported beside the
@@ -492,6 +498,13 @@ def main():
     alloc_t1 = eng.alloc_counters()
     info = eng.info()
     C_bytes, P_pairs, T_tok = info["nbytes"], info["npairs"], info["ntokens"]
+    # the stage breakdown, after the timed region: every stage's events
+    eng.set_timing(True)
+    stage_steps = []
+    for _ in range(max(1, args.stage_steps)):
+        eng.run_corpus(corpus)
+        stage_steps.append(eng.info()["stages"])
+    info = eng.info()
 
     # output emission, outside the timed region and not in `value`:
     # GPU %.16f formatting of the last step's lines, then the pinned D2H + write path
@@ -586,6 +599,8 @@ def main():
             "stage_ms": {k: round(v, 4) for k, v in info["stages"].items()},
             "stage_ms_mean": {k: round(float(np.mean([st[k] for st in stage_steps])), 4) for k in info["stages"]},
             "stage_ms_max": {k: round(float(np.max([st[k] for st in stage_steps])), 4) for k in info["stages"]},
+            "stage_ms_source": f"{len(stage_steps)} untimed steps after the timed ones, with per-stage HIP events "
+                               f"(the timed steps record K1's and the whole run's events only)",
             # the idf table (log(N/df) on the host's libm, TFIDF.c:243) is rebuilt inside every
             # timed step on host threads beside the device stages (TFIDF_IDF_CACHE=1: kept
             # across runs of one N, reported as idf_cached)

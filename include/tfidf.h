@@ -208,7 +208,9 @@ int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info);
 /* The same device-allocation counters without a run (process-wide, cumulative). */
 int tfidf_alloc_stats(uint64_t* allocs, uint64_t* bytes);
 const char* tfidf_stage_name(int stage);
-/* Enables per-stage HIP event timing (adds a few event records per run). */
+/* HIP event timing of a run's stages (tfidf_run_info.ms_stage / ms_tokcount / ms_total):
+ * enable 0 none, 1 every stage (the default; ten event records per run), 2 the tokenize+count
+ * kernel and the whole run only (four records; each record costs the stream ~5 us). */
 int tfidf_set_timing(tfidf_ctx* ctx, int enable);
 /* Diagnostics: per-phase cycle sums of the fast tokenize+count kernel, available only
  * from the diagnostic build lib/libtfidf_hip_stamps.so with TFIDF_STAMPS=1 set before

@@ -112,7 +112,7 @@ struct tfidf_ctx {
     hipStream_t stream = nullptr;
     Xport* xp = nullptr;    /* peers of the DF exchange (RCCL or in-process); owned */
     int rank = 0, nranks = 1;
-    bool timing = true;
+    int timing = 1;         /* tfidf_set_timing: 0 none, 1 every stage, 2 K1 and the whole run only */
     int k1_mode = 0;        /* 0 auto (k_tokcount_sl up to K1_ST_MAX_CAP slots, k_tokcount_vs beyond),
                                1 round-1 kernel (TFIDF_K1=vs), 2 general K1 (TFIDF_K1=general),
                                3 k_tokcount_sl (TFIDF_K1=sl) — cross-checks and A/B timing;
@@ -178,7 +178,9 @@ struct tfidf_ctx {
     bool idf_cache = false;
     double* idf_pin = nullptr;
     size_t idf_pin_n = 0;
-    hipEvent_t ev_idf = nullptr;          /* the table's upload (idf_pin reusable after it) */
+    bool idf_pin_busy = false;            /* an upload from idf_pin is enqueued and not known complete (the
+                                             run's final wait clears it; no event record: each costs
+                                             the stream ~5 us, scripts/micro/host_api_cost.hip) */
     struct IdfPool {                      /* persistent workers: no thread start per run */
         std::mutex mu;
         std::condition_variable go, done;
@@ -301,8 +303,12 @@ static int arena_reset(tfidf_ctx* ctx, size_t want) {
     return 0;
 }
 
+/* each event record costs the stream ~5 us (scripts/micro/host_api_cost.hip): level 2 records
+ * only the four K1 and whole-run bounds */
 static void mark(tfidf_ctx* ctx, int stage) {
-    if (ctx->timing) (void)hipEventRecord(ctx->ev[stage], ctx->stream);
+    if (ctx->timing == 1 ||
+        (ctx->timing == 2 && (stage == S_PREP || stage == S_TOKCOUNT || stage == S_VOCAB || stage == S_NSTAGES)))
+        (void)hipEventRecord(ctx->ev[stage], ctx->stream);
 }
 
 /* The run's waits for its own stream (K1's counters, the final status): the host polls an
@@ -383,7 +389,6 @@ int tfidf_open(int device, tfidf_ctx** out) {
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ctx->ev_order, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&ctx->ev_idf, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ctx->ev_spin, hipEventDisableTiming));
     {
         const char* ic = getenv("TFIDF_IDF_CACHE");
@@ -415,7 +420,6 @@ void tfidf_close(tfidf_ctx* ctx) {
     if (ctx->ev_order) (void)hipEventDestroy(ctx->ev_order);
     idf_pool_stop(ctx);
     g_live_ctx.fetch_sub(1);
-    if (ctx->ev_idf) { (void)hipEventSynchronize(ctx->ev_idf); (void)hipEventDestroy(ctx->ev_idf); }
     if (ctx->idf_pin) (void)hipHostFree(ctx->idf_pin);
     for (int i = 0; i < WR_NBUF; ++i) {
         if (ctx->wr_buf[i]) (void)hipHostFree(ctx->wr_buf[i]);
@@ -450,7 +454,7 @@ void tfidf_close(tfidf_ctx* ctx) {
 
 int tfidf_set_timing(tfidf_ctx* ctx, int enable) {
     if (!ctx) return TFIDF_E_INVAL;
-    ctx->timing = enable != 0;
+    ctx->timing = enable == 2 ? 2 : (enable != 0 ? 1 : 0);
     return TFIDF_OK;
 }
 
@@ -783,6 +787,10 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     ctx->run_N = N;
     ctx->run_V = 0;
     mark(ctx, S_PREP);
+    /* the side stream's fork point (the document order needs only the run's inputs): recorded
+     * first, while the device still waits for the host's first launches, since a record costs
+     * the stream ~5 us wherever it sits */
+    HIPCHK(hipEventRecord(ctx->ev_fork, s));
     /* ---- buffers ---- */
     if (ctx->xp) {   /* the exchange's count rows (sized before its agreement: see exchange_owner) */
         const size_t R = (size_t)ctx->nranks;
@@ -936,8 +944,7 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
         ctx->arena2.base = (uint8_t*)ctx->arena2_buf.p;
         ctx->arena2.cap = ctx->arena2_buf.cap;
         ctx->arena2.used = 0;
-        HIPCHK(hipEventRecord(ctx->ev_fork, s));
-        HIPCHK(hipStreamWaitEvent(s2, ctx->ev_fork, 0));
+        HIPCHK(hipStreamWaitEvent(s2, ctx->ev_fork, 0));   /* recorded when the attempt started */
         LCHK(launch_doc_keys(dev_ids, N, ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), s2));
         /* base-11 keys of 10 digits are < 11^10 < 2^35: five bytes, no probe */
         /* up to SORT_TILE_MAXN documents: two launches (tile bitonic sort + rank) instead of
@@ -1198,7 +1205,10 @@ static int idf_start(tfidf_ctx* ctx, uint64_t Nt) {
     ctx->ms_idf_host = ctx->ms_idf_wait = 0;
     if (Nt > IDF_FULL_MAX) return TFIDF_OK;                          /* distinct-df path in run_post */
     if (ctx->idf_cache && ctx->idf_full_n == Nt) return TFIDF_OK;    /* TFIDF_IDF_CACHE=1 */
-    HIPCHK(hipEventSynchronize(ctx->ev_idf));   /* the previous upload has read idf_pin */
+    if (ctx->idf_pin_busy) {   /* a failed run left its upload of idf_pin unwaited */
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        ctx->idf_pin_busy = false;
+    }
     const size_t n = (size_t)Nt + 1;
     if (ctx->idf_pin_n < n) {
         if (ctx->idf_pin) (void)hipHostFree(ctx->idf_pin);
@@ -1255,7 +1265,7 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
             ENSURE(ctx->idf_vals, (size_t)(Nt + 1) * 8);
             idf_join(ctx);
             HIPCHK(hipMemcpyAsync(ctx->idf_vals.p, ctx->idf_pin, (size_t)(Nt + 1) * 8, hipMemcpyHostToDevice, s));
-            HIPCHK(hipEventRecord(ctx->ev_idf, s));
+            ctx->idf_pin_busy = true;
             ctx->idf_full_n = Nt;
         } else if (ctx->idf_full_n != Nt) {
             return TFIDF_E_STATE;   /* idf_start made no table and none is cached: not reachable */
@@ -1293,7 +1303,10 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
         }
         ENSURE(ctx->idf_vals, (size_t)K * 8 + 8);
         /* the distinct df values' logs on the context's workers, into pinned memory */
-        HIPCHK(hipEventSynchronize(ctx->ev_idf));   /* the previous upload has read idf_pin */
+        if (ctx->idf_pin_busy) {   /* a failed run left its upload of idf_pin unwaited */
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        ctx->idf_pin_busy = false;
+    }
         if (ctx->idf_pin_n < (size_t)K + 1) {
             if (ctx->idf_pin) (void)hipHostFree(ctx->idf_pin);
             ctx->idf_pin = nullptr;
@@ -1312,7 +1325,7 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
                 idf_join(ctx);
             }
             HIPCHK(hipMemcpyAsync(ctx->idf_vals.p, ctx->idf_pin, (size_t)K * 8, hipMemcpyHostToDevice, s));
-            HIPCHK(hipEventRecord(ctx->ev_idf, s));
+            ctx->idf_pin_busy = true;
         }
         ctx->idf_logs = K;   /* this run's distinct df values */
     }
@@ -1379,6 +1392,7 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
         XCHK(launch_words_to_host(wl, ctx->hpin_dev + 24, s));
     }
     XSYNC(s);
+    ctx->idf_pin_busy = false;   /* the stream has drained */
     const uint32_t st_end = (uint32_t)ctx->hpin[24];
     const uint64_t P = ctx->hpin[25];
     ctx->npairs = P;
@@ -1500,7 +1514,15 @@ extern "C" int tfidf_run(tfidf_ctx* ctx, const tfidf_corpus* in) {
     ctx->ndocs_total = Nt;
     ctx->have_result = true;
     ctx->have_info = true;
-    if (ctx->timing) {
+    if (ctx->timing == 2) {
+        for (int i = 0; i < S_NSTAGES; ++i) ctx->ms_stage[i] = 0;
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, ctx->ev[S_TOKCOUNT], ctx->ev[S_VOCAB]);
+        ctx->ms_stage[S_TOKCOUNT] = ms;
+        float tot = 0;
+        (void)hipEventElapsedTime(&tot, ctx->ev[S_PREP], ctx->ev[S_NSTAGES]);
+        ctx->ms_total = tot;
+    } else if (ctx->timing) {
         for (int i = 0; i < S_NSTAGES; ++i) {
             float ms = 0;
             (void)hipEventElapsedTime(&ms, ctx->ev[i], ctx->ev[i + 1]);

@@ -205,8 +205,10 @@ class Engine:
     def __exit__(self, *a):
         self.close()
 
-    def set_timing(self, on: bool):
-        _chk(lib().tfidf_set_timing(self.h, 1 if on else 0), "set_timing")
+    def set_timing(self, on):
+        """True / 1: every stage; 2: K1 and the whole run only; False / 0: none"""
+        lvl = 2 if (on == 2 and on is not True) else (1 if on else 0)
+        _chk(lib().tfidf_set_timing(self.h, lvl), "set_timing")
 
     def comm_init(self, uid: bytes, rank: int, nranks: int):
         buf = (C.c_uint8 * UNIQUE_ID_BYTES).from_buffer_copy(uid)

@@ -10,6 +10,8 @@ __global__ void k_spin(unsigned long long cycles) {
 }
 __global__ void k_tiny(int* p) { if (threadIdx.x == 0 && blockIdx.x == 0) p[0] += 1; }
 
+int device_side();
+
 int main() {
     hipStream_t s, s2;
     hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
@@ -34,5 +36,43 @@ int main() {
     bench("hipMemsetAsync 4 KB", [&](int) { hipMemsetAsync(d, 0, 4096, s); });
     bench("hipStreamWaitEvent (other stream)", [&](int i) { hipEventRecord(ev[i % 64], s); hipStreamWaitEvent(s2, ev[i % 64], 0); });
     bench("launch + event record", [&](int i) { k_tiny<<<1, 64, 0, s>>>(d); hipEventRecord(ev[i % 64], s); });
+    return device_side();
+}
+// (appended) device-side cost of the packets between kernels: N tiny kernels alone, and with
+// an event record (timing / no timing) or a wait on a completed event of another stream after
+// each; all enqueued behind a spin kernel, timed by events around them
+int device_side() {
+    hipStream_t s, s2;
+    hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
+    int* d;
+    hipMalloc(&d, 4096);
+    hipEvent_t t0, t1, et, en, done;
+    hipEventCreate(&t0);
+    hipEventCreate(&t1);
+    hipEventCreate(&et);
+    hipEventCreateWithFlags(&en, hipEventDisableTiming);
+    hipEventCreateWithFlags(&done, hipEventDisableTiming);
+    k_tiny<<<1, 64, 0, s2>>>(d);
+    hipEventRecord(done, s2);
+    hipStreamSynchronize(s2);
+    const int n = 100;
+    for (int mode = 0; mode < 4; ++mode) {
+        k_spin<<<1, 64, 0, s>>>(200000000ull);
+        hipEventRecord(t0, s);
+        for (int i = 0; i < n; ++i) {
+            k_tiny<<<1, 64, 0, s>>>(d);
+            if (mode == 1) hipEventRecord(et, s);
+            if (mode == 2) hipEventRecord(en, s);
+            if (mode == 3) hipStreamWaitEvent(s, done, 0);
+        }
+        hipEventRecord(t1, s);
+        hipEventSynchronize(t1);
+        float ms = 0;
+        hipEventElapsedTime(&ms, t0, t1);
+        const char* what[] = {"tiny kernels alone", "+ timing event record", "+ no-timing event record",
+                              "+ wait on a completed event"};
+        printf("device: %-28s %7.2f us per kernel\n", what[mode], ms * 1e3 / n);
+    }
     return 0;
 }
