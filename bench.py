@@ -480,22 +480,22 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    k1_ms, tot_ms, stage_steps, idf_steps = [], [], [], []
     barrier()
     hip_device_sync()
     alloc_t0 = eng.alloc_counters()
+    eng.totals(reset=True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(args.steps):   # nothing but the runs: their K1 / run / idf times are summed by the engine
         eng.run_corpus(corpus)
-        info = eng.info()
-        k1_ms.append(info["ms_tokcount"])
-        tot_ms.append(info["ms_total"])
-        stage_steps.append(info["stages"])
-        idf_steps.append((info["idf_logs"], info["ms_idf_host"], info["ms_idf_wait"]))
     hip_device_sync()
     barrier()
     elapsed = time.perf_counter() - t0
     alloc_t1 = eng.alloc_counters()
+    tt = eng.totals(reset=True)
+    nrun = max(1, int(tt["runs"]))
+    k1_ms = [tt["ms_tokcount"] / nrun]
+    tot_ms = [tt["ms_total"] / nrun]
+    idf_steps = [(tt["idf_logs"] / nrun, tt["ms_idf_host"] / nrun, tt["ms_idf_wait"] / nrun)]
     info = eng.info()
     C_bytes, P_pairs, T_tok = info["nbytes"], info["npairs"], info["ntokens"]
     # the stage breakdown, after the timed region: every stage's events

@@ -205,6 +205,16 @@ typedef struct tfidf_run_info {
 #define TFIDF_RUN_XCHG_DENSE 16u  /* multi-rank: the DF exchange used the dense all-reduce form
                                      (else the hash-owner all-to-all; single rank: no exchange) */
 int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* info);
+/* Sums over the successful runs since the last reset (a caller timing many runs reads them
+ * once instead of querying every run): runs, K1 ms, whole-run ms (HIP events: 0 while
+ * timing is off), idf logs, idf host ms, idf wait ms.  reset != 0 zeroes them after the read. */
+typedef struct tfidf_run_totals {
+    uint64_t runs;
+    double ms_tokcount, ms_total;
+    uint64_t idf_logs;
+    double ms_idf_host, ms_idf_wait;
+} tfidf_run_totals;
+int tfidf_run_totals_get(tfidf_ctx* ctx, tfidf_run_totals* out, int reset);
 /* The same device-allocation counters without a run (process-wide, cumulative). */
 int tfidf_alloc_stats(uint64_t* allocs, uint64_t* bytes);
 const char* tfidf_stage_name(int stage);

@@ -196,6 +196,7 @@ struct tfidf_ctx {
         int64_t end_ns = 0;
     } idf_pool;
     uint64_t idf_logs = 0;                /* log() calls of the last run */
+    tfidf_run_totals totals{};            /* sums over the runs since the last tfidf_run_totals_get reset */
     double ms_idf_host = 0, ms_idf_wait = 0;
     DevBuf dkey0, dkey1, dseq0, dseq1, npairs_ord, out_off, doc_meta;
     DevBuf out_term, out_cnt, out_score, idf_rank, large_list, split_tasks, cls_off;
@@ -1532,6 +1533,19 @@ extern "C" int tfidf_run(tfidf_ctx* ctx, const tfidf_corpus* in) {
         (void)hipEventElapsedTime(&tot, ctx->ev[S_PREP], ctx->ev[S_NSTAGES]);
         ctx->ms_total = tot;
     }
+    ctx->totals.runs += 1;
+    ctx->totals.ms_tokcount += ctx->timing ? ctx->ms_stage[S_TOKCOUNT] : 0.0;
+    ctx->totals.ms_total += ctx->timing ? ctx->ms_total : 0.0;
+    ctx->totals.idf_logs += ctx->idf_logs;
+    ctx->totals.ms_idf_host += ctx->ms_idf_host;
+    ctx->totals.ms_idf_wait += ctx->ms_idf_wait;
+    return TFIDF_OK;
+}
+
+extern "C" int tfidf_run_totals_get(tfidf_ctx* ctx, tfidf_run_totals* out, int reset) {
+    if (!ctx || !out) return TFIDF_E_INVAL;
+    *out = ctx->totals;
+    if (reset) ctx->totals = tfidf_run_totals{};
     return TFIDF_OK;
 }
 

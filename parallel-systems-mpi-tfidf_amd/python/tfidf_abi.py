@@ -36,7 +36,7 @@ EXPORTS = [
     "tfidf_ingest_dir_device", "tfidf_hbm_probe", "tfidf_group_open", "tfidf_group_size", "tfidf_group_ctx",
     "tfidf_group_run", "tfidf_group_write_output", "tfidf_group_close", "tfidf_plan_dir", "tfidf_plan_free",
     "tfidf_ingest_shard_device", "tfidf_doc_name_order", "tfidf_shard_split", "tfidf_device_count",
-    "tfidf_last_output_info",
+    "tfidf_last_output_info", "tfidf_run_totals_get",
 ]
 TFIDF_GROUP_LOCAL = 1
 E_PEER = -11
@@ -70,6 +70,11 @@ class RunInfo(C.Structure):
         ("device_allocs", C.c_uint64), ("device_alloc_bytes", C.c_uint64),
         ("idf_logs", C.c_uint64), ("ms_idf_host", C.c_double), ("ms_idf_wait", C.c_double),
     ]
+
+
+class RunTotals(C.Structure):
+    _fields_ = [("runs", C.c_uint64), ("ms_tokcount", C.c_double), ("ms_total", C.c_double),
+                ("idf_logs", C.c_uint64), ("ms_idf_host", C.c_double), ("ms_idf_wait", C.c_double)]
 
 
 class OutputInfo(C.Structure):
@@ -112,6 +117,7 @@ def lib() -> C.CDLL:
         L.tfidf_result_free.argtypes = [C.POINTER(Result)]
         L.tfidf_result_free.restype = None
         L.tfidf_last_run_info.argtypes = [C.c_void_p, C.POINTER(RunInfo)]
+        L.tfidf_run_totals_get.argtypes = [C.c_void_p, C.POINTER(RunTotals), C.c_int]
         L.tfidf_alloc_stats.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.tfidf_stage_name.restype = C.c_char_p
         L.tfidf_set_timing.argtypes = [C.c_void_p, C.c_int]
@@ -275,6 +281,12 @@ class Engine:
         a, b = C.c_uint64(), C.c_uint64()
         _chk(lib().tfidf_alloc_stats(C.byref(a), C.byref(b)), "tfidf_alloc_stats")
         return int(a.value), int(b.value)
+
+    def totals(self, reset: bool = False) -> dict:
+        """sums over the successful runs since the last reset (tfidf_run_totals_get)"""
+        t = RunTotals()
+        _chk(lib().tfidf_run_totals_get(self.h, C.byref(t), 1 if reset else 0), "tfidf_run_totals_get")
+        return {k: getattr(t, k) for k, _ in RunTotals._fields_}
 
     def info(self) -> dict:
         r = RunInfo()
