@@ -776,6 +776,42 @@ static int exchange_df(tfidf_ctx* ctx, int local_rc, uint32_t V) {
     return rc;
 }
 
+/* The document order (`docN@` strcmp order of the run's documents) on the side stream,
+ * joined before the per-position metadata (run_post).  Enqueued right after K1 for a large
+ * N (its radix sort is long: started early, it is done long before it is needed), after the
+ * vocabulary stage's launches for up to SORT_TILE_MAXN documents (two short launches: the
+ * device runs the vocabulary stage while the host enqueues them; c2 +0.9 %, while c5's
+ * 1e6-document sort beside its merge stage slowed that by 0.07 ms). */
+static int enqueue_doc_order(tfidf_ctx* ctx, const uint32_t* dev_ids, uint32_t N) {
+    ENSURE(ctx->dkey0, (size_t)N * 8 + 8);
+    ENSURE(ctx->dkey1, (size_t)N * 8 + 8);
+    ENSURE(ctx->dseq0, (size_t)N * 4 + 4);
+    ENSURE(ctx->dseq1, (size_t)N * 4 + 4);
+    {
+        hipStream_t s2 = ctx->stream2;
+        /* the radix histograms, or the tile sort's staging (20 B per document) */
+        const size_t need2 = (size_t)256 * 4 * ((N + 2047) / 2048 + 1) + (size_t)N * 20 + (1u << 20);
+        if (need2 > ctx->arena2_buf.cap && ctx->arena2_buf.ensure(need2) != 0) return TFIDF_E_NOMEM;
+        ctx->arena2.base = (uint8_t*)ctx->arena2_buf.p;
+        ctx->arena2.cap = ctx->arena2_buf.cap;
+        ctx->arena2.used = 0;
+        HIPCHK(hipStreamWaitEvent(s2, ctx->ev_fork, 0));   /* recorded when the attempt started */
+        LCHK(launch_doc_keys(dev_ids, N, ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), s2));
+        /* base-11 keys of 10 digits are < 11^10 < 2^35: five bytes, no probe */
+        /* up to SORT_TILE_MAXN documents: two launches (tile bitonic sort + rank) instead of
+         * two per digit byte */
+        int dc = N <= SORT_TILE_MAXN
+            ? tile_sort_u64(ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), ctx->dkey1.as<uint64_t>(),
+                            ctx->dseq1.as<uint32_t>(), N, ctx->arena2, s2)
+            : radix_sort_u64(ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), ctx->dkey1.as<uint64_t>(),
+                             ctx->dseq1.as<uint32_t>(), N, 0x1Fu, ctx->arena2, s2);
+        LCHK(dc);
+        ctx->order = dc ? ctx->dseq1.as<uint32_t>() : ctx->dseq0.as<uint32_t>();
+        HIPCHK(hipEventRecord(ctx->ev_order, s2));
+    }
+    return 0;
+}
+
 /* The local stages of one attempt (this shard only, no collective): K0, K1, vocabulary,
  * merge, local DF.  Returns 0, 1 to retry with grown capacities, <0 on error.  Also
  * checks that the main arena holds what the stages after the exchange need, so that they
@@ -932,32 +968,9 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     if (st & ST_REC_FULL) { ctx->rec_cap = R_main + R_main / 4 + 4096; retry = true; }
     if (st & ST_PART_FULL) { ctx->part_cap = Q + Q / 4 + 4096; retry = true; }
     if (retry) return 1;
-    /* ---- document order on the side stream (joined before the per-position metadata) ---- */
-    ENSURE(ctx->dkey0, (size_t)N * 8 + 8);
-    ENSURE(ctx->dkey1, (size_t)N * 8 + 8);
-    ENSURE(ctx->dseq0, (size_t)N * 4 + 4);
-    ENSURE(ctx->dseq1, (size_t)N * 4 + 4);
-    {
-        hipStream_t s2 = ctx->stream2;
-        /* the radix histograms, or the tile sort's staging (20 B per document) */
-        const size_t need2 = (size_t)256 * 4 * ((N + 2047) / 2048 + 1) + (size_t)N * 20 + (1u << 20);
-        if (need2 > ctx->arena2_buf.cap && ctx->arena2_buf.ensure(need2) != 0) return TFIDF_E_NOMEM;
-        ctx->arena2.base = (uint8_t*)ctx->arena2_buf.p;
-        ctx->arena2.cap = ctx->arena2_buf.cap;
-        ctx->arena2.used = 0;
-        HIPCHK(hipStreamWaitEvent(s2, ctx->ev_fork, 0));   /* recorded when the attempt started */
-        LCHK(launch_doc_keys(dev_ids, N, ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), s2));
-        /* base-11 keys of 10 digits are < 11^10 < 2^35: five bytes, no probe */
-        /* up to SORT_TILE_MAXN documents: two launches (tile bitonic sort + rank) instead of
-         * two per digit byte */
-        int dc = N <= SORT_TILE_MAXN
-            ? tile_sort_u64(ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), ctx->dkey1.as<uint64_t>(),
-                            ctx->dseq1.as<uint32_t>(), N, ctx->arena2, s2)
-            : radix_sort_u64(ctx->dkey0.as<uint64_t>(), ctx->dseq0.as<uint32_t>(), ctx->dkey1.as<uint64_t>(),
-                             ctx->dseq1.as<uint32_t>(), N, 0x1Fu, ctx->arena2, s2);
-        LCHK(dc);
-        ctx->order = dc ? ctx->dseq1.as<uint32_t>() : ctx->dseq0.as<uint32_t>();
-        HIPCHK(hipEventRecord(ctx->ev_order, s2));
+    if (N > SORT_TILE_MAXN) {   /* see enqueue_doc_order */
+        const int rc = enqueue_doc_order(ctx, dev_ids, N);
+        if (rc) return rc;
     }
     /* ---- vocabulary ---- */
     ctx->V = V;
@@ -1017,6 +1030,10 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     if (V <= 65536u) { ENSURE(ctx->rank16, cap * 2); r16 = ctx->rank16.as<uint16_t>(); }
     LCHK(launch_vocab_rank(ctx->sorted_dense, ctx->vslot.as<uint32_t>(), V, ctx->rank_of_slot.as<uint32_t>(),
                            ctx->slot_of_rank.as<uint32_t>(), r16, s));
+    if (N <= SORT_TILE_MAXN) {   /* see enqueue_doc_order */
+        const int rc = enqueue_doc_order(ctx, dev_ids, N);
+        if (rc) return rc;
+    }
     /* ---- partial documents ---- */
     mark(ctx, S_MERGE);
     uint64_t R_total = R_main;
