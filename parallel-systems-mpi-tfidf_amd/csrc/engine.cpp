@@ -138,6 +138,9 @@ struct tfidf_ctx {
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_order = nullptr;
     hipEvent_t ev_spin = nullptr;   /* the run's host waits (spin_sync) */
+    hipStream_t stream3 = nullptr;  /* the idf table's upload, beside the merge / DF stages */
+    hipEvent_t ev_idf_up = nullptr;
+    bool idf_early = false;         /* this run's table is on its way up stream3 (run_post waits on ev_idf_up) */
     Arena arena2;
     DevBuf arena2_buf;
     /* host-input staging */
@@ -246,6 +249,8 @@ struct tfidf_ctx {
     hipError_t last_err = hipSuccess;
 };
 static void idf_pool_stop(tfidf_ctx* ctx);   /* the per-run idf table's workers (idf_start) */
+static bool idf_done(tfidf_ctx* ctx);
+static void idf_join(tfidf_ctx* ctx);
 /* open contexts in this process: the idf workers of all of them share IDF_POOL threads' worth
  * of work (a group of K shards in one process would otherwise start 8 K of them) */
 static std::atomic<int> g_live_ctx{0};
@@ -310,6 +315,11 @@ static void mark(tfidf_ctx* ctx, int stage) {
     if (ctx->timing == 1 ||
         (ctx->timing == 2 && (stage == S_PREP || stage == S_TOKCOUNT || stage == S_VOCAB || stage == S_NSTAGES)))
         (void)hipEventRecord(ctx->ev[stage], ctx->stream);
+}
+
+/* the run's global df by term rank: the exchange's result, or with one rank the local df */
+static uint32_t* df_of_run(tfidf_ctx* ctx) {
+    return ctx->xp ? ctx->df_global.as<uint32_t>() : ctx->df_local.as<uint32_t>();
 }
 
 /* The run's waits for its own stream (K1's counters, the final status): the host polls an
@@ -388,9 +398,11 @@ int tfidf_open(int device, tfidf_ctx** out) {
     }
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ctx->ev_order, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ctx->ev_spin, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ctx->ev_idf_up, hipEventDisableTiming));
     {
         const char* ic = getenv("TFIDF_IDF_CACHE");
         ctx->idf_cache = ic && ic[0] == '1';
@@ -416,6 +428,8 @@ void tfidf_close(tfidf_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     delete ctx->xp;
     if (ctx->stream2) { (void)hipStreamSynchronize(ctx->stream2); (void)hipStreamDestroy(ctx->stream2); }
+    if (ctx->stream3) { (void)hipStreamSynchronize(ctx->stream3); (void)hipStreamDestroy(ctx->stream3); }
+    if (ctx->ev_idf_up) (void)hipEventDestroy(ctx->ev_idf_up);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_spin) (void)hipEventDestroy(ctx->ev_spin);
     if (ctx->ev_order) (void)hipEventDestroy(ctx->ev_order);
@@ -1034,6 +1048,18 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
         const int rc = enqueue_doc_order(ctx, dev_ids, N);
         if (rc) return rc;
     }
+    /* this run's full idf table (idf_start's workers finish during K1 in practice) goes up
+     * on its own copy stream now, beside the merge and DF stages, instead of inside the idf
+     * stage on the main stream (an SDMA copy of (N+1) doubles: ~35 us there for c2) */
+    if (ctx->idf_pool.busy && !ctx->idf_early && idf_done(ctx)) {
+        idf_join(ctx);
+        ENSURE(ctx->idf_vals, (size_t)(Nt + 1) * 8);
+        HIPCHK(hipMemcpyAsync(ctx->idf_vals.p, ctx->idf_pin, (size_t)(Nt + 1) * 8, hipMemcpyHostToDevice,
+                              ctx->stream3));
+        HIPCHK(hipEventRecord(ctx->ev_idf_up, ctx->stream3));
+        ctx->idf_pin_busy = true;
+        ctx->idf_early = true;
+    }
     /* ---- partial documents ---- */
     mark(ctx, S_MERGE);
     uint64_t R_total = R_main;
@@ -1220,6 +1246,7 @@ static void idf_post(tfidf_ctx* ctx, double* lut, uint64_t Nt, const uint32_t* v
 }
 static int idf_start(tfidf_ctx* ctx, uint64_t Nt) {
     ctx->idf_logs = 0;
+    ctx->idf_early = false;
     ctx->ms_idf_host = ctx->ms_idf_wait = 0;
     if (Nt > IDF_FULL_MAX) return TFIDF_OK;                          /* distinct-df path in run_post */
     if (ctx->idf_cache && ctx->idf_full_n == Nt) return TFIDF_OK;    /* TFIDF_IDF_CACHE=1 */
@@ -1256,6 +1283,12 @@ struct IdfJoin {
     tfidf_ctx* c;
     ~IdfJoin() { idf_join(c); }
 };
+/* the table finished by now? (no wait) */
+static bool idf_done(tfidf_ctx* ctx) {
+    tfidf_ctx::IdfPool& P = ctx->idf_pool;
+    std::lock_guard<std::mutex> lk(P.mu);
+    return P.left == 0;
+}
 
 /* The stages after the DF exchange: idf LUT, document order, score.  They never return 1
  * (run_local checked their scratch before the exchange), so no rank can ever enter the
@@ -1279,7 +1312,10 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
     constexpr uint32_t IDF_SPEC = 16384;
     std::vector<uint32_t> vals;
     if (full_lut) {
-        if (ctx->idf_pool.busy) {   /* this run's table (idf_start): join, upload */
+        if (ctx->idf_early) {       /* on its way up stream3 (run_local) */
+            HIPCHK(hipStreamWaitEvent(s, ctx->ev_idf_up, 0));
+            ctx->idf_full_n = Nt;
+        } else if (ctx->idf_pool.busy) {   /* this run's table (idf_start): join, upload */
             ENSURE(ctx->idf_vals, (size_t)(Nt + 1) * 8);
             idf_join(ctx);
             HIPCHK(hipMemcpyAsync(ctx->idf_vals.p, ctx->idf_pin, (size_t)(Nt + 1) * 8, hipMemcpyHostToDevice, s));
@@ -1292,7 +1328,7 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
         ctx->idf_full_n = 0;   /* idf_vals is rewritten below */
         ENSURE(ctx->present, (Nt + 2) * 4);
         HIPCHK(hipMemsetAsync(ctx->present.p, 0, (Nt + 2) * 4, s));
-        XCHK(launch_df_mark(ctx->df_global.as<uint32_t>(), V, ctx->present.as<uint32_t>(), s));
+        XCHK(launch_df_mark(df_of_run(ctx), V, ctx->present.as<uint32_t>(), s));
         XCHK(scan_excl_u32(ctx->present.as<uint32_t>(), ctx->present.as<uint32_t>(), Nt + 1, ar, s));
         vals_dev = (uint32_t*)ar.get((size_t)(Nt + 2) * 4);
         if (!vals_dev) return TFIDF_E_CAPACITY;   /* checked by run_local: not reachable */
@@ -1368,7 +1404,7 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
     a.rec_slot = ctx->rec_slot.as<uint32_t>();
     a.rec_cnt = ctx->rec_cnt.as<uint32_t>();
     a.rank_of_slot = ctx->rank_of_slot.as<uint32_t>();
-    a.df_of_rank = ctx->df_global.as<uint32_t>();
+    a.df_of_rank = df_of_run(ctx);
     a.idf_idx = full_lut ? nullptr : ctx->present.as<uint32_t>();   /* null: idf indexed by df */
     a.idf = ctx->idf_vals.as<double>();
     a.idf_rank = ctx->idf_rank.as<double>();
@@ -1434,10 +1470,7 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
         if (rc) return rc;
     } else {
         if (rc) return rc;
-        ctx->Vg = ctx->run_V;
-        if (ctx->run_V)
-            HIPCHK(hipMemcpyAsync(ctx->df_global.p, ctx->df_local.p, (size_t)ctx->run_V * 4, hipMemcpyDeviceToDevice,
-                                  ctx->stream));
+        ctx->Vg = ctx->run_V;   /* one rank: the global df is the local one (df_of_run) */
     }
     return run_post(ctx, Nt);
 }
@@ -1710,7 +1743,7 @@ extern "C" int tfidf_fetch(tfidf_ctx* ctx, tfidf_result* r) {
         HIPCHK(hipMemcpyAsync(order.data(), ctx->order, (size_t)N * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(ooff.data(), ctx->out_off.p, ((size_t)N + 1) * 8, hipMemcpyDeviceToHost, s));
     }
-    if (V) HIPCHK(hipMemcpyAsync(r->term_df, ctx->df_global.p, (size_t)V * 4, hipMemcpyDeviceToHost, s));
+    if (V) HIPCHK(hipMemcpyAsync(r->term_df, df_of_run(ctx), (size_t)V * 4, hipMemcpyDeviceToHost, s));
     /* term strings in rank order */
     std::vector<uint4> keys(V);
     std::vector<uint32_t> sor(V);
