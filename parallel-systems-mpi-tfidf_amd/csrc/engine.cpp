@@ -138,6 +138,7 @@ struct tfidf_ctx {
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_order = nullptr;
     hipEvent_t ev_spin = nullptr;   /* the run's host waits (spin_sync) */
+    uint64_t wait_token = 0;        /* the last completion token of a status-words kernel (words_wait) */
     hipStream_t stream3 = nullptr;  /* the idf table's upload, beside the merge / DF stages */
     hipEvent_t ev_idf_up = nullptr;
     bool idf_early = false;         /* this run's table is on its way up stream3 (run_post waits on ev_idf_up) */
@@ -317,6 +318,29 @@ static void mark(tfidf_ctx* ctx, int stage) {
         (void)hipEventRecord(ctx->ev[stage], ctx->stream);
 }
 
+/* Status words into hpin (launch_words_to_host at hpin_dev + at) and the wait for them: in
+ * a single-context process the kernel also writes a completion token after the words and
+ * the host polls that word in pinned memory — no event record on the stream (~5 us each) and
+ * no blocking wake-up; bounded (2 s, then the stream is synchronised, which also reports a
+ * failed kernel).  Several contexts in the process: the stream is synchronised. */
+static hipError_t words_wait(tfidf_ctx* ctx, WordList& wl, uint32_t at, hipStream_t s) {
+    const bool poll = g_live_ctx.load() <= 1;
+    wl.token = poll ? (0x7A5E000000000000ull | ++ctx->wait_token) : 0ull;
+    if (launch_words_to_host(wl, ctx->hpin_dev + at, s)) return hipErrorLaunchFailure;
+    if (!poll) return hipStreamSynchronize(s);
+    volatile uint64_t* tok = ctx->hpin + at + wl.n;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t it = 0; *tok != wl.token; ++it) {
+        if ((it & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+            const hipError_t e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return e;
+            return *tok == wl.token ? hipSuccess : hipErrorUnknown;
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return hipSuccess;
+}
+
 /* the run's global df by term rank: the exchange's result, or with one rank the local df */
 static uint32_t* df_of_run(tfidf_ctx* ctx) {
     return ctx->xp ? ctx->df_global.as<uint32_t>() : ctx->df_local.as<uint32_t>();
@@ -410,7 +434,9 @@ int tfidf_open(int device, tfidf_ctx** out) {
     for (int i = 0; i <= S_NSTAGES; ++i) HIPCHK(hipEventCreate(&ctx->ev[i]));
     if (arena_reset(ctx, 64ull << 20) != 0) { delete ctx; return TFIDF_E_NOMEM; }
     if (ctx->counters.ensure(256) != 0) { delete ctx; return TFIDF_E_NOMEM; }
-    if (hipHostMalloc((void**)&ctx->hpin, 256, hipHostMallocDefault) != hipSuccess) { delete ctx; return TFIDF_E_NOMEM; }
+    /* coherent: the status words a kernel writes (and its completion token) reach the host
+     * without a cache flush at the kernel's end */
+    if (hipHostMalloc((void**)&ctx->hpin, 256, hipHostMallocCoherent) != hipSuccess) { delete ctx; return TFIDF_E_NOMEM; }
     if (hipHostGetDevicePointer((void**)&ctx->hpin_dev, ctx->hpin, 0) != hipSuccess || !ctx->hpin_dev) {
         delete ctx;
         return TFIDF_E_NOMEM;
@@ -952,9 +978,8 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
         wl.src[8] = ctx->dense.as<uint32_t>() + cap;
         wl.bytes[8] = 4;
         wl.n = 9;
-        LCHK(launch_words_to_host(wl, ctx->hpin_dev, s));
+        HIPCHK(words_wait(ctx, wl, 0, s));
     }
-    HIPCHK(spin_sync(ctx, s));
     const uint32_t V = (uint32_t)hp[8];
     unsigned long long hc[8];
     for (int i = 0; i < 8; ++i) hc[i] = hp[i];
@@ -1443,9 +1468,13 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
         wl.src[2] = cnt + 12;
         wl.bytes[2] = 4;
         wl.n = ctx->xp ? 3 : 2;
-        XCHK(launch_words_to_host(wl, ctx->hpin_dev + 24, s));
+        if (ctx->xp) {
+            XCHK(launch_words_to_host(wl, ctx->hpin_dev + 24, s));
+            XSYNC(s);
+        } else {
+            HIPCHK(words_wait(ctx, wl, 24, s));
+        }
     }
-    XSYNC(s);
     ctx->idf_pin_busy = false;   /* the stream has drained */
     const uint32_t st_end = (uint32_t)ctx->hpin[24];
     const uint64_t P = ctx->hpin[25];
@@ -1565,6 +1594,7 @@ extern "C" int tfidf_run(tfidf_ctx* ctx, const tfidf_corpus* in) {
     ctx->ndocs_total = Nt;
     ctx->have_result = true;
     ctx->have_info = true;
+    if (ctx->timing) (void)hipEventSynchronize(ctx->ev[S_NSTAGES]);   /* done on the device; the runtime may not know yet */
     if (ctx->timing == 2) {
         for (int i = 0; i < S_NSTAGES; ++i) ctx->ms_stage[i] = 0;
         float ms = 0;

@@ -158,8 +158,17 @@ int launch_fill_multi(const FillList& l, hipStream_t s) {
  * after the stream synchronises) */
 __global__ void k_words_to_host(const WordList l, uint64_t* dst) {
     const uint32_t i = threadIdx.x;
-    if (i >= l.n) return;
-    dst[i] = l.bytes[i] == 8 ? *(const volatile uint64_t*)l.src[i] : (uint64_t) * (const volatile uint32_t*)l.src[i];
+    if (i < l.n)
+        *(volatile uint64_t*)&dst[i] =
+            l.bytes[i] == 8 ? *(const volatile uint64_t*)l.src[i] : (uint64_t) * (const volatile uint32_t*)l.src[i];
+    if (l.token) {
+        __threadfence_system();   /* every lane's word reaches the host before the token */
+        __syncthreads();
+        if (i == 0) {
+            __threadfence_system();
+            *(volatile uint64_t*)&dst[l.n] = l.token;
+        }
+    }
 }
 int launch_words_to_host(const WordList& l, uint64_t* host_dst, hipStream_t s) {
     if (l.n == 0) return 0;

@@ -135,6 +135,8 @@ struct WordList {
     const void* src[WORDS_MAX];
     uint32_t bytes[WORDS_MAX];   /* 4 or 8 */
     uint32_t n;
+    uint64_t token;              /* nonzero: written to dst[n] after the words (system-scope fence
+                                    between): the host polls it instead of waiting on the stream */
 };
 int launch_words_to_host(const WordList& l, uint64_t* host_dst, hipStream_t s);
 int launch_vocab_rank(const uint32_t* sorted_dense, const uint32_t* vslot, uint32_t V, uint32_t* rank_of_slot,
