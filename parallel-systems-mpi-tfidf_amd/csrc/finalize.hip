@@ -743,11 +743,11 @@ int launch_dense_emit(const uint32_t* dense, uint32_t nb, uint32_t V, const uint
 constexpr uint32_t DFH_RECS = 65535;      /* records per workgroup: u16 bins cannot overflow */
 constexpr uint32_t DFH_MAXV = 65536;
 
-/* LDS-privatised DF histogram: 1024 threads (16 waves, the 100 KB bin array allows one
+/* LDS-privatised DF histogram: 1024 threads (16 waves; at V = 65536 the 128 KB bin array allows one
  * workgroup per CU).  Each thread owns 64 records of the workgroup's range and keeps
  * DFH_B of them in flight at once (slot loads, then rank lookups, then LDS adds): the
  * loop is latency-bound, so the number of dependent round trips is what matters.  The
- * slot -> rank lookups go through a 16 KB direct-mapped LDS cache first (the frequent
+ * slot -> rank lookups go through a 32 KB direct-mapped LDS cache first (the frequent
  * terms recur in every document of the workgroup's range); only its misses send a
  * random L2 request into the 2-byte map (c2 DF 0.385 -> 0.344 ms, profiles/r04_k1_ab_c2.txt). */
 constexpr int DFH_NT = 1024;
@@ -755,8 +755,12 @@ constexpr int DFH_NT = 1024;
 #define DFH_B_N 16
 #endif
 constexpr int DFH_B = DFH_B_N;
-constexpr uint32_t DFH_CK = 2048;          /* LDS slot -> rank cache entries (16 KB) */
-__device__ __forceinline__ uint32_t dfh_cslot(uint32_t slot) { return (slot * 0x9E3779B1u) >> (32 - 11); }
+#ifndef DFH_CK_BITS
+#define DFH_CK_BITS 12
+#endif
+constexpr uint32_t DFH_CK = 1u << DFH_CK_BITS;   /* LDS slot -> rank cache entries (4096: 32 KB; with V = 65536 the
+                                                    bins + cache fill the 160 KB of LDS exactly) */
+__device__ __forceinline__ uint32_t dfh_cslot(uint32_t slot) { return (slot * 0x9E3779B1u) >> (32 - DFH_CK_BITS); }
 __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ rec_slot, uint64_t nrec,
                                                         const uint32_t* __restrict__ nrec_extra,
                                                         const uint32_t* __restrict__ rank_of_slot,

@@ -277,6 +277,25 @@ def test_doc_with_more_pairs_than_lds_table(engine):
     check_vs_oracle(engine, *docs_to_arrays(docs))
 
 
+@pytest.mark.parametrize("V", [65535, 65536, 65537])
+def test_df_histogram_vocabulary_boundary(engine, V):
+    """Vocabularies at the LDS histogram's limit (finalize.hip DFH_MAXV): at V = 65536 the
+    u16 bins (128 KB) and the slot -> rank cache (32 KB) fill the 160 KB of LDS exactly;
+    V = 65537 takes the partitioned global-atomic path.  Every term occurs at least once and
+    16 frequent terms occur in every document (the cache's hits)."""
+    rng = np.random.default_rng(V)
+    words = _distinct_words(V, rng)
+    hot = [words[i] for i in rng.choice(V, 16, replace=False)]
+    docs = []
+    for part in np.array_split(rng.permutation(V), 1500):
+        toks = [words[i] for i in part] + hot + [words[i] for i in rng.integers(0, V, 8)]
+        rng.shuffle(toks)
+        docs.append(b" ".join(toks) + b"\n")
+    res = check_vs_oracle(engine, *docs_to_arrays(docs))
+    assert engine.info()["nterms"] == V
+    assert int(np.max(res["df"])) == len(docs)
+
+
 def test_complete_doc_over_k5_limit(engine):
     """~2500 distinct terms in a 25 KB document: complete inside one chunk but larger than
     K5's in-LDS sort, so it is routed through the partial merge."""
