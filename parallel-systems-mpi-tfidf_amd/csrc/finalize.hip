@@ -1466,8 +1466,11 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
             if (lane == 0) G(a.large_list)[atomicAdd(a.large_count, 1u)] = i;
             continue;
         }
+#ifndef K5_SCATTER
+#define K5_SCATTER 0
+#endif
 #ifndef K5_NO_WIDE
-        if constexpr (WIDE) if (wide) {
+        if constexpr (WIDE || K5_SCATTER) if (wide || gmax <= K5_GROUP_MAX) {
             /* wide ranks (V > 2^21): keys hold the rank bits below the bucket and the index;
              * each lane counts its own elements' smaller bucket mates and stores its pairs
              * at their output positions directly (as the counting path does) */
@@ -1482,7 +1485,7 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
             constexpr int EB = K5_EB;
 #pragma unroll
             for (int q0 = 0; q0 < K5_RQ; q0 += EB) {
-                if (64u * q0 >= n) break;
+                if (64u * q0 >= n) continue;
                 uint32_t pos[EB], cnt[EB];
                 double idf[EB];
 #pragma unroll
@@ -1529,6 +1532,7 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
                          rb, ob, ds);
             continue;
         }
+#if !K5_SCATTER
 #pragma unroll
         for (int q = 0; q < K5_RQ; ++q) {
             const uint32_t j = 64u * q + lane;
@@ -1585,6 +1589,7 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
     }  /* persistent loop */
 }
 
