@@ -1466,11 +1466,8 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
             if (lane == 0) G(a.large_list)[atomicAdd(a.large_count, 1u)] = i;
             continue;
         }
-#ifndef K5_SCATTER
-#define K5_SCATTER 0
-#endif
 #ifndef K5_NO_WIDE
-        if constexpr (WIDE || K5_SCATTER) if (wide || gmax <= K5_GROUP_MAX) {
+        if constexpr (WIDE) if (wide) {
             /* wide ranks (V > 2^21): keys hold the rank bits below the bucket and the index;
              * each lane counts its own elements' smaller bucket mates and stores its pairs
              * at their output positions directly (as the counting path does) */
@@ -1532,7 +1529,6 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
                          rb, ob, ds);
             continue;
         }
-#if !K5_SCATTER
 #pragma unroll
         for (int q = 0; q < K5_RQ; ++q) {
             const uint32_t j = 64u * q + lane;
@@ -1589,7 +1585,6 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#endif
     }  /* persistent loop */
 }
 
