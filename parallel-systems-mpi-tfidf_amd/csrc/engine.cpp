@@ -142,6 +142,11 @@ struct tfidf_ctx {
     hipStream_t stream3 = nullptr;  /* the idf table's upload, beside the merge / DF stages */
     hipEvent_t ev_idf_up = nullptr;
     bool idf_early = false;         /* this run's table is on its way up stream3 (run_post waits on ev_idf_up) */
+    /* split DF (V <= 65536 with partial records): the main records' histogram runs on stream2
+     * beside the merge stage, the merged records' is added on the main stream after it */
+    bool df_split = true;           /* env TFIDF_DF_SPLIT=0: one DF pass after the merge */
+    hipEvent_t ev_vrank = nullptr, ev_dfmain = nullptr;
+    DevBuf df_scratch;
     Arena arena2;
     DevBuf arena2_buf;
     /* host-input staging */
@@ -400,6 +405,8 @@ int tfidf_open(int device, tfidf_ctx** out) {
     ctx->xagg_table = kxa && !strcmp(kxa, "table");
     const char* kxb = getenv("TFIDF_XB_STAGE_MAX");
     ctx->xb_stage_max = kxb ? (uint32_t)atoi(kxb) : ~0u;
+    const char* kds = getenv("TFIDF_DF_SPLIT");
+    ctx->df_split = !(kds && !strcmp(kds, "0"));
     const char* kn = getenv("TFIDF_TEST_XNOMEM_RANK");
     ctx->xnomem_rank = kn ? atoi(kn) : -1;
     /* diagnostics: initial vocabulary capacity (power of two) and the loads it may reach
@@ -427,6 +434,8 @@ int tfidf_open(int device, tfidf_ctx** out) {
     HIPCHK(hipEventCreateWithFlags(&ctx->ev_order, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ctx->ev_spin, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ctx->ev_idf_up, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ctx->ev_vrank, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ctx->ev_dfmain, hipEventDisableTiming));
     {
         const char* ic = getenv("TFIDF_IDF_CACHE");
         ctx->idf_cache = ic && ic[0] == '1';
@@ -456,6 +465,8 @@ void tfidf_close(tfidf_ctx* ctx) {
     if (ctx->stream2) { (void)hipStreamSynchronize(ctx->stream2); (void)hipStreamDestroy(ctx->stream2); }
     if (ctx->stream3) { (void)hipStreamSynchronize(ctx->stream3); (void)hipStreamDestroy(ctx->stream3); }
     if (ctx->ev_idf_up) (void)hipEventDestroy(ctx->ev_idf_up);
+    if (ctx->ev_vrank) (void)hipEventDestroy(ctx->ev_vrank);
+    if (ctx->ev_dfmain) (void)hipEventDestroy(ctx->ev_dfmain);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_spin) (void)hipEventDestroy(ctx->ev_spin);
     if (ctx->ev_order) (void)hipEventDestroy(ctx->ev_order);
@@ -469,6 +480,7 @@ void tfidf_close(tfidf_ctx* ctx) {
     for (int i = 0; i < WR_GROUPS; ++i)
         if (ctx->wr_fmt[i]) (void)hipEventDestroy(ctx->wr_fmt[i]);
     ctx->arena2_buf.release();
+    ctx->df_scratch.release();
     DevBuf* bufs[] = {&ctx->arena_buf, &ctx->in_bytes, &ctx->in_off, &ctx->in_ids, &ctx->syn_bytes, &ctx->syn_off,
                       &ctx->syn_ids, &ctx->syn_ntok, &ctx->syn_blkfirst, &ctx->syn_blkbytes, &ctx->syn_cdf,
                       &ctx->chunk_start, &ctx->chunk_doc, &ctx->vkeys, &ctx->vrep, &ctx->rec_slot, &ctx->rec_cnt,
@@ -1073,6 +1085,29 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
         const int rc = enqueue_doc_order(ctx, dev_ids, N);
         if (rc) return rc;
     }
+    /* split DF: with partial records to merge, the main records' histogram (which needs only
+     * the term ranks) starts on stream2 now and runs beside the merge stage's short
+     * launches; the merged records are added after the merge (accumulate pass below) */
+    const bool df_split = ctx->df_split && Q && R_main && V <= 65536u;
+    ENSURE(ctx->df_local, (size_t)V * 4 + 4);
+    ENSURE(ctx->df_global, (size_t)V * 4 + 4);
+    if (df_split) {
+        if (R_main + Q > ctx->rec_cap) {   /* the merge's growth, done before stream2 reads the records */
+            uint64_t ncap = R_main + Q + (R_main + Q) / 8 + 4096;
+            if (ctx->rec_slot.grow_keep(ncap * 4, R_main * 4, s) || ctx->rec_cnt.grow_keep(ncap * 4, R_main * 4, s))
+                return TFIDF_E_NOMEM;
+            ctx->rec_cap = ncap;
+        }
+        ENSURE(ctx->df_scratch, df_hist_scratch(R_main, V));
+        Arena da;
+        da.base = (uint8_t*)ctx->df_scratch.p;
+        da.cap = ctx->df_scratch.cap;
+        HIPCHK(hipEventRecord(ctx->ev_vrank, s));
+        HIPCHK(hipStreamWaitEvent(ctx->stream2, ctx->ev_vrank, 0));
+        LCHK(launch_df_hist(ctx->rec_slot.as<uint32_t>(), R_main, nullptr, R_main, ctx->rank_of_slot.as<uint32_t>(),
+                            r16, V, cap, (uint32_t*)(cnt + 3), ctx->df_local.as<uint32_t>(), da, ctx->stream2));
+        HIPCHK(hipEventRecord(ctx->ev_dfmain, ctx->stream2));
+    }
     /* this run's full idf table (idf_start's workers finish during K1 in practice) goes up
      * on its own copy stream now, beside the merge and DF stages, instead of inside the idf
      * stage on the main stream (an SDMA copy of (N+1) doubles: ~35 us there for c2) */
@@ -1187,13 +1222,17 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     }
     /* ---- DF ---- */
     mark(ctx, S_DF);
-    ENSURE(ctx->df_local, (size_t)V * 4 + 4);
-    ENSURE(ctx->df_global, (size_t)V * 4 + 4);
-    /* also rewrites every record's slot as its term rank (K5 then needs no rank gather) */
-    LCHK(launch_df_hist(ctx->rec_slot.as<uint32_t>(), R_main, merged_count, R_total,
-                        ctx->rank_of_slot.as<uint32_t>(),
-                        V <= 65536u ? ctx->rank16.as<uint16_t>() : nullptr, V, cap,
-                        (uint32_t*)(cnt + 3), ctx->df_local.as<uint32_t>(), ar, s));
+    if (df_split) {   /* the merged records (term ranks) added to the main records' df */
+        HIPCHK(hipStreamWaitEvent(s, ctx->ev_dfmain, 0));
+        LCHK(launch_df_hist(ctx->rec_slot.as<uint32_t>() + R_main, 0, merged_count, R_total - R_main,
+                            ctx->rank_of_slot.as<uint32_t>(), r16, V, cap, (uint32_t*)(cnt + 3),
+                            ctx->df_local.as<uint32_t>(), ar, s, true));
+    } else {
+        /* also rewrites every record's slot as its term rank (K5 then needs no rank gather) */
+        LCHK(launch_df_hist(ctx->rec_slot.as<uint32_t>(), R_main, merged_count, R_total,
+                            ctx->rank_of_slot.as<uint32_t>(), r16, V, cap, (uint32_t*)(cnt + 3),
+                            ctx->df_local.as<uint32_t>(), ar, s));
+    }
     ctx->run_V = V;
     ctx->run_cap = cap;
     ctx->run_R_total = R_total;

@@ -976,37 +976,54 @@ __global__ __launch_bounds__(DFS_NT) void k_dfs_slice(const uint32_t* __restrict
     for (uint32_t j = threadIdx.x; j < sw; j += DFS_NT) df[s0 + j] = sbins[j];
 }
 
+/* the LDS histogram's split of nrec_max records: records per workgroup (<= DFH_RECS) so
+ * that the workgroups fill whole waves of the CUs' resident slots (c2: 946 x 65535 records
+ * = 3.7 waves -> 1024 x 60548, no tail) */
+static void df_lds_plan(uint64_t nrec_max, uint32_t V, uint32_t* per_out, uint32_t* nparts_out) {
+    uint32_t nparts = (uint32_t)((nrec_max + DFH_RECS - 1) / DFH_RECS);
+    const uint32_t W = (V + 1) / 2;
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+    }
+    const uint64_t wg_lds = (uint64_t)((W + 1) & ~1u) * 4 + (uint64_t)DFH_CK * 8;
+    const uint64_t per_cu = (uint64_t)163840 / wg_lds >= 2 ? 2 : 1;   /* 1024-thread workgroups */
+    const uint64_t slots = (uint64_t)ncu * per_cu;
+    const uint64_t full = (nparts + slots - 1) / slots * slots;
+    uint32_t per = (uint32_t)((nrec_max + full - 1) / full);
+    if (per < 8192u) per = 8192u;   /* small inputs: few workgroups (each clears and writes W words) */
+    *per_out = per;
+    *nparts_out = (uint32_t)((nrec_max + per - 1) / per);
+}
+
+size_t df_hist_scratch(uint64_t nrec_max, uint32_t V) {
+    if (V == 0 || V > DFH_MAXV || nrec_max == 0) return 0;
+    uint32_t per = 0, nparts = 0;
+    df_lds_plan(nrec_max, V, &per, &nparts);
+    return (size_t)nparts * ((V + 1) / 2) * 4 + 256;
+}
+
 int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra, uint64_t nrec_max,
                    const uint32_t* rank_of_slot, const uint16_t* rank16, uint32_t V, uint64_t slot_cap,
-                   uint32_t* status, uint32_t* df, Arena& ar, hipStream_t s) {
+                   uint32_t* status, uint32_t* df, Arena& ar, hipStream_t s, bool accumulate) {
     /* records [0, nrec) hold vocabulary slots (K1), the merged ones after them term ranks */
     const uint64_t ranked_from = nrec;
     if (V == 0) return 0;
     if (nrec_max < nrec) nrec_max = nrec;
-    if (nrec_max == 0) return hipMemsetAsync(df, 0, (size_t)V * 4, s) == hipSuccess ? 0 : -1;
+    if (accumulate && (V > DFH_MAXV)) return -1;   /* adds into df: the LDS histogram only */
+    if (nrec_max == 0)
+        return accumulate ? 0 : hipMemsetAsync(df, 0, (size_t)V * 4, s) == hipSuccess ? 0 : -1;
     if (V <= DFH_MAXV) {
-        uint32_t nparts = (uint32_t)((nrec_max + DFH_RECS - 1) / DFH_RECS);
-        uint32_t W = (V + 1) / 2;
-        /* records per workgroup (<= DFH_RECS): the workgroups fill whole waves of the CUs'
-         * resident slots (c2: 946 x 65535 records = 3.7 waves -> 1024 x 60548, no tail) */
-        static int ncu = 0;
-        if (!ncu) {
-            int dev = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-                ncu = 256;
-        }
-        const uint64_t wg_lds = (uint64_t)((W + 1) & ~1u) * 4 + (uint64_t)DFH_CK * 8;
-        const uint64_t per_cu = (uint64_t)163840 / wg_lds >= 2 ? 2 : 1;   /* 1024-thread workgroups */
-        const uint64_t slots = (uint64_t)ncu * per_cu;
-        const uint64_t full = (nparts + slots - 1) / slots * slots;
-        uint32_t per = (uint32_t)((nrec_max + full - 1) / full);
-        if (per < 8192u) per = 8192u;   /* small inputs: few workgroups (each clears and writes W words) */
-        nparts = (uint32_t)((nrec_max + per - 1) / per);
+        uint32_t per = 0, nparts = 0;
+        df_lds_plan(nrec_max, V, &per, &nparts);
+        const uint32_t W = (V + 1) / 2;
         size_t m = ar.mark();
         uint32_t* part = (uint32_t*)ar.get((size_t)nparts * W * 4);
         if (!part) return -2;
-        if (hipMemsetAsync(df, 0, (size_t)V * 4, s) != hipSuccess) return -1;
+        if (!accumulate && hipMemsetAsync(df, 0, (size_t)V * 4, s) != hipSuccess) return -1;
         const size_t lds = (size_t)((W + 1) & ~1u) * 4 + (size_t)DFH_CK * 8;
         k_df_hist_lds<<<nparts, DFH_NT, lds, s>>>(rec_slot, nrec, nrec_extra, rank_of_slot, rank16, V, slot_cap,
                                                              ranked_from, status, per, part);
