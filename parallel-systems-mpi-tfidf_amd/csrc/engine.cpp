@@ -142,7 +142,7 @@ struct tfidf_ctx {
     hipStream_t stream3 = nullptr;  /* the idf table's upload, beside the merge / DF stages */
     hipEvent_t ev_idf_up = nullptr;
     bool idf_early = false;         /* this run's table is on its way up stream3 (run_post waits on ev_idf_up) */
-    /* split DF (V <= 65536 with partial records): the main records' histogram runs on stream2
+    /* split DF (runs with partial records): the main records' histogram runs on stream2
      * beside the merge stage, the merged records' is added on the main stream after it */
     bool df_split = true;           /* env TFIDF_DF_SPLIT=0: one DF pass after the merge */
     hipEvent_t ev_vrank = nullptr, ev_dfmain = nullptr;
@@ -1088,7 +1088,7 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     /* split DF: with partial records to merge, the main records' histogram (which needs only
      * the term ranks) starts on stream2 now and runs beside the merge stage's short
      * launches; the merged records are added after the merge (accumulate pass below) */
-    const bool df_split = ctx->df_split && Q && R_main && V <= 65536u;
+    const bool df_split = ctx->df_split && Q && R_main;
     ENSURE(ctx->df_local, (size_t)V * 4 + 4);
     ENSURE(ctx->df_global, (size_t)V * 4 + 4);
     if (df_split) {

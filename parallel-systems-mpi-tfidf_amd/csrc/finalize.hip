@@ -956,7 +956,8 @@ __global__ __launch_bounds__(DFS_NT) void k_dfs_scatter(const uint32_t* __restri
     }
 }
 __global__ __launch_bounds__(DFS_NT) void k_dfs_slice(const uint32_t* __restrict__ part, const uint32_t* __restrict__ off,
-                                                      uint32_t ntiles, uint32_t V, uint32_t* __restrict__ df) {
+                                                      uint32_t ntiles, uint32_t V, uint32_t* __restrict__ df,
+                                                      bool accumulate) {
     extern __shared__ uint32_t sbins[];
     const uint32_t k = blockIdx.x, s0 = k * DFS_SLICE;
     const uint32_t sw = V - s0 < DFS_SLICE ? V - s0 : DFS_SLICE;
@@ -973,7 +974,7 @@ __global__ __launch_bounds__(DFS_NT) void k_dfs_slice(const uint32_t* __restrict
             if (r[q] != 0xFFFFFFFFu) atomicAdd(&sbins[r[q] - s0], 1u);
     }
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < sw; j += DFS_NT) df[s0 + j] = sbins[j];
+    for (uint32_t j = threadIdx.x; j < sw; j += DFS_NT) df[s0 + j] = accumulate ? df[s0 + j] + sbins[j] : sbins[j];
 }
 
 /* the LDS histogram's split of nrec_max records: records per workgroup (<= DFH_RECS) so
@@ -1000,10 +1001,17 @@ static void df_lds_plan(uint64_t nrec_max, uint32_t V, uint32_t* per_out, uint32
 }
 
 size_t df_hist_scratch(uint64_t nrec_max, uint32_t V) {
-    if (V == 0 || V > DFH_MAXV || nrec_max == 0) return 0;
-    uint32_t per = 0, nparts = 0;
-    df_lds_plan(nrec_max, V, &per, &nparts);
-    return (size_t)nparts * ((V + 1) / 2) * 4 + 256;
+    if (V == 0 || nrec_max == 0) return 256;
+    if (V <= DFH_MAXV) {
+        uint32_t per = 0, nparts = 0;
+        df_lds_plan(nrec_max, V, &per, &nparts);
+        return (size_t)nparts * ((V + 1) / 2) * 4 + 256;
+    }
+    /* the sliced pass: slice counts per tile (+ their scan's tile sums) and the ranks
+     * grouped by slice */
+    const uint64_t nsl = ((uint64_t)V + DFS_SLICE - 1) / DFS_SLICE;
+    const uint64_t ntiles = (nrec_max + DFS_TILE - 1) / DFS_TILE;
+    return (size_t)((ntiles * nsl + 1) * 4 + nrec_max * 4 + (ntiles * nsl) / 16 + 8192 + 1024);
 }
 
 int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra, uint64_t nrec_max,
@@ -1013,7 +1021,6 @@ int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra
     const uint64_t ranked_from = nrec;
     if (V == 0) return 0;
     if (nrec_max < nrec) nrec_max = nrec;
-    if (accumulate && (V > DFH_MAXV)) return -1;   /* adds into df: the LDS histogram only */
     if (nrec_max == 0)
         return accumulate ? 0 : hipMemsetAsync(df, 0, (size_t)V * 4, s) == hipSuccess ? 0 : -1;
     if (V <= DFH_MAXV) {
@@ -1048,14 +1055,14 @@ int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra
                 k_dfs_scatter<<<(uint32_t)ntiles, DFS_NT, 0, s>>>(rec_slot, nrec, nrec_extra, V, nsl, cnt, part);
                 if (ok()) return -1;
                 k_dfs_slice<<<nsl, DFS_NT, (size_t)(V < DFS_SLICE ? V : DFS_SLICE) * 4, s>>>(part, cnt, (uint32_t)ntiles,
-                                                                                           V, df);
+                                                                                           V, df, accumulate);
                 ar.release(m);
                 return ok();
             }
         }
     }
 #endif
-    if (hipMemsetAsync(df, 0, (size_t)V * 4, s) != hipSuccess) return -1;
+    if (!accumulate && hipMemsetAsync(df, 0, (size_t)V * 4, s) != hipSuccess) return -1;
     k_df_hist_atomic<<<4096, NT, 0, s>>>(rec_slot, nrec, nrec_extra, rank_of_slot, slot_cap, ranked_from, V, status,
                                          df);
     return ok();

@@ -168,12 +168,12 @@ int launch_dense_emit(const uint32_t* dense, uint32_t nb, uint32_t V, const uint
                       uint32_t* rec_slot, uint32_t* rec_cnt, uint64_t* doc_recoff, uint32_t* doc_npairs,
                       uint8_t* doc_flags, Arena& ar, hipStream_t s);
 
-/* DF.  accumulate: add into df instead of overwriting it (V <= 65536 only: the split DF of
- * a run with partial records, whose main records are counted beside the merge stage) */
+/* DF.  accumulate: add into df instead of overwriting it (the split DF of a run with
+ * partial records, whose main records are counted beside the merge stage) */
 int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra, uint64_t nrec_max,
                    const uint32_t* rank_of_slot, const uint16_t* rank16, uint32_t V, uint64_t slot_cap,
                    uint32_t* status, uint32_t* df, Arena& ar, hipStream_t s, bool accumulate = false);
-/* device scratch launch_df_hist takes from its arena for V <= 65536 (0 otherwise) */
+/* device scratch launch_df_hist takes from its arena (an upper bound) */
 size_t df_hist_scratch(uint64_t nrec_max, uint32_t V);
 int launch_df_mark(const uint32_t* df, uint32_t V, uint32_t* present, hipStream_t s);
 int launch_df_list(const uint32_t* present_scan, uint64_t nvals, uint32_t* vals, hipStream_t s);

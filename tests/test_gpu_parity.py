@@ -341,18 +341,18 @@ def test_vocabulary_table_growth(monkeypatch, cap, load):
 
 
 @pytest.mark.parametrize("split", ["1", "0"])
-@pytest.mark.parametrize("cfg,scale", [("c2", 0.002), ("c5", 0.002)])
+@pytest.mark.parametrize("cfg,scale", [("c2", 0.002), ("c5", 0.002), ("c4", 0.002)])
 def test_df_split_pass(monkeypatch, split, cfg, scale):
-    """With partial records to merge (V <= 65536), the main records' DF pass runs on the side
-    stream beside the merge stage and the merged records are added after it (engine.cpp
-    run_local); TFIDF_DF_SPLIT=0 keeps one pass after the merge.  Both agree with the oracle."""
+    """With partial records to merge, the main records' DF pass runs on the side stream beside
+    the merge stage and the merged records are added after it (engine.cpp run_local; the LDS
+    histogram for V <= 65536, the sliced pass above: c4); TFIDF_DF_SPLIT=0 keeps one pass
+    after the merge.  Both agree with the oracle."""
     monkeypatch.setenv("TFIDF_DF_SPLIT", split)
     p = tfidf_configs.plan(cfg, scale=scale)
     data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
     with tfidf_abi.Engine(0) as e:
         check_vs_oracle(e, data, off, p["doc_ids"], p["ndocs_total"])
         info = e.info()
-    assert info["nterms"] <= 65536
     if cfg == "c5":   # its long documents always span chunks
         assert info["partial_records"] > 0
 
