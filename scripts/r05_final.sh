@@ -44,9 +44,11 @@ else
     done
     echo "traffic $n done"
   }
+  if [ "${SKIP_TRAFFIC:-0}" != 1 ]; then   # SKIP_TRAFFIC=1: counters and trace only (K1 unchanged)
   run_traffic c2 --config c2 && run_traffic c4 --config c4 && run_traffic c5 --config c5 && \
   run_traffic c2_g2 --config c2 --shard-of 0/2 && run_traffic c2_g4 --config c2 --shard-of 0/4 && \
   run_traffic c2_g8 --config c2 --shard-of 0/8 && run_traffic c3_strong_g8 --config c3 --strong --shard-of 0/8 || exit 1
+  fi
   timeout -s KILL 150 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_c2 -o kt -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-emit --no-probe > $OUT/kt_c2.log 2>&1 || { echo "trace failed"; exit 1; }
   echo "trace done"
 fi
