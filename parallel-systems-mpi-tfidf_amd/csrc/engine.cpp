@@ -145,6 +145,7 @@ struct tfidf_ctx {
     /* split DF (runs with partial records): the main records' histogram runs on stream2
      * beside the merge stage, the merged records' is added on the main stream after it */
     bool df_split = true;           /* env TFIDF_DF_SPLIT=0: one DF pass after the merge */
+    bool doc_order_s3 = false;      /* env TFIDF_DOC_ORDER_S3=1 (A/B): a small run's document order on stream3 after the DF fork */
     hipEvent_t ev_vrank = nullptr, ev_dfmain = nullptr;
     DevBuf df_scratch;
     Arena arena2;
@@ -407,6 +408,8 @@ int tfidf_open(int device, tfidf_ctx** out) {
     ctx->xb_stage_max = kxb ? (uint32_t)atoi(kxb) : ~0u;
     const char* kds = getenv("TFIDF_DF_SPLIT");
     ctx->df_split = !(kds && !strcmp(kds, "0"));
+    const char* kdo = getenv("TFIDF_DOC_ORDER_S3");
+    ctx->doc_order_s3 = kdo && !strcmp(kdo, "1");
     const char* kn = getenv("TFIDF_TEST_XNOMEM_RANK");
     ctx->xnomem_rank = kn ? atoi(kn) : -1;
     /* diagnostics: initial vocabulary capacity (power of two) and the loads it may reach
@@ -834,13 +837,12 @@ static int exchange_df(tfidf_ctx* ctx, int local_rc, uint32_t V) {
  * vocabulary stage's launches for up to SORT_TILE_MAXN documents (two short launches: the
  * device runs the vocabulary stage while the host enqueues them; c2 +0.9 %, while c5's
  * 1e6-document sort beside its merge stage slowed that by 0.07 ms). */
-static int enqueue_doc_order(tfidf_ctx* ctx, const uint32_t* dev_ids, uint32_t N) {
+static int enqueue_doc_order(tfidf_ctx* ctx, const uint32_t* dev_ids, uint32_t N, hipStream_t s2) {
     ENSURE(ctx->dkey0, (size_t)N * 8 + 8);
     ENSURE(ctx->dkey1, (size_t)N * 8 + 8);
     ENSURE(ctx->dseq0, (size_t)N * 4 + 4);
     ENSURE(ctx->dseq1, (size_t)N * 4 + 4);
     {
-        hipStream_t s2 = ctx->stream2;
         /* the radix histograms, or the tile sort's staging (20 B per document) */
         const size_t need2 = (size_t)256 * 4 * ((N + 2047) / 2048 + 1) + (size_t)N * 20 + (1u << 20);
         if (need2 > ctx->arena2_buf.cap && ctx->arena2_buf.ensure(need2) != 0) return TFIDF_E_NOMEM;
@@ -1020,7 +1022,7 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     if (st & ST_PART_FULL) { ctx->part_cap = Q + Q / 4 + 4096; retry = true; }
     if (retry) return 1;
     if (N > SORT_TILE_MAXN) {   /* see enqueue_doc_order */
-        const int rc = enqueue_doc_order(ctx, dev_ids, N);
+        const int rc = enqueue_doc_order(ctx, dev_ids, N, ctx->stream2);
         if (rc) return rc;
     }
     /* ---- vocabulary ---- */
@@ -1081,8 +1083,8 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     if (V <= 65536u) { ENSURE(ctx->rank16, cap * 2); r16 = ctx->rank16.as<uint16_t>(); }
     LCHK(launch_vocab_rank(ctx->sorted_dense, ctx->vslot.as<uint32_t>(), V, ctx->rank_of_slot.as<uint32_t>(),
                            ctx->slot_of_rank.as<uint32_t>(), r16, s));
-    if (N <= SORT_TILE_MAXN) {   /* see enqueue_doc_order */
-        const int rc = enqueue_doc_order(ctx, dev_ids, N);
+    if (N <= SORT_TILE_MAXN && !ctx->doc_order_s3) {   /* see enqueue_doc_order */
+        const int rc = enqueue_doc_order(ctx, dev_ids, N, ctx->stream2);
         if (rc) return rc;
     }
     /* split DF: with partial records to merge, the main records' histogram (which needs only
@@ -1107,6 +1109,10 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
         LCHK(launch_df_hist(ctx->rec_slot.as<uint32_t>(), R_main, nullptr, R_main, ctx->rank_of_slot.as<uint32_t>(),
                             r16, V, cap, (uint32_t*)(cnt + 3), ctx->df_local.as<uint32_t>(), da, ctx->stream2));
         HIPCHK(hipEventRecord(ctx->ev_dfmain, ctx->stream2));
+    }
+    if (N <= SORT_TILE_MAXN && ctx->doc_order_s3) {   /* A/B: beside the merge / DF stages */
+        const int rc = enqueue_doc_order(ctx, dev_ids, N, ctx->stream3);
+        if (rc) return rc;
     }
     /* this run's full idf table (idf_start's workers finish during K1 in practice) goes up
      * on its own copy stream now, beside the merge and DF stages, instead of inside the idf
