@@ -116,6 +116,7 @@ struct tfidf_ctx {
     int k1_mode = 0;        /* 0 auto (k_tokcount_sl up to K1_ST_MAX_CAP slots, k_tokcount_vs beyond),
                                1 round-1 kernel (TFIDF_K1=vs), 2 general K1 (TFIDF_K1=general),
                                3 k_tokcount_sl (TFIDF_K1=sl) — cross-checks and A/B timing;
+                               4 the two-pass form of k_tokcount_sl (TFIDF_K1=2p: k_tok_resolve + k_tok_count);
                                round 3's k_tokcount_st was retired in round 5 (git history) */
     bool stamps_on = false; /* env TFIDF_STAMPS=1 with the diagnostic library build */
     int xfail_rank = -1;    /* env TFIDF_TEST_XFAIL_RANK (tests): this rank fails inside the exchange of
@@ -126,6 +127,7 @@ struct tfidf_ctx {
     DevBuf stamps;
     bool k1_vs = false;     /* last run used the slot-keyed kernel (default) */
     bool k1_sl = false;     /* ... or tokcount_sl (else tokcount_vs) */
+    bool k1_2p = false;     /* ... in its two-pass form (token stream between the passes) */
     uint64_t sl_maxcap = K1_ST_MAX_CAP;   /* env TFIDF_SL_MAXCAP: tokcount_sl up to this many vocabulary slots */
     K1Out* k1out_host = nullptr;   /* pinned: tokcount_sl's output block, copied to k1out_dev per run */
     DevBuf k1out_dev;
@@ -148,6 +150,7 @@ struct tfidf_ctx {
     bool doc_order_s3 = false;      /* env TFIDF_DOC_ORDER_S3=1 (A/B): a small run's document order on stream3 after the DF fork */
     hipEvent_t ev_vrank = nullptr, ev_dfmain = nullptr;
     DevBuf df_scratch;
+    size_t df_scratch_min = 0;      /* grown when the split DF pass reported a shortfall (retried) */
     Arena arena2;
     DevBuf arena2_buf;
     /* host-input staging */
@@ -156,6 +159,7 @@ struct tfidf_ctx {
     DevBuf syn_bytes, syn_off, syn_ids, syn_ntok, syn_blkfirst, syn_blkbytes, syn_cdf;
     /* stage buffers */
     DevBuf chunk_start, chunk_doc;
+    DevBuf tok_stream, chunk_tok, chunk_caps, chunk_ntok, doc_tok;   /* K1 two-pass form */
     DevBuf vkeys, vrep;
     /* vocabulary table: K1 is measurably faster at low load (fewer displaced keys behind
      * the two slots it loads per token): 1M slots (16 MB) to start, x4 past 12 % load */
@@ -389,6 +393,7 @@ int tfidf_open(int device, tfidf_ctx** out) {
     if (km && !strcmp(km, "general")) ctx->k1_mode = 2;
     if (km && !strcmp(km, "vs")) ctx->k1_mode = 1;
     if (km && !strcmp(km, "sl")) ctx->k1_mode = 3;
+    if (km && !strcmp(km, "2p")) ctx->k1_mode = 4;
     {
         const char* sm = getenv("TFIDF_SL_MAXCAP");
         const unsigned long long v = sm ? strtoull(sm, nullptr, 0) : 0ull;
@@ -486,7 +491,8 @@ void tfidf_close(tfidf_ctx* ctx) {
     ctx->df_scratch.release();
     DevBuf* bufs[] = {&ctx->arena_buf, &ctx->in_bytes, &ctx->in_off, &ctx->in_ids, &ctx->syn_bytes, &ctx->syn_off,
                       &ctx->syn_ids, &ctx->syn_ntok, &ctx->syn_blkfirst, &ctx->syn_blkbytes, &ctx->syn_cdf,
-                      &ctx->chunk_start, &ctx->chunk_doc, &ctx->vkeys, &ctx->vrep, &ctx->rec_slot, &ctx->rec_cnt,
+                      &ctx->chunk_start, &ctx->chunk_doc, &ctx->tok_stream, &ctx->chunk_tok, &ctx->chunk_caps,
+                      &ctx->chunk_ntok, &ctx->doc_tok, &ctx->vkeys, &ctx->vrep, &ctx->rec_slot, &ctx->rec_cnt,
                       &ctx->part_doc, &ctx->part_slot, &ctx->part_cnt, &ctx->doc_recoff, &ctx->doc_npairs,
                       &ctx->doc_size, &ctx->doc_flags, &ctx->counters, &ctx->dense, &ctx->vslot, &ctx->skey0,
                       &ctx->skey1, &ctx->seq0, &ctx->seq1, &ctx->rank_of_slot, &ctx->slot_of_rank, &ctx->rank16, &ctx->pkey0,
@@ -896,7 +902,9 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     const bool aligned = (((uintptr_t)c.bytes & 15u) == 0);
     ctx->k1_vs = aligned && ctx->k1_mode != 2;
     if (ctx->k1_vs && ctx->vcap > K1_VS_MAX_CAP) return TFIDF_E_CAPACITY;
-    ctx->k1_sl = ctx->k1_vs && (ctx->k1_mode == 0 || ctx->k1_mode == 3) && ctx->vcap <= ctx->sl_maxcap;
+    ctx->k1_sl = ctx->k1_vs && (ctx->k1_mode == 0 || ctx->k1_mode == 3 || ctx->k1_mode == 4) &&
+                 ctx->vcap <= ctx->sl_maxcap;
+    ctx->k1_2p = ctx->k1_sl && ctx->k1_mode == 4;
     /* tokcount_sl over a high-cardinality table (TFIDF_SL_MAXCAP): half-size chunks, as
      * tokcount_vs, since nearly every token is a new pair for its LDS table */
     const uint32_t cb = ctx->k1_sl ? (ctx->vcap > K1_ST_MAX_CAP ? CHUNK_BYTES : CHUNK_BYTES_ST) : CHUNK_BYTES;
@@ -968,12 +976,32 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
         /* pinned source: the copy is stream-ordered before the launch, and the block is not
          * rewritten before the next run (every run synchronises with the host after K1) */
         if (!ctx->k1out_valid || memcmp(ctx->k1out_host, &o, sizeof(K1Out)) != 0) {   /* steady state: unchanged */
+            ctx->k1out_valid = false;   /* until the copy of the new block is enqueued */
             *ctx->k1out_host = o;
             HIPCHK(hipMemcpyAsync(ctx->k1out_dev.p, ctx->k1out_host, sizeof(K1Out), hipMemcpyHostToDevice, s));
             ctx->k1out_valid = true;
         }
-        LCHK(launch_tokcount_sl(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd,
-                                ctx->k1out_dev.as<K1Out>(), s));
+        if (ctx->k1_2p) {
+            /* the token stream: each chunk's range holds at most len / 2 + its documents + 2
+             * tokens (k_chunk_tokcap), at most span / 2 + N + 3 nchunks in all */
+            ENSURE(ctx->chunk_caps, (nchunks + 1) * 8);
+            ENSURE(ctx->chunk_tok, (nchunks + 1) * 8);
+            ENSURE(ctx->chunk_ntok, nchunks * 4 + 4);
+            ENSURE(ctx->doc_tok, (size_t)N * 4 + 4);
+            ENSURE(ctx->tok_stream, (span / 2 + N + 3 * nchunks + 64) * 4);
+            TokStream ts{};
+            ts.tok = ctx->tok_stream.as<uint32_t>();
+            ts.chunk_tok = ctx->chunk_tok.as<uint64_t>();
+            ts.chunk_ntok = ctx->chunk_ntok.as<uint32_t>();
+            ts.doc_tok = ctx->doc_tok.as<uint32_t>();
+            ts.status = (uint32_t*)(cnt + 3);
+            ts.chunk_ctr = cnt + 24;
+            LCHK(launch_tok_twopass(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), nchunks, vd, ts,
+                                    ctx->chunk_caps.as<uint64_t>(), ctx->k1out_dev.as<K1Out>(), ar, s));
+        } else {
+            LCHK(launch_tokcount_sl(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd,
+                                    ctx->k1out_dev.as<K1Out>(), s));
+        }
     } else if (nchunks && ctx->k1_vs)
         LCHK(launch_tokcount_vs(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
     else if (nchunks)
@@ -1100,14 +1128,20 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
                 return TFIDF_E_NOMEM;
             ctx->rec_cap = ncap;
         }
-        ENSURE(ctx->df_scratch, df_hist_scratch(R_main, V));
+        const size_t dneed = df_hist_scratch(R_main, V);
+        ENSURE(ctx->df_scratch, dneed > ctx->df_scratch_min ? dneed : ctx->df_scratch_min);
         Arena da;
         da.base = (uint8_t*)ctx->df_scratch.p;
         da.cap = ctx->df_scratch.cap;
         HIPCHK(hipEventRecord(ctx->ev_vrank, s));
         HIPCHK(hipStreamWaitEvent(ctx->stream2, ctx->ev_vrank, 0));
-        LCHK(launch_df_hist(ctx->rec_slot.as<uint32_t>(), R_main, nullptr, R_main, ctx->rank_of_slot.as<uint32_t>(),
-                            r16, V, cap, (uint32_t*)(cnt + 3), ctx->df_local.as<uint32_t>(), da, ctx->stream2));
+        const int dl = launch_df_hist(ctx->rec_slot.as<uint32_t>(), R_main, nullptr, R_main, ctx->rank_of_slot.as<uint32_t>(),
+                                      r16, V, cap, (uint32_t*)(cnt + 3), ctx->df_local.as<uint32_t>(), da, ctx->stream2);
+        if (dl == -2) {   /* its own scratch was short: grow it (not the arena) and retry */
+            ctx->df_scratch_min = da.peak + da.peak / 2 + 4096;
+            return 1;
+        }
+        LCHK(dl);
         HIPCHK(hipEventRecord(ctx->ev_dfmain, ctx->stream2));
     }
     if (N <= SORT_TILE_MAXN && ctx->doc_order_s3) {   /* A/B: beside the merge / DF stages */
@@ -1314,16 +1348,23 @@ static void idf_post(tfidf_ctx* ctx, double* lut, uint64_t Nt, const uint32_t* v
     }
     P.go.notify_all();
 }
+/* Waits for every upload that may still read idf_pin or write idf_vals: a failed run can leave
+ * the early upload (stream3, run_local) or the late one (the main stream, run_post) queued, and
+ * the next run must neither rewrite / free idf_pin under it nor have it land after its own copy */
+static int idf_pin_quiesce(tfidf_ctx* ctx) {
+    if (!ctx->idf_pin_busy) return TFIDF_OK;
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream3));
+    ctx->idf_pin_busy = false;
+    return TFIDF_OK;
+}
 static int idf_start(tfidf_ctx* ctx, uint64_t Nt) {
     ctx->idf_logs = 0;
     ctx->idf_early = false;
     ctx->ms_idf_host = ctx->ms_idf_wait = 0;
     if (Nt > IDF_FULL_MAX) return TFIDF_OK;                          /* distinct-df path in run_post */
     if (ctx->idf_cache && ctx->idf_full_n == Nt) return TFIDF_OK;    /* TFIDF_IDF_CACHE=1 */
-    if (ctx->idf_pin_busy) {   /* a failed run left its upload of idf_pin unwaited */
-        HIPCHK(hipStreamSynchronize(ctx->stream));
-        ctx->idf_pin_busy = false;
-    }
+    if (const int q = idf_pin_quiesce(ctx)) return q;   /* a failed run left an upload of idf_pin unwaited */
     const size_t n = (size_t)Nt + 1;
     if (ctx->idf_pin_n < n) {
         if (ctx->idf_pin) (void)hipHostFree(ctx->idf_pin);
@@ -1427,10 +1468,7 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
         }
         ENSURE(ctx->idf_vals, (size_t)K * 8 + 8);
         /* the distinct df values' logs on the context's workers, into pinned memory */
-        if (ctx->idf_pin_busy) {   /* a failed run left its upload of idf_pin unwaited */
-        HIPCHK(hipStreamSynchronize(ctx->stream));
-        ctx->idf_pin_busy = false;
-    }
+        if (const int q = idf_pin_quiesce(ctx)) return q;   /* a failed run left an upload of idf_pin unwaited */
         if (ctx->idf_pin_n < (size_t)K + 1) {
             if (ctx->idf_pin) (void)hipHostFree(ctx->idf_pin);
             ctx->idf_pin = nullptr;
@@ -1627,7 +1665,11 @@ extern "C" int tfidf_run(tfidf_ctx* ctx, const tfidf_corpus* in) {
         /* with peers, an allocation failure is reported through the agreement as well */
         rc = arc ? arc : run_once(ctx, c, dev_ids, Nt);
         if (arc && ctx->xp) (void)exchange_agree(ctx, arc, 0, nullptr);
-        if (rc == 1) { HIPCHK(hipStreamSynchronize(s)); HIPCHK(hipStreamSynchronize(ctx->stream2)); }
+        if (rc == 1) {
+            HIPCHK(hipStreamSynchronize(s));
+            HIPCHK(hipStreamSynchronize(ctx->stream2));
+            HIPCHK(hipStreamSynchronize(ctx->stream3));   /* the early idf upload (run_local) */
+        }
     }
     if (rc == 1) return TFIDF_E_CAPACITY;
     if (rc) return rc;
@@ -1757,6 +1799,7 @@ extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* out) {
     for (int i = 0; i < S_NSTAGES; ++i) info->ms_stage[i] = ctx->ms_stage[i];
     info->nstages = S_NSTAGES;
     info->flags = (ctx->k1_vs ? TFIDF_RUN_K1_VS : 0u) | (ctx->k1_sl ? TFIDF_RUN_K1_SL : 0u) |
+                  (ctx->k1_2p ? TFIDF_RUN_K1_2P : 0u) |
                   (ctx->xp && ctx->last_dense ? TFIDF_RUN_XCHG_DENSE : 0u);
     info->device_allocs = g_dev_allocs.load(std::memory_order_relaxed);
     info->device_alloc_bytes = g_dev_alloc_bytes.load(std::memory_order_relaxed);

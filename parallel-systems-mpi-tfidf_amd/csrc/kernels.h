@@ -108,6 +108,21 @@ int launch_tokcount_vs(const CorpusDev& c, const uint64_t* chunk_start, const ui
  * 16-byte aligned corpus base; -3 when the vocabulary exceeds K1_ST_MAX_CAP slots */
 int launch_tokcount_sl(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc, uint64_t c0,
                        uint64_t c1, const VocabDev& v, const K1Out* o_dev, hipStream_t s);
+/* K1 two-pass form (tokcount_sl.hip, TFIDF_K1=2p): K1a tokenizes and resolves every token into
+ * a token stream of LDS keys (chunk ranges bounded by k_chunk_tokcap + a scan into chunk_tok),
+ * K1b counts the stream per group with k_tokcount_sl's table and flush.  caps: nch + 1 u64
+ * scratch; -3 when the vocabulary exceeds K1_SL_MAX_CAP slots, -2 when the arena is short */
+struct TokStream {
+    uint32_t* tok;                   /* token stream: 1 << 31 | document in group << sb | slot (0: unresolved) */
+    const uint64_t* chunk_tok;       /* nch + 1: each chunk's first stream index (scan of its bound) */
+    uint32_t* chunk_ntok;            /* nch: tokens of each chunk */
+    uint32_t* doc_tok;               /* per document starting a group (not a chunk): its chunk-local first token */
+    uint32_t* status;
+    unsigned long long* chunk_ctr;   /* K1a's chunk schedule (zeroed per run) */
+};
+int launch_tok_twopass(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc, uint64_t nch,
+                       const VocabDev& v, const TokStream& t, uint64_t* caps, const K1Out* o_dev, Arena& ar,
+                       hipStream_t s);
 
 
 /* vocabulary finalisation */

@@ -14,7 +14,7 @@ for r in $(seq 1 ${ROUNDS:-2}); do
   for v in ${VARIANTS:-base}; do
     L=$v; [ $v = base ] && L=""
     EV=""; case $v in env:*) L=""; EV=${v#env:}; EV=${EV//,/ };; esac   # env:NAME=VALUE[,NAME=VALUE] = the product library with those settings
-    env $EV TFIDF_LIB=$L timeout -k 10 200 python3 -u bench.py --config ${CFG:-c2} --steps 10 --warmup 2 --no-cpu-baseline --no-emit --no-probe > $OUT/ab.json 2>$OUT/ab.err || { echo "fail $v"; tail -5 $OUT/ab.err; exit 1; }
+    env TFIDF_LIB=$L $EV timeout -k 10 200 python3 -u bench.py --config ${CFG:-c2} --steps 10 --warmup 2 --no-cpu-baseline --no-emit --no-probe > $OUT/ab.json 2>$OUT/ab.err || { echo "fail $v"; tail -5 $OUT/ab.err; exit 1; }
     python3 -c "import json; d=json.load(open('$OUT/ab.json')); s=d['stage_ms_mean']; print('$v', d['value'], 'k1', s['tokcount'], 'score', s['score'], 'df', s['df'], 'merge', s['merge'], 'vocab', s['vocab'])"
   done
 done

@@ -206,6 +206,26 @@ def test_exchange_failure_after_allgather_aborts_peers(failing, xchg, monkeypatc
         assert b"".join(g.ranks[r].text() for r in range(3)) == ora["output_txt"]
 
 
+def test_failed_run_then_other_n_gets_its_own_idf_table(monkeypatch):
+    """A run that fails inside the exchange may leave its idf-table upload (stream3, queued
+    before the exchange) in flight.  The next run of the same contexts has another document
+    count N, so its idf table differs in every entry: a stale upload landing after the new
+    one, or a rewrite of the pinned table under the old copy, would change its scores.  The
+    second run must match the oracle byte for byte (engine.cpp idf_pin_quiesce)."""
+    monkeypatch.setenv("TFIDF_XCHG", "dense")
+    monkeypatch.setenv("TFIDF_TEST_XFAIL_RANK", "1")   # read by tfidf_open; fires once
+    first = _shards("c2", 0.002, 2)
+    second = _shards("c2", 0.0013, 2)
+    with tfidf_abi.Group(2, devices=[0, 0]) as g:
+        with pytest.raises(tfidf_abi.TfidfError):
+            g.run_host(first)
+        g.run_host(second)
+        ora = _full("c2", 0.0013)
+        assert b"".join(g.ranks[r].text() for r in range(2)) == ora["output_txt"]
+        g.run_host(first)
+        assert b"".join(g.ranks[r].text() for r in range(2)) == _full("c2", 0.002)["output_txt"]
+
+
 @pytest.mark.parametrize("xchg", ["dense", "owner"])
 @pytest.mark.parametrize("failing", [0, 2])
 def test_exchange_agreed_alloc_failure_keeps_group_usable(failing, xchg, monkeypatch):
