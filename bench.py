@@ -602,9 +602,8 @@ def main():
             "stage_ms_source": f"{len(stage_steps)} untimed steps after the timed ones, with per-stage HIP events "
                                f"(the timed steps record K1's and the whole run's events only)",
             # the idf table (log(N/df) on the host's libm, TFIDF.c:243) is rebuilt inside every
-            # timed step on host threads beside the device stages (TFIDF_IDF_CACHE=1: kept
-            # across runs of one N, reported as idf_cached)
-            "idf": {"idf_cached": bool(os.environ.get("TFIDF_IDF_CACHE") == "1"),
+            # timed step on host threads beside the device stages (no cache across runs)
+            "idf": {"idf_cached": False,
                     "logs_per_step": int(np.mean([x[0] for x in idf_steps])),
                     "lut_host_ms_mean": round(float(np.mean([x[1] for x in idf_steps])), 4),
                     "wait_ms_mean": round(float(np.mean([x[2] for x in idf_steps])), 4)},

@@ -192,8 +192,7 @@ typedef struct tfidf_run_info {
      * every df = 1..N is tabulated by the context's host worker threads while the device runs
      * the stages before the score; beyond that only the run's distinct df values, after the DF
      * stage (one host round trip) */
-    uint64_t idf_logs;        /* libm log() calls made for this run's table (0: the table of
-                                 the previous run's N was kept, TFIDF_IDF_CACHE=1) */
+    uint64_t idf_logs;        /* libm log() calls made for this run's table (every run builds its own) */
     double   ms_idf_host;     /* wall time of those calls (host threads) */
     double   ms_idf_wait;     /* time the run waited for them before the score stage */
 } tfidf_run_info;

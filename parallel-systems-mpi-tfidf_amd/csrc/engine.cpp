@@ -147,7 +147,6 @@ struct tfidf_ctx {
     /* split DF (runs with partial records): the main records' histogram runs on stream2
      * beside the merge stage, the merged records' is added on the main stream after it */
     bool df_split = true;           /* env TFIDF_DF_SPLIT=0: one DF pass after the merge */
-    bool doc_order_s3 = false;      /* env TFIDF_DOC_ORDER_S3=1 (A/B): a small run's document order on stream3 after the DF fork */
     hipEvent_t ev_vrank = nullptr, ev_dfmain = nullptr;
     DevBuf df_scratch;
     size_t df_scratch_min = 0;      /* grown when the split DF pass reported a shortfall (retried) */
@@ -187,9 +186,7 @@ struct tfidf_ctx {
     uint64_t idf_full_n = 0;   /* idf_vals holds log(N/df) for df = 0..N of this N (0: not) */
     /* the per-run idf table (N <= IDF_FULL_MAX): host threads fill the pinned idf_pin with
      * log(N/df) for df = 0..N while the device runs the stages before the score; run_post
-     * joins them and uploads it.  TFIDF_IDF_CACHE=1 keeps the table of an unchanged N
-     * instead (round 4's behaviour; the bench reports which) */
-    bool idf_cache = false;
+     * joins them and uploads it (every run: round 4's per-N cache was retired in round 6) */
     double* idf_pin = nullptr;
     size_t idf_pin_n = 0;
     bool idf_pin_busy = false;            /* an upload from idf_pin is enqueued and not known complete (the
@@ -413,8 +410,6 @@ int tfidf_open(int device, tfidf_ctx** out) {
     ctx->xb_stage_max = kxb ? (uint32_t)atoi(kxb) : ~0u;
     const char* kds = getenv("TFIDF_DF_SPLIT");
     ctx->df_split = !(kds && !strcmp(kds, "0"));
-    const char* kdo = getenv("TFIDF_DOC_ORDER_S3");
-    ctx->doc_order_s3 = kdo && !strcmp(kdo, "1");
     const char* kn = getenv("TFIDF_TEST_XNOMEM_RANK");
     ctx->xnomem_rank = kn ? atoi(kn) : -1;
     /* diagnostics: initial vocabulary capacity (power of two) and the loads it may reach
@@ -444,10 +439,6 @@ int tfidf_open(int device, tfidf_ctx** out) {
     HIPCHK(hipEventCreateWithFlags(&ctx->ev_idf_up, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ctx->ev_vrank, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ctx->ev_dfmain, hipEventDisableTiming));
-    {
-        const char* ic = getenv("TFIDF_IDF_CACHE");
-        ctx->idf_cache = ic && ic[0] == '1';
-    }
     for (int i = 0; i <= S_NSTAGES; ++i) HIPCHK(hipEventCreate(&ctx->ev[i]));
     if (arena_reset(ctx, 64ull << 20) != 0) { delete ctx; return TFIDF_E_NOMEM; }
     if (ctx->counters.ensure(256) != 0) { delete ctx; return TFIDF_E_NOMEM; }
@@ -1111,7 +1102,7 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     if (V <= 65536u) { ENSURE(ctx->rank16, cap * 2); r16 = ctx->rank16.as<uint16_t>(); }
     LCHK(launch_vocab_rank(ctx->sorted_dense, ctx->vslot.as<uint32_t>(), V, ctx->rank_of_slot.as<uint32_t>(),
                            ctx->slot_of_rank.as<uint32_t>(), r16, s));
-    if (N <= SORT_TILE_MAXN && !ctx->doc_order_s3) {   /* see enqueue_doc_order */
+    if (N <= SORT_TILE_MAXN) {   /* see enqueue_doc_order */
         const int rc = enqueue_doc_order(ctx, dev_ids, N, ctx->stream2);
         if (rc) return rc;
     }
@@ -1143,10 +1134,6 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
         }
         LCHK(dl);
         HIPCHK(hipEventRecord(ctx->ev_dfmain, ctx->stream2));
-    }
-    if (N <= SORT_TILE_MAXN && ctx->doc_order_s3) {   /* A/B: beside the merge / DF stages */
-        const int rc = enqueue_doc_order(ctx, dev_ids, N, ctx->stream3);
-        if (rc) return rc;
     }
     /* this run's full idf table (idf_start's workers finish during K1 in practice) goes up
      * on its own copy stream now, beside the merge and DF stages, instead of inside the idf
@@ -1363,7 +1350,6 @@ static int idf_start(tfidf_ctx* ctx, uint64_t Nt) {
     ctx->idf_early = false;
     ctx->ms_idf_host = ctx->ms_idf_wait = 0;
     if (Nt > IDF_FULL_MAX) return TFIDF_OK;                          /* distinct-df path in run_post */
-    if (ctx->idf_cache && ctx->idf_full_n == Nt) return TFIDF_OK;    /* TFIDF_IDF_CACHE=1 */
     if (const int q = idf_pin_quiesce(ctx)) return q;   /* a failed run left an upload of idf_pin unwaited */
     const size_t n = (size_t)Nt + 1;
     if (ctx->idf_pin_n < n) {

@@ -34,6 +34,7 @@
 #include "kernels.h"
 #include "xport.h"
 #include "comm_rank.h"
+#include "comm_init.h"
 
 namespace {
 
@@ -409,59 +410,30 @@ struct LocalXport final : Xport {
 
 }  // namespace
 
-/* one rank of a process-per-GPU job (tfidf_comm_init).  RCCL 2.27's ncclCommInitRankConfig
- * blocks its caller in the bootstrap until every rank has joined, even for a non-blocking
- * communicator (measured on the GPU box: a 2-rank init whose peer never starts did not
- * return within 40 s).  So the init runs on a helper thread and this call waits for it at
- * most TFIDF_COMM_TIMEOUT_S: a peer that never joins gives TFIDF_E_PEER instead of a hang.
- * The helper then stays blocked in RCCL's bootstrap (it cannot be interrupted); if the peers
- * ever do join, it aborts the communicator nobody will use. */
-struct InitJob {
-    std::mutex mu;
-    std::condition_variable cv;
-    bool done = false, abandoned = false;
-    int rc = TFIDF_OK;
-    ncclComm_t comm = nullptr;
-};
+/* one rank of a process-per-GPU job (tfidf_comm_init): the init runs with a deadline on a
+ * helper thread (comm_init.h: RCCL 2.27 blocks the caller in its bootstrap until every rank
+ * joined; at most one abandoned helper per process) */
 int rccl_init_rank(const void* unique_id, int rank, int nranks, int device, Xport** out) {
     *out = nullptr;
     ncclUniqueId u;
     memcpy(&u, unique_id, sizeof(u));
     const int64_t tmo = comm_timeout_ms_from_env();
-    auto job = std::make_shared<InitJob>();
-    std::thread([job, u, rank, nranks, device, tmo] {
-        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-        cfg.blocking = 0;
-        ncclComm_t comm = nullptr;
-        int rc = TFIDF_OK;
-        if (hipSetDevice(device) != hipSuccess) rc = TFIDF_E_HIP;
-        if (!rc && (nccl_issue(ncclCommInitRankConfig(&comm, nranks, u, rank, &cfg)) < 0 || !comm)) rc = TFIDF_E_RCCL;
-        if (!rc) {
-            std::vector<ncclComm_t> one{comm};
-            rc = comms_ready(one, tmo);
-        }
-        std::lock_guard<std::mutex> lk(job->mu);
-        if (job->abandoned || rc) {   /* nobody takes it: abort what was made */
-            if (comm) (void)ncclCommAbort(comm);
-            comm = nullptr;
-        }
-        job->rc = rc;
-        job->comm = comm;
-        job->done = true;
-        job->cv.notify_all();
-    }).detach();
-    std::unique_lock<std::mutex> lk(job->mu);
-    const bool done = tmo > 0 ? job->cv.wait_for(lk, std::chrono::milliseconds(tmo), [&] { return job->done; })
-                              : (job->cv.wait(lk, [&] { return job->done; }), true);
-    if (!done) {
-        job->abandoned = true;
-        fprintf(stderr, "tfidf: rank %d of %d: the other ranks did not join within %lld s (TFIDF_COMM_TIMEOUT_S)\n",
-                rank, nranks, (long long)(tmo / 1000));
-        return TFIDF_E_PEER;
-    }
-    if (job->rc) return job->rc;
+    char who[64];
+    snprintf(who, sizeof who, "rank %d of %d", rank, nranks);
+    ncclComm_t comm = nullptr;
+    const int rc = comm_init_with_deadline<RcclB>(
+        [u, rank, nranks, device, tmo](ncclComm_t* c) -> int {
+            ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+            cfg.blocking = 0;
+            if (hipSetDevice(device) != hipSuccess) return TFIDF_E_HIP;
+            if (nccl_issue(ncclCommInitRankConfig(c, nranks, u, rank, &cfg)) < 0 || !*c) return TFIDF_E_RCCL;
+            std::vector<ncclComm_t> one{*c};
+            return comms_ready(one, tmo);
+        },
+        tmo, &comm, who);
+    if (rc) return rc;
     RcclXport* x = new RcclXport();
-    x->cr.comm = job->comm;
+    x->cr.comm = comm;
     x->cr.timeout_ms = tmo;
     x->rank = rank;
     x->nranks = nranks;
@@ -536,7 +508,9 @@ int tfidf_group_open(int nranks, const int* devices, uint32_t flags, tfidf_group
             (void)hipSetDevice(cur);
             if (bad) rc = TFIDF_E_RCCL;
             else rc = comms_ready(cl->comms, cl->timeout_ms);
-            if (rc == TFIDF_E_PEER) {   /* timed out: abandoned, not aborted (rccl_init_rank) */
+            if (rc == TFIDF_E_PEER) {   /* timed out: aborted on a helper thread (an abort may wait in the
+                                           same bootstrap; comm_init.h) */
+                comm_reap_async<RcclB>(cl->comms);
                 for (ncclComm_t& c : cl->comms) c = nullptr;
             } else if (rc) {   /* nothing usable: abort what was created */
                 for (ncclComm_t& c : cl->comms)

@@ -1350,6 +1350,9 @@ __global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_tok_count(const ui
         const uint32_t dfirst = chunk_doc[chunk], dlast = chunk_doc[chunk + 1];
         const uint64_t tbase = t.chunk_tok[chunk];
         const uint32_t ntk = t.chunk_ntok[chunk];
+        /* the chunk's stream range as a buffer: 16-byte loads past its end read zeros */
+        const __amdgpu_buffer_rsrc_t trs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(tok + tbase), 0, (int)(ntk * 4u), RSRC_WORD3);
         if (cs < ce) {
             if (!clean) {
                 uint4* tt = reinterpret_cast<uint4*>(S.TK);
@@ -1369,16 +1372,24 @@ __global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_tok_count(const ui
                 if ((uint32_t)tid < ng) S.dfull[tid] = doc_off[gd0 + tid] >= cs && doc_off[gd0 + tid + 1] <= ce;
                 lds_barrier();
                 uint32_t wclaims = 0;
-                const uint32_t nr = (t1 - t0 + 63u) / 64u;
-                uint32_t i = t0 + (uint32_t)wid * 64u + (uint32_t)lane;
-                uint32_t nk = i < t1 ? gload(&tok[tbase + i]) : 0u;
-                for (uint32_t k = (uint32_t)wid; k < nr; k += NWAVE) {
-                    const uint32_t key = nk;
-                    i += 64u * NWAVE;
-                    nk = i < t1 ? gload(&tok[tbase + i]) : 0u;   /* the wave's next round */
-                    if (key) wave_agg_add(S.dsz, (key & 0x7FFFFFFFu) >> sb);
-                    tokens_w += (uint32_t)__popcll(__ballot(key != 0u));
-                    lds_count(S, o, key, wclaims, gd0, sb SL_STC);
+                /* super-rounds of 256 tokens: lane L holds tokens 4L .. 4L+3 of one 16-byte load (a
+                 * 1 KiB piece per wave, the next one in flight while four rounds are counted: one
+                 * dword per lane and round left each wave HBM-latency-bound) */
+                const uint32_t nsr = (t1 - t0 + 255u) / 256u;
+                uint32_t i = t0 + (uint32_t)wid * 256u + 4u * (uint32_t)lane;
+                uint4 nk = bload16<2>(trs, (int32_t)(i * 4u));
+                for (uint32_t k = (uint32_t)wid; k < nsr; k += NWAVE) {
+                    const uint4 cur = nk;
+                    const uint32_t i0 = i;
+                    i += 256u * NWAVE;
+                    nk = bload16<2>(trs, (int32_t)(i * 4u));   /* the wave's next super-round (zeros past the range) */
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t key = (i0 + (uint32_t)q < t1) ? (&cur.x)[q] : 0u;
+                        if (key) wave_agg_add(S.dsz, (key & 0x7FFFFFFFu) >> sb);
+                        tokens_w += (uint32_t)__popcll(__ballot(key != 0u));
+                        lds_count(S, o, key, wclaims, gd0, sb SL_STC);
+                    }
                 }
 #ifdef SL_STAMPS
                 if (ng <= FEW) {

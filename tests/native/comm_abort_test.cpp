@@ -14,10 +14,12 @@
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <mutex>
 #include <thread>
 #include <vector>
 
+#include "comm_init.h"
 #include "comm_rank.h"
 
 namespace {
@@ -116,6 +118,29 @@ std::vector<Outcome> run_clique(int nranks, int ncoll, int fail_rank, int fail_a
     return out;
 }
 
+/* a fake communicator init (comm_init.h) that blocks until the test opens its gate, as RCCL's
+ * bootstrap blocks until every rank joined */
+struct InitGate {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool open = false;
+};
+InitGate g_gate;
+std::atomic<int> g_init_aborts{0};
+struct FakeInitB {
+    using Comm = int;
+    static void abort(Comm) { g_init_aborts.fetch_add(1); }
+};
+int fake_init(int* c) {
+    std::unique_lock<std::mutex> lk(g_gate.mu);
+    g_gate.cv.wait(lk, [] { return g_gate.open; });
+    *c = 7;
+    return TFIDF_OK;
+}
+double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
 int g_fail = 0;
 void check(bool ok, const char* what) {
     printf("%s %s\n", ok ? "ok  " : "FAIL", what);
@@ -167,6 +192,42 @@ int main() {
         check(rc == TFIDF_E_PEER && net.issued[0] == 0 && net.aborts[0].load() == 1,
               "an aborted rank's next call returns TFIDF_E_PEER and issues nothing");
         g_net = nullptr;
+    }
+    {   /* an init whose peers never join: the caller gets TFIDF_E_PEER at its deadline */
+        int comm = -1, live = 0, ab = 0;
+        auto t0 = std::chrono::steady_clock::now();
+        const int rc = comm_init_with_deadline<FakeInitB>([](int* c) { return fake_init(c); }, 200, &comm, "test");
+        const double ms = ms_since(t0);
+        comm_init_counts(&live, &ab);
+        check(rc == TFIDF_E_PEER && comm == 0 && ms >= 150 && ms < 5000 && live == 1 && ab == 1,
+              "init never completes: TFIDF_E_PEER after the 200 ms deadline, one abandoned helper");
+        /* a second init while that helper is still blocked: refused at once, no new thread */
+        t0 = std::chrono::steady_clock::now();
+        const int rc2 = comm_init_with_deadline<FakeInitB>([](int* c) { return fake_init(c); }, 200, &comm, "test");
+        const double ms2 = ms_since(t0);
+        comm_init_counts(&live, &ab);
+        check(rc2 == TFIDF_E_PEER && ms2 < 100 && live == 1 && ab == 1,
+              "a second init while the first is blocked: refused at once, still one helper thread");
+        /* the peers join late: the abandoned helper aborts the communicator nobody takes, and exits */
+        {
+            std::lock_guard<std::mutex> lk(g_gate.mu);
+            g_gate.open = true;
+        }
+        g_gate.cv.notify_all();
+        t0 = std::chrono::steady_clock::now();
+        do {
+            std::this_thread::sleep_for(std::chrono::milliseconds(2));
+            comm_init_counts(&live, &ab);
+        } while ((live || ab) && ms_since(t0) < 5000);
+        check(live == 0 && ab == 0 && g_init_aborts.load() == 1,
+              "the late init's communicator is aborted and its helper thread exits (nothing left)");
+        /* and the process can create a communicator again */
+        const int rc3 = comm_init_with_deadline<FakeInitB>([](int* c) { return fake_init(c); }, 200, &comm, "test");
+        do {
+            comm_init_counts(&live, &ab);
+        } while (live && ms_since(t0) < 5000);
+        check(rc3 == TFIDF_OK && comm == 7 && g_init_aborts.load() == 1 && live == 0,
+              "a later init succeeds and hands its communicator to the caller (not aborted)");
     }
     printf(g_fail ? "FAILED\n" : "ALL OK\n");
     return g_fail;

@@ -1,7 +1,10 @@
 """CPU test of the RCCL ranks' abort protocol (csrc/comm_rank.h): a fake clique whose
 collectives complete only when every rank issued them, so a rank that waits for a failed
 peer is released only by the protocol itself.  Replaces the reference's exit()-and-let-
-mpirun-kill behaviour (TFIDF.c:122,137).  No GPU: the C++ state machine is compiled with g++."""
+mpirun-kill behaviour (TFIDF.c:122,137).  Also the communicator init with a deadline
+(csrc/comm_init.h): an init that never completes returns at its deadline, a process keeps at
+most one blocked helper thread, and a late init's communicator is aborted.  No GPU: the C++
+state machines are compiled with g++."""
 import os
 import subprocess
 
@@ -20,4 +23,4 @@ def test_comm_abort_state_machine(tmp_path):
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ALL OK" in r.stdout
-    assert r.stdout.count("ok  ") == 7
+    assert r.stdout.count("ok  ") == 11
