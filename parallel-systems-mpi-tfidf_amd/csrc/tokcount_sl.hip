@@ -111,6 +111,10 @@ struct SlShared {
             uint32_t drun[GCAP];
             uint8_t dstate[GCAP];
         } f;
+        struct {
+            uint32_t wtot[NWAVE * 4];   /* few-document flush: each wave's per-document entry counts */
+            uint4 lrank[NT];            /* ... each thread's first staging index per document (16-bit) */
+        } q;
     };
     uint4 sel[16];                      /* v_perm selectors of a term of length n */
     uint32_t lbase[8];                  /* few-document flush: a document's first staging index */
@@ -435,22 +439,22 @@ __device__ __forceinline__ void sl_flush_few(SlShared& S, const K1Out* o, uint32
     const int lane = tid & 63, w = tid >> 6;
     lds_barrier();
     uint32_t ek[EPT], ec[EPT];
-    uint32_t pk[FEW / 2] = {0, 0, 0, 0};
+    /* per document, this thread's entry count in a 4-bit field (EPT < 16): one shift-add per
+     * entry (an empty entry, key 0, adds 0 to document 0's field) */
+    uint32_t c4 = 0;
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
         ek[j] = S.TK[j * NT + tid];
         ec[j] = S.TC[j * NT + tid];
-        if (ek[j]) {
-            const uint32_t rel = (ek[j] & 0x7FFFFFFFu) >> sb;
-#pragma unroll
-            for (uint32_t q = 0; q < FEW / 2; ++q) pk[q] += (rel >> 1) == q ? (1u << (16 * (rel & 1u))) : 0u;
-        }
+        c4 += (ek[j] >> 31) << (4u * ((ek[j] & 0x7FFFFFFFu) >> sb));
     }
-    uint32_t inc[FEW / 2];
+    static_assert(EPT < 16 && FEW == 8, "4-bit per-document entry counts of eight documents");
+    uint32_t pk[FEW / 2], inc[FEW / 2];
 #pragma unroll
     for (uint32_t q = 0; q < FEW / 2; ++q) {
+        pk[q] = ((c4 >> (8u * q)) & 15u) | (((c4 >> (8u * q + 4u)) & 15u) << 16);
         inc[q] = wave_incl_scan(pk[q]);
-        if (lane == 63) S.f.dcnt[w * (FEW / 2) + q] = inc[q];
+        if (lane == 63) S.q.wtot[w * (FEW / 2) + q] = inc[q];
     }
     SLF_STAMP(9);
     lds_barrier();
@@ -460,7 +464,7 @@ __device__ __forceinline__ void sl_flush_few(SlShared& S, const K1Out* o, uint32
         uint32_t base = 0, t = 0;
 #pragma unroll
         for (int k = 0; k < NWAVE; ++k) {
-            const uint32_t x = S.f.dcnt[k * (FEW / 2) + q];
+            const uint32_t x = S.q.wtot[k * (FEW / 2) + q];
             base += k < w ? x : 0u;
             t += x;
         }
@@ -497,13 +501,11 @@ __device__ __forceinline__ void sl_flush_few(SlShared& S, const K1Out* o, uint32
         const bool rec_ok = rb + nrec <= o->rec_cap, part_ok = pb + npart <= o->part_cap;
         if (lane == 0 && !rec_ok) atomicOr(o->status, ST_REC_FULL);
         if (lane == 0 && !part_ok) atomicOr(o->status, ST_PART_FULL);
-        if (d < ng) {
-            if (st == 2) {
-                gmem(o->doc_recoff)[gd0 + d] = rb + (off & 0xFFFFu);
-                gmem(o->doc_npairs)[gd0 + d] = SL_ABL ? 0u : cnt;
-            }
-            S.lbase[d] = st == 2 ? (off & 0xFFFFu) : nrec + (off >> 16);   /* staging index */
+        if (d < ng && st == 2) {
+            gmem(o->doc_recoff)[gd0 + d] = rb + (off & 0xFFFFu);
+            gmem(o->doc_npairs)[gd0 + d] = SL_ABL ? 0u : cnt;
         }
+        if (d < FEW) S.lbase[d] = d >= ng ? 0u : (st == 2 ? (off & 0xFFFFu) : nrec + (off >> 16));   /* staging index */
         if (lane == 0) {
             S.fl_nrec = nrec;
             S.fl_npart = npart;
@@ -513,20 +515,25 @@ __device__ __forceinline__ void sl_flush_few(SlShared& S, const K1Out* o, uint32
     }
     lds_barrier();
     SLF_STAMP(10);
-    /* every entry to its staging index (sl_write_staged): its document's base + its rank */
+    /* every entry to its staging index (sl_write_staged): its document's base + the entries
+     * of that document before it (earlier threads, then this thread's earlier entries).  The
+     * thread's first index per document goes to LDS as eight 16-bit values (staging indices
+     * < TB), so an entry reads its base instead of selecting it from registers */
+    {
+        const uint4 lb0 = *reinterpret_cast<const uint4*>(&S.lbase[0]);
+        const uint4 lb1 = *reinterpret_cast<const uint4*>(&S.lbase[4]);
+        S.q.lrank[tid] = make_uint4(rank[0] + (lb0.x | (lb0.y << 16)), rank[1] + (lb0.z | (lb0.w << 16)),
+                                    rank[2] + (lb1.x | (lb1.y << 16)), rank[3] + (lb1.z | (lb1.w << 16)));
+    }
+    const uint16_t* const lr16 = reinterpret_cast<const uint16_t*>(&S.q.lrank[tid]);
+    uint32_t run = 0;   /* 4-bit per-document counts of this thread's entries placed so far */
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
         const uint32_t key = ek[j];
         if (key) {
-            const uint32_t rel = (key & 0x7FFFFFFFu) >> sb;
-            uint32_t r = 0;
-#pragma unroll
-            for (uint32_t q = 0; q < FEW / 2; ++q)
-                if ((rel >> 1) == q) {
-                    r = (rank[q] >> (16 * (rel & 1u))) & 0xFFFFu;
-                    rank[q] += 1u << (16 * (rel & 1u));
-                }
-            const uint32_t loc = S.lbase[rel] + r;
+            const uint32_t rel4 = 4u * ((key & 0x7FFFFFFFu) >> sb);
+            const uint32_t loc = (uint32_t)lr16[rel4 >> 2] + ((run >> rel4) & 15u);
+            run += 1u << rel4;
             S.TK[loc] = key;
             S.TC[loc] = ec[j];
         }
@@ -779,8 +786,8 @@ __global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_tokcount_sl(Corpus
         uint32_t fill = 0;             /* wave-uniform: built lanes of acc */
         uint32_t wclaims = 0;          /* this wave's LDS table claims (wave-uniform) */
 
-        /* resolve + count one round */
-        /* pend takes acc's token and issues its vocabulary loads */
+        /* pend takes acc's token and issues its vocabulary loads (two rounds whose roles swap
+         * instead, to save the copy, made the compiler select between them through scratch) */
         auto promote = [&](Round& p, const Round& a) {
             p.k0 = a.k0; p.k1 = a.k1; p.k2 = a.k2; p.k3 = a.k3;
             p.h = a.h; p.rel = a.rel; p.kind = a.kind; p.ap = a.ap;
@@ -838,6 +845,32 @@ __global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_tokcount_sl(Corpus
 #endif
             lds_count(S, o, key, wclaims, gd0, sb SL_STC);
         };
+        /* one lane's token into the round being built: its key from the staged bytes */
+        auto build = [&](Round& a, uint32_t e, int32_t sbp) {
+            const uint32_t pos = e & 1023u, len = (e >> 10) & 31u;
+            a.rel = e >> 16;
+            a.ap = sbp - 16 + (int32_t)pos;
+            a.kind = len >= 16u ? 2u : 1u;   /* 16..31: a long term or one past the window */
+#ifdef SL_DEBUG
+            a.ent = e;
+#endif
+            const u32x4u raw = *reinterpret_cast<const u32x4u*>(stage + pos);
+            const uint4 sl = S.sel[len & 15u];
+            a.k0 = __builtin_amdgcn_perm(0x09090909u, raw.x, sl.x);
+            a.k1 = __builtin_amdgcn_perm(0x09090909u, raw.y, sl.y);
+            a.k2 = __builtin_amdgcn_perm(0x09090909u, raw.z, sl.z);
+            a.k3 = __builtin_amdgcn_perm(0x09090909u, raw.w, sl.w);
+            a.h = (uint32_t)key_hash(((uint64_t)a.k1 << 32) | a.k0, ((uint64_t)a.k3 << 32) | a.k2) & (uint32_t)v.mask & ~1u;
+        };
+        /* acc is full (or the group's last): count pend, then send acc's vocabulary loads
+         * straight into the registers pend just released (a loaded value is never copied: a
+         * copy would wait for the load at once) */
+        auto turn = [&]() {
+            finish(pend);
+            promote(pend, acc);
+            acc.kind = 0u;
+            fill = 0u;
+        };
 
         if (gs < ge) {
             const int32_t bs = gs & ~15;
@@ -888,7 +921,8 @@ __global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_tokcount_sl(Corpus
                 if (!(sbp >= gs && sbp + WSTEP <= ge) && own) own &= ~outside16(gpos, gs, ge);
                 const uint32_t starts = ~ws & ((ws << 1) | prev | ds) & own & 0xFFFFu;
                 uint32_t nul = 0;
-                if (__ballot(lt9 != 0u) != 0ull)   /* a byte below 0x09 somewhere: exact NUL mask */
+                const bool nulany = __ballot(lt9 != 0u) != 0ull;
+                if (nulany)   /* a byte below 0x09 somewhere: exact NUL mask */
                     nul = compress4(zero_bits(cur.x)) | (compress4(zero_bits(cur.y)) << 4) |
                           (compress4(zero_bits(cur.z)) << 8) | (compress4(zero_bits(cur.w)) << 12);
                 const uint32_t stop = ws | ds;
@@ -904,8 +938,24 @@ __global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_tokcount_sl(Corpus
                 continue;
 #endif
                 if (!multi && lane == 0) atomicAdd(&S.dsz[wr], ntok);   /* the whole step is in document wr */
+                /* the common step (no document start in its window, no byte below 0x09, one
+                 * list pass): a token entry is its start bit, its length as the first stop bit
+                 * after it (lengths >= 16 are long terms whatever their value) and one OR into
+                 * the lane's loop-invariant (lane, document) bits — 10 VALU per entry with the
+                 * loop, against 25 in the general form below */
+                const bool fast = !multi && !nulany && ntok <= (uint32_t)TLW;
                 for (uint32_t tb = 0; tb < ntok; tb += TLW) {
-                    {
+                    if (fast) {
+                        /* bit 31 set: a token with no stop in the window gets length 31 - i >= 16 */
+                        const uint32_t eb = ((uint32_t)lane << 4) | (wr << 16), s32 = stop32 | 0x80000000u;
+                        uint32_t sm = starts;
+                        uint32_t* p = tl + (incl - nmine);
+                        while (sm) {
+                            const uint32_t i = __builtin_ctz(sm);
+                            sm &= sm - 1;
+                            *p++ = eb | i | ((uint32_t)__builtin_ctz(s32 >> i) << 10);
+                        }
+                    } else {
                         uint32_t sm = starts, idx = incl - nmine;
                         while (sm) {
                             const uint32_t i = __builtin_ctz(sm);
@@ -934,33 +984,13 @@ __global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_tokcount_sl(Corpus
                         const uint32_t m = (64u - fill) < (cnt - t) ? (64u - fill) : (cnt - t);
                         if ((uint32_t)lane >= fill && (uint32_t)lane < fill + m) {
                             const uint32_t e = tl[t + (uint32_t)lane - fill];
-                            const uint32_t pos = e & 1023u, len = (e >> 10) & 31u;
-                            acc.rel = e >> 16;
-                            acc.ap = sbp - 16 + (int32_t)pos;
-                            acc.kind = len == LEN_LONG ? 2u : 1u;
-#ifdef SL_DEBUG
-                            acc.ent = e;
-#endif
-                            const u32x4u raw = *reinterpret_cast<const u32x4u*>(stage + pos);
-                            const uint4 sl = S.sel[len & 15u];
-                            acc.k0 = __builtin_amdgcn_perm(0x09090909u, raw.x, sl.x);
-                            acc.k1 = __builtin_amdgcn_perm(0x09090909u, raw.y, sl.y);
-                            acc.k2 = __builtin_amdgcn_perm(0x09090909u, raw.z, sl.z);
-                            acc.k3 = __builtin_amdgcn_perm(0x09090909u, raw.w, sl.w);
-                            acc.h = (uint32_t)key_hash(((uint64_t)acc.k1 << 32) | acc.k0, ((uint64_t)acc.k3 << 32) | acc.k2) &
-                                    (uint32_t)v.mask & ~1u;
+                            build(acc, e, sbp);
                         }
                         t += m;
                         fill += m;
                         if (fill == 64u) {
-                            /* count the previous round, then send this one's vocabulary loads
-                             * straight into the registers that round just released: a loaded
-                             * value is never copied (a copy would wait for the load at once) */
                             SL_STAMP(3);
-                            finish(pend);
-                            promote(pend, acc);
-                            acc.kind = 0u;
-                            fill = 0u;
+                            turn();
                             SL_STAMP(4);
                         }
                     }
@@ -971,10 +1001,7 @@ __global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_tokcount_sl(Corpus
             }
         }
         SL_STAMP(3);
-        if (fill) {   /* the group's last, partial round */
-            finish(pend);
-            promote(pend, acc);
-        }
+        if (fill) turn();   /* the group's last, partial round */
         finish(pend);   /* drain */
 #ifdef SL_STAMPS
         SL_STAMP(5);
