@@ -82,12 +82,13 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 
-/* Vocabulary hash of a 128-bit term key: two 32-bit multiplies (v_mul_lo_u32 is a
- * quarter-rate instruction; every token of K1 pays this hash) and an xor-shift that brings
- * the products' high bits into the low bits the table mask keeps.  On c2's 5e4 terms it
- * probes like the four-multiply murmur finaliser it replaced: at a 1M-slot table 2.7 % of
- * the keys leave their home slot (2.5 % before), 0.15 % go past the next one.  Tables are
- * < 2^32 slots. */
+/* Vocabulary hash of a 128-bit term key: two 32-bit multiplies and an xor-shift that brings
+ * the products' high bits into the low bits the table mask keeps (on gfx950 v_mul_lo_u32
+ * issues like a shift or a v_perm, ~4.8 cycles per wave-instruction per SIMD:
+ * scripts/micro/valu_rates.hip).  On c2's 5e4 terms it probes like the four-multiply murmur
+ * finaliser it replaced: at a 1M-slot table 2.7 % of the keys leave their home slot (2.5 %
+ * before), 0.15 % go past the next one (24-bit-multiply forms that issue as cheaply placed
+ * 5-8 % past the pair: not used).  Tables are < 2^32 slots. */
 __device__ __forceinline__ uint64_t key_hash(uint64_t lo, uint64_t hi) {
     const uint32_t a = (uint32_t)lo, b = (uint32_t)(lo >> 32), c = (uint32_t)hi, d = (uint32_t)(hi >> 32);
     uint32_t h = ((a ^ __builtin_rotateleft32(c, 16)) * 0x9E3779B1u) ^ ((b ^ __builtin_rotateleft32(d, 8)) * 0x85EBCA77u);

@@ -116,8 +116,8 @@ struct tfidf_ctx {
     int k1_mode = 0;        /* 0 auto (k_tokcount_sl up to K1_ST_MAX_CAP slots, k_tokcount_vs beyond),
                                1 round-1 kernel (TFIDF_K1=vs), 2 general K1 (TFIDF_K1=general),
                                3 k_tokcount_sl (TFIDF_K1=sl) — cross-checks and A/B timing;
-                               4 the two-pass form of k_tokcount_sl (TFIDF_K1=2p: k_tok_resolve + k_tok_count);
-                               round 3's k_tokcount_st was retired in round 5 (git history) */
+                               round 3's k_tokcount_st was retired in round 5, round 6's two-pass form of
+                               k_tokcount_sl (measured slower: DESIGN §8) in round 6 (git history) */
     bool stamps_on = false; /* env TFIDF_STAMPS=1 with the diagnostic library build */
     int xfail_rank = -1;    /* env TFIDF_TEST_XFAIL_RANK (tests): this rank fails inside the exchange of
                                its first run, right after the key all-gather (the abort path of
@@ -127,7 +127,6 @@ struct tfidf_ctx {
     DevBuf stamps;
     bool k1_vs = false;     /* last run used the slot-keyed kernel (default) */
     bool k1_sl = false;     /* ... or tokcount_sl (else tokcount_vs) */
-    bool k1_2p = false;     /* ... in its two-pass form (token stream between the passes) */
     uint64_t sl_maxcap = K1_ST_MAX_CAP;   /* env TFIDF_SL_MAXCAP: tokcount_sl up to this many vocabulary slots */
     K1Out* k1out_host = nullptr;   /* pinned: tokcount_sl's output block, copied to k1out_dev per run */
     DevBuf k1out_dev;
@@ -158,7 +157,6 @@ struct tfidf_ctx {
     DevBuf syn_bytes, syn_off, syn_ids, syn_ntok, syn_blkfirst, syn_blkbytes, syn_cdf;
     /* stage buffers */
     DevBuf chunk_start, chunk_doc;
-    DevBuf tok_stream, chunk_tok, chunk_caps, chunk_ntok, doc_tok;   /* K1 two-pass form */
     DevBuf vkeys, vrep;
     /* vocabulary table: K1 is measurably faster at low load (fewer displaced keys behind
      * the two slots it loads per token): 1M slots (16 MB) to start, x4 past 12 % load */
@@ -218,6 +216,9 @@ struct tfidf_ctx {
     DevBuf x_rrec, x_rslot, x_reply, x_tkey, x_tdf;
     /* dense exchange (small vocabularies): gathered keys, shared positions, the DF vector */
     DevBuf x_gkeys, x_pos, x_dense;
+    /* cross-rank check of long terms (exchange_long_check): this rank's list, its send block
+     * (entries + bytes), the gathered blocks, the check's key table */
+    DevBuf x_lloc, x_lsend, x_lgath, x_ltab;
     int xchg_mode = 0;      /* env TFIDF_XCHG: 0 auto (dense up to DENSE_XCHG_MAXV terms per rank), 1 owner, 2 dense,
                                3 dense with table numbering */
     bool last_dense = false;   /* the last exchange used the dense form */
@@ -390,7 +391,6 @@ int tfidf_open(int device, tfidf_ctx** out) {
     if (km && !strcmp(km, "general")) ctx->k1_mode = 2;
     if (km && !strcmp(km, "vs")) ctx->k1_mode = 1;
     if (km && !strcmp(km, "sl")) ctx->k1_mode = 3;
-    if (km && !strcmp(km, "2p")) ctx->k1_mode = 4;
     {
         const char* sm = getenv("TFIDF_SL_MAXCAP");
         const unsigned long long v = sm ? strtoull(sm, nullptr, 0) : 0ull;
@@ -482,8 +482,7 @@ void tfidf_close(tfidf_ctx* ctx) {
     ctx->df_scratch.release();
     DevBuf* bufs[] = {&ctx->arena_buf, &ctx->in_bytes, &ctx->in_off, &ctx->in_ids, &ctx->syn_bytes, &ctx->syn_off,
                       &ctx->syn_ids, &ctx->syn_ntok, &ctx->syn_blkfirst, &ctx->syn_blkbytes, &ctx->syn_cdf,
-                      &ctx->chunk_start, &ctx->chunk_doc, &ctx->tok_stream, &ctx->chunk_tok, &ctx->chunk_caps,
-                      &ctx->chunk_ntok, &ctx->doc_tok, &ctx->vkeys, &ctx->vrep, &ctx->rec_slot, &ctx->rec_cnt,
+                      &ctx->chunk_start, &ctx->chunk_doc, &ctx->vkeys, &ctx->vrep, &ctx->rec_slot, &ctx->rec_cnt,
                       &ctx->part_doc, &ctx->part_slot, &ctx->part_cnt, &ctx->doc_recoff, &ctx->doc_npairs,
                       &ctx->doc_size, &ctx->doc_flags, &ctx->counters, &ctx->dense, &ctx->vslot, &ctx->skey0,
                       &ctx->skey1, &ctx->seq0, &ctx->seq1, &ctx->rank_of_slot, &ctx->slot_of_rank, &ctx->rank16, &ctx->pkey0,
@@ -493,7 +492,7 @@ void tfidf_close(tfidf_ctx* ctx) {
                       &ctx->doc_toff, &ctx->text, &ctx->out_term, &ctx->out_cnt,
                       &ctx->out_score, &ctx->idf_rank, &ctx->large_list, &ctx->split_tasks, &ctx->cls_off, &ctx->x_mine, &ctx->x_srec,
                       &ctx->x_sidx, &ctx->x_back, &ctx->x_cnt, &ctx->x_rrec, &ctx->x_rslot, &ctx->x_reply, &ctx->x_gkeys,
-                      &ctx->x_pos, &ctx->x_dense,
+                      &ctx->x_pos, &ctx->x_dense, &ctx->x_lloc, &ctx->x_lsend, &ctx->x_lgath, &ctx->x_ltab,
                       &ctx->x_tkey, &ctx->x_tdf, &ctx->stamps, &ctx->big_list, &ctx->big_idx, &ctx->dense_cnt, &ctx->kcnt,
                       &ctx->tile_cnt};
     for (DevBuf* b : bufs) b->release();
@@ -790,7 +789,79 @@ static int exchange_dense(tfidf_ctx* ctx, uint32_t V, const std::vector<uint64_t
     return 0;
 }
 
-static int exchange_df(tfidf_ctx* ctx, int local_rc, uint32_t V) {
+/* Cross-rank identity of terms of >= 16 bytes (TFIDF.c:229 joins words across ranks with
+ * strcmp).  A long term's identity key is a 120-bit hash of its bytes: inside a rank every
+ * key match is checked against the bytes (dev_vocab.h), and here, after the DF exchange, so is
+ * every key that two ranks share.  The ranks agree on the largest byte total of their long
+ * terms, all-gather their lists (key, length, blob offset; padded with EMPTY keys) and blobs,
+ * and every rank compares each entry with the first entry of its key (finalize.hip
+ * k_long_verify).  Every rank checks the same gathered data, so all reach the same verdict: a
+ * mismatch fails the run everywhere with TFIDF_E_CAPACITY (the terms are never merged), with
+ * the transport still usable (*agreed).  Only when some rank holds a long term (bit 32 of the
+ * agreement word), so runs without long terms pay nothing. */
+static int exchange_long_check(tfidf_ctx* ctx, uint32_t V, const uint8_t* bytes, bool* agreed) {
+    hipStream_t s = ctx->stream;
+    Xport* xp = ctx->xp;
+    const uint64_t R = (uint64_t)xp->nranks;
+    int arc = ctx->x_lloc.ensure((size_t)V * (sizeof(LongEnt) + 8) + 64) ? TFIDF_E_NOMEM : 0;
+    LongEnt* ents = ctx->x_lloc.as<LongEnt>();
+    uint64_t* src = reinterpret_cast<uint64_t*>(ents + V);
+    unsigned long long* lc = reinterpret_cast<unsigned long long*>(src + V);
+    uint64_t L = 0, B = 0;
+    if (!arc) {
+        XCHK(launch_long_list(ctx->vkeys.as<uint4>(), ctx->vrep.as<uint64_t>(), ctx->slot_of_rank.as<uint32_t>(), V, ents,
+                              src, lc, s));
+        HIPCHK(hipMemcpyAsync(ctx->hpin + 28, lc, 16, hipMemcpyDeviceToHost, s));
+        XSYNC(s);
+        L = ctx->hpin[28];
+        B = ctx->hpin[29];
+    }
+    std::vector<uint64_t> bs;
+    int rc = exchange_agree(ctx, arc, B, &bs);
+    if (rc) { *agreed = true; return rc == 1 ? TFIDF_E_STATE : rc; }
+    uint64_t maxb = 0;
+    for (uint64_t x : bs) maxb = x > maxb ? x : maxb;
+    const uint64_t lcap = maxb / 16 + 1;            /* a long term has >= 16 bytes */
+    const uint64_t bcap = (maxb + 16) & ~15ull;
+    const uint64_t n = R * lcap, tcap = table_cap(n);
+    arc = (ctx->x_lsend.ensure(lcap * sizeof(LongEnt) + bcap) || ctx->x_lgath.ensure(n * sizeof(LongEnt) + R * bcap) ||
+           ctx->x_ltab.ensure(tcap * 20))
+              ? TFIDF_E_NOMEM
+              : 0;
+    rc = exchange_agree(ctx, arc, 0, nullptr);
+    if (rc) { *agreed = true; return rc == 1 ? TFIDF_E_STATE : rc; }
+    LongEnt* se = ctx->x_lsend.as<LongEnt>();
+    uint8_t* sblob = reinterpret_cast<uint8_t*>(se + lcap);
+    HIPCHK(hipMemsetAsync(se, 0xEE, lcap * sizeof(LongEnt), s));
+    if (L) HIPCHK(hipMemcpyAsync(se, ents, L * sizeof(LongEnt), hipMemcpyDeviceToDevice, s));
+    XCHK(launch_long_bytes(ents, src, (uint32_t)L, bytes, sblob, s));
+    LongEnt* ge = ctx->x_lgath.as<LongEnt>();
+    uint8_t* gblob = reinterpret_cast<uint8_t*>(ge + n);
+    rc = xp->allgather(se, ge, lcap * sizeof(LongEnt), s);
+    if (rc) return rc;
+    rc = xp->allgather(sblob, gblob, bcap, s);
+    if (rc) return rc;
+    uint4* tkey = ctx->x_ltab.as<uint4>();
+    uint32_t* status = reinterpret_cast<uint32_t*>(lc);   /* the list's counters are read: reused */
+    HIPCHK(hipMemsetAsync(status, 0, 4, s));
+    XCHK(launch_long_verify(ge, n, lcap, gblob, bcap, tkey, reinterpret_cast<uint32_t*>(tkey + tcap), tcap, status, s));
+    ctx->hpin[30] = 0;
+    HIPCHK(hipMemcpyAsync(ctx->hpin + 30, status, 4, hipMemcpyDeviceToHost, s));
+    XSYNC(s);
+    const uint32_t st = (uint32_t)ctx->hpin[30];
+    *agreed = true;   /* the same verdict on every rank */
+    if (st & ST_LONG_COLLIDE) {
+        fprintf(stderr, "tfidf: two distinct terms of 16 bytes or more on different ranks share their 120-bit identity key\n");
+        return TFIDF_E_CAPACITY;
+    }
+    if (st & (ST_BOUNDS | ST_VOCAB_SPIN)) {
+        fprintf(stderr, "tfidf: internal bounds check tripped in the long-term check (status 0x%x)\n", st);
+        return TFIDF_E_STATE;
+    }
+    return 0;
+}
+
+static int exchange_df(tfidf_ctx* ctx, int local_rc, uint32_t V, const uint8_t* bytes) {
     std::vector<uint64_t> vs;
     /* the dense form's buffers, sized from this rank's V before the agreement; a failure
      * travels as bit 33 of step 1's word (no extra exchange): the ranks then take the owner
@@ -824,6 +895,10 @@ static int exchange_df(tfidf_ctx* ctx, int local_rc, uint32_t V) {
     bool agreed = false;
     rc = dense ? exchange_dense(ctx, V, vs, !any_long && ctx->xchg_mode != 3, &agreed)
                : exchange_owner(ctx, V, vs, &agreed);
+    if (!rc && any_long) {
+        agreed = false;
+        rc = exchange_long_check(ctx, V, bytes, &agreed);
+    }
     if (rc && rc != TFIDF_E_PEER && !agreed) ctx->xp->abort();
     return rc;
 }
@@ -893,9 +968,8 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     const bool aligned = (((uintptr_t)c.bytes & 15u) == 0);
     ctx->k1_vs = aligned && ctx->k1_mode != 2;
     if (ctx->k1_vs && ctx->vcap > K1_VS_MAX_CAP) return TFIDF_E_CAPACITY;
-    ctx->k1_sl = ctx->k1_vs && (ctx->k1_mode == 0 || ctx->k1_mode == 3 || ctx->k1_mode == 4) &&
+    ctx->k1_sl = ctx->k1_vs && (ctx->k1_mode == 0 || ctx->k1_mode == 3) &&
                  ctx->vcap <= ctx->sl_maxcap;
-    ctx->k1_2p = ctx->k1_sl && ctx->k1_mode == 4;
     /* tokcount_sl over a high-cardinality table (TFIDF_SL_MAXCAP): half-size chunks, as
      * tokcount_vs, since nearly every token is a new pair for its LDS table */
     const uint32_t cb = ctx->k1_sl ? (ctx->vcap > K1_ST_MAX_CAP ? CHUNK_BYTES : CHUNK_BYTES_ST) : CHUNK_BYTES;
@@ -972,27 +1046,8 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
             HIPCHK(hipMemcpyAsync(ctx->k1out_dev.p, ctx->k1out_host, sizeof(K1Out), hipMemcpyHostToDevice, s));
             ctx->k1out_valid = true;
         }
-        if (ctx->k1_2p) {
-            /* the token stream: each chunk's range holds at most len / 2 + its documents + 2
-             * tokens (k_chunk_tokcap), at most span / 2 + N + 3 nchunks in all */
-            ENSURE(ctx->chunk_caps, (nchunks + 1) * 8);
-            ENSURE(ctx->chunk_tok, (nchunks + 1) * 8);
-            ENSURE(ctx->chunk_ntok, nchunks * 4 + 4);
-            ENSURE(ctx->doc_tok, (size_t)N * 4 + 4);
-            ENSURE(ctx->tok_stream, (span / 2 + N + 3 * nchunks + 64) * 4);
-            TokStream ts{};
-            ts.tok = ctx->tok_stream.as<uint32_t>();
-            ts.chunk_tok = ctx->chunk_tok.as<uint64_t>();
-            ts.chunk_ntok = ctx->chunk_ntok.as<uint32_t>();
-            ts.doc_tok = ctx->doc_tok.as<uint32_t>();
-            ts.status = (uint32_t*)(cnt + 3);
-            ts.chunk_ctr = cnt + 24;
-            LCHK(launch_tok_twopass(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), nchunks, vd, ts,
-                                    ctx->chunk_caps.as<uint64_t>(), ctx->k1out_dev.as<K1Out>(), ar, s));
-        } else {
-            LCHK(launch_tokcount_sl(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd,
-                                    ctx->k1out_dev.as<K1Out>(), s));
-        }
+        LCHK(launch_tokcount_sl(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd,
+                                ctx->k1out_dev.as<K1Out>(), s));
     } else if (nchunks && ctx->k1_vs)
         LCHK(launch_tokcount_vs(c, ctx->chunk_start.as<uint64_t>(), ctx->chunk_doc.as<uint32_t>(), 0, nchunks, vd, o, s));
     else if (nchunks)
@@ -1564,7 +1619,7 @@ static int run_once(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids,
     int rc = run_local(ctx, c, dev_ids, Nt);
     mark(ctx, S_EXCHANGE);
     if (ctx->xp) {
-        rc = exchange_df(ctx, rc, ctx->run_V);
+        rc = exchange_df(ctx, rc, ctx->run_V, c.bytes);
         if (rc) return rc;
     } else {
         if (rc) return rc;
@@ -1785,7 +1840,6 @@ extern "C" int tfidf_last_run_info(tfidf_ctx* ctx, tfidf_run_info* out) {
     for (int i = 0; i < S_NSTAGES; ++i) info->ms_stage[i] = ctx->ms_stage[i];
     info->nstages = S_NSTAGES;
     info->flags = (ctx->k1_vs ? TFIDF_RUN_K1_VS : 0u) | (ctx->k1_sl ? TFIDF_RUN_K1_SL : 0u) |
-                  (ctx->k1_2p ? TFIDF_RUN_K1_2P : 0u) |
                   (ctx->xp && ctx->last_dense ? TFIDF_RUN_XCHG_DENSE : 0u);
     info->device_allocs = g_dev_allocs.load(std::memory_order_relaxed);
     info->device_alloc_bytes = g_dev_alloc_bytes.load(std::memory_order_relaxed);

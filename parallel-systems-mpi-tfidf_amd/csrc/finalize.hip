@@ -1145,7 +1145,11 @@ constexpr uint32_t K5_WAVE = 1024;    /* one wave, LDS radix sort of packed (ran
 constexpr uint32_t K5_IDX_BITS = 11;  /* index bits of a packed key (n <= 2048) */
 constexpr int K5_BATCH = 8;           /* gathers per lane in flight together */
 #ifndef K5_EB
-#define K5_EB 4                       /* bucket path: idf gathers per lane in flight together */
+#define K5_EB 4                       /* wide path: idf gathers per lane in flight together */
+#endif
+#ifndef K5_EMIT
+#define K5_EMIT 8                     /* bucket path's emission: positions per lane whose idf are gathered
+                                         before any of their stores */
 #endif
 #ifndef K5_WPS
 #define K5_WPS 4                      /* waves per SIMD the wave kernel is compiled for */
@@ -1309,6 +1313,12 @@ __device__ __forceinline__ void k5_prefetch(const K5Args& a, const uint4& m, uin
     }
 }
 
+__device__ __forceinline__ uint32_t lane_id_fresh() {
+    uint32_t l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
 /* WIDE: the instance launched when ranks exceed 32 - K5_IDX_BITS bits (its extra path
  * costs registers the common instance must not pay: c2 score 0.88 -> 1.16 ms with it) */
 template <bool WIDE>
@@ -1339,6 +1349,10 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
     uint32_t s_cur[K5_PF], c_cur[K5_PF];
     k5_prefetch(a, m_cur, lane, s_cur, c_cur);
     for (; li < lcount; li += stride) {
+        /* the lane index recomputed per document (an asm the compiler cannot hoist): held
+         * across the loop it and the LDS addresses derived from it were spilled, and each
+         * reload's vmcnt wait also waited for the next document's prefetch loads */
+        const uint32_t lane = lane_id_fresh();
         const uint32_t i = i_cur;
         const uint4 mc = m_cur;
         const uint64_t ob = ob_cur;
@@ -1562,19 +1576,19 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         /* h[d] is now bucket d's end (= bucket d+1's start).  Every position is computed
          * before any key moves (buf1 is read by the in-bucket counts), then the keys are
-         * placed in order and emitted with coalesced stores. */
-        uint32_t pk[K5_RQ], pp[K5_RQ];
+         * placed in order and emitted with coalesced stores.  Positions are computed per
+         * element (q, lane), whose key is (r[q], its index): only the positions are held
+         * (round 5 held each bucketed slot's key as well, 16 more VGPRs: 9 spilled) */
+        uint32_t pp[K5_RQ];
 #pragma unroll
         for (int q = 0; q < K5_RQ; ++q) {
             const uint32_t j = 64u * q + lane;
-            pk[q] = 0u;
             pp[q] = 0u;
             if (j < n) {
-                const uint32_t k = buf1[j], d = (k >> K5_IDX_BITS) >> hsh;
+                const uint32_t k = (r[q] << K5_IDX_BITS) | j, d = r[q] >> hsh;
                 const uint32_t gs = d ? h[d - 1] : 0u, ge = h[d];
                 uint32_t less = 0;
                 for (uint32_t f = gs; f < ge; ++f) less += buf1[f] < k ? 1u : 0u;
-                pk[q] = k;
                 pp[q] = gs + less;
             }
         }
@@ -1582,28 +1596,32 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
         for (int q = 0; q < K5_RQ; ++q)
-            if (64u * q + lane < n) buf1[pp[q]] = pk[q];
+            if (64u * q + lane < n) buf1[pp[q]] = (r[q] << K5_IDX_BITS) | (64u * q + lane);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        constexpr int EB = K5_EB;
+        /* Emission: every idf of a batch is gathered before any of its stores, and a batch
+         * covers up to K5_EMIT positions per lane.  gfx950's vmcnt counts stores as well as
+         * loads, in order, so a gather issued after a store cannot be waited for without
+         * waiting for the store: round 5's 4-position batches made each later batch (and the
+         * next document's first load) wait for the earlier batches' store acknowledgements.
+         * Only the idf values are held across the gathers; keys and counts are re-read from
+         * LDS at the store. */
+        constexpr int EB = K5_EMIT;
         for (uint32_t j0 = 0; j0 < n; j0 += 64 * EB) {
-            uint32_t key[EB], cnt[EB];
             double idf[EB];
 #pragma unroll
             for (int q = 0; q < EB; ++q) {
                 const uint32_t j = j0 + 64 * q + lane;
-                key[q] = j < n ? buf1[j] : 0u;
-                cnt[q] = j < n ? buf0[key[q] & ((1u << K5_IDX_BITS) - 1u)] : 0u;
+                idf[q] = k5_idf(a, (j < n ? buf1[j] : 0u) >> K5_IDX_BITS);
             }
-#pragma unroll
-            for (int q = 0; q < EB; ++q) idf[q] = k5_idf(a, key[q] >> K5_IDX_BITS);
 #pragma unroll
             for (int q = 0; q < EB; ++q) {
                 const uint32_t j = j0 + 64 * q + lane;
                 if (j < n) {
-                    sto(&a.out_term[ob + j], (uint32_t)(key[q] >> K5_IDX_BITS));
-                    sto(&a.out_cnt[ob + j], (uint32_t)(cnt[q]));
-                    sto(&a.out_score[ob + j], (double)(((double)cnt[q] / ds) * idf[q])); /* TFIDF.c:202,243-244 */
+                    const uint32_t key = buf1[j], cnt = buf0[key & ((1u << K5_IDX_BITS) - 1u)];
+                    sto(&a.out_term[ob + j], (uint32_t)(key >> K5_IDX_BITS));
+                    sto(&a.out_cnt[ob + j], (uint32_t)(cnt));
+                    sto(&a.out_score[ob + j], (double)(((double)cnt / ds) * idf[q])); /* TFIDF.c:202,243-244 */
                 }
             }
         }
@@ -2723,6 +2741,102 @@ int launch_dense_scatter(const uint4* mine, const uint32_t* df, uint32_t V, cons
 int launch_dense_gather(const uint32_t* dense, const uint32_t* pos, uint32_t V, uint32_t* df_global, hipStream_t s) {
     if (!V) return 0;
     k_dense_gather<<<grid_for(V), NT, 0, s>>>(dense, pos, V, df_global);
+    return ok();
+}
+
+/* ---- cross-rank identity of long terms (kernels.h LongEnt).  Within a rank a long term's
+ * key match is verified against the incumbent's bytes (dev_vocab.h); across ranks the DF
+ * exchange matches keys only, so every key that two ranks share is checked here against the
+ * terms' bytes, as TFIDF.c:229's strcmp would compare them. */
+__global__ void k_long_list(const uint4* __restrict__ vkeys, const uint64_t* __restrict__ vrep,
+                            const uint32_t* __restrict__ slot_of_rank, uint32_t V, LongEnt* __restrict__ ents,
+                            uint64_t* __restrict__ src, unsigned long long* __restrict__ cnt) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= V) return;
+    const uint32_t sl = slot_of_rank[r];
+    const uint4 k = vkeys[sl];
+    if ((k.w >> 24) != 0xFFu) return;   /* short term: its key is its bytes */
+    const uint64_t rep = vrep[sl];      /* (length << 40) | corpus offset of one occurrence */
+    const uint32_t len = (uint32_t)(rep >> 40);
+    const unsigned long long e = atomicAdd(&cnt[0], 1ull);
+    const unsigned long long b = atomicAdd(&cnt[1], (unsigned long long)len);
+    LongEnt x;
+    x.key = k;
+    x.len = len;
+    x.pad = 0;
+    x.boff = b;
+    ents[e] = x;
+    src[e] = rep & ((1ull << 40) - 1ull);
+}
+/* one wave per entry: its bytes from the corpus into the rank's blob */
+__global__ void k_long_bytes(const LongEnt* __restrict__ ents, const uint64_t* __restrict__ src, uint32_t n,
+                             const uint8_t* __restrict__ bytes, uint8_t* __restrict__ blob) {
+    const uint32_t e = blockIdx.x * (NT / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (e >= n) return;
+    const uint64_t s0 = src[e], d0 = ents[e].boff;
+    const uint32_t len = ents[e].len;
+    for (uint32_t i = lane; i < len; i += 64) blob[d0 + i] = bytes[s0 + i];
+}
+__global__ void k_long_insert(const LongEnt* __restrict__ g, uint64_t n, uint4* __restrict__ tkey, uint64_t tmask,
+                              uint32_t* __restrict__ tpos, uint32_t* __restrict__ status) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 k = g[i].key;
+        const uint64_t hi = ((uint64_t)k.w << 32) | k.z;
+        if (hi == KEY_EMPTY_HI) continue;   /* padding */
+        bool claimed = false;
+        const uint32_t sl = owner_insert(tkey, tmask, ((uint64_t)k.y << 32) | k.x, hi, &claimed, status);
+        if (sl == INVALID_SLOT) atomicOr(status, ST_BOUNDS);
+        else atomicMin(&tpos[sl], (uint32_t)i);
+    }
+}
+/* one wave per gathered entry: against the first entry of its key (the smallest gathered
+ * index), length and bytes */
+__global__ void k_long_verify(const LongEnt* __restrict__ g, uint64_t n, uint64_t lcap, const uint8_t* __restrict__ gblob,
+                              uint64_t bcap, const uint4* __restrict__ tkey, uint64_t tmask,
+                              const uint32_t* __restrict__ tpos, uint32_t* __restrict__ status) {
+    const uint64_t i = (uint64_t)blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (i >= n) return;
+    const LongEnt a = g[i];
+    const uint64_t hi = ((uint64_t)a.key.w << 32) | a.key.z;
+    if (hi == KEY_EMPTY_HI) return;
+    const uint32_t sl = owner_find(tkey, tmask, ((uint64_t)a.key.y << 32) | a.key.x, hi);
+    if (sl == INVALID_SLOT) { if (lane == 0) atomicOr(status, ST_BOUNDS); return; }
+    const uint64_t j = tpos[sl];
+    if (j == i) return;   /* the key's first entry */
+    const LongEnt b = g[j];
+    bool diff = a.len != b.len;
+    if (!diff) {
+        const uint8_t* pa = gblob + (i / lcap) * bcap + a.boff;
+        const uint8_t* pb = gblob + (j / lcap) * bcap + b.boff;
+        for (uint32_t k = lane; k < a.len && !diff; k += 64) diff = pa[k] != pb[k];
+    }
+    if (__ballot(diff) != 0ull && lane == 0) atomicOr(status, ST_LONG_COLLIDE);
+}
+int launch_long_list(const uint4* vkeys, const uint64_t* vrep, const uint32_t* slot_of_rank, uint32_t V, LongEnt* ents,
+                     uint64_t* src, unsigned long long* cnt, hipStream_t s) {
+    if (hipMemsetAsync(cnt, 0, 16, s) != hipSuccess) return -1;
+    if (!V) return 0;
+    k_long_list<<<grid_for(V), NT, 0, s>>>(vkeys, vrep, slot_of_rank, V, ents, src, cnt);
+    return ok();
+}
+int launch_long_bytes(const LongEnt* ents, const uint64_t* src, uint32_t n, const uint8_t* bytes, uint8_t* blob,
+                      hipStream_t s) {
+    if (!n) return 0;
+    k_long_bytes<<<(n + NT / 64 - 1) / (NT / 64), NT, 0, s>>>(ents, src, n, bytes, blob);
+    return ok();
+}
+int launch_long_verify(const LongEnt* g, uint64_t n, uint64_t lcap, const uint8_t* gblob, uint64_t bcap, uint4* tkey,
+                       uint32_t* tpos, uint64_t tcap, uint32_t* status, hipStream_t s) {
+    if (hipMemsetAsync(tkey, 0xEE, tcap * 16, s) != hipSuccess || hipMemsetAsync(tpos, 0xFF, tcap * 4, s) != hipSuccess)
+        return -1;
+    if (!n) return 0;
+    const uint64_t nb = (n + NT - 1) / NT;
+    k_long_insert<<<(unsigned)(nb < 8192 ? nb : 8192), NT, 0, s>>>(g, n, tkey, tcap - 1, tpos, status);
+    if (hipGetLastError() != hipSuccess) return -1;
+    const uint64_t wb = (n + NT / 64 - 1) / (NT / 64);
+    if (wb > 0x7FFFFFFFull) return -3;
+    k_long_verify<<<(unsigned)wb, NT, 0, s>>>(g, n, lcap, gblob, bcap, tkey, tcap - 1, tpos, status);
     return ok();
 }
 

@@ -108,21 +108,6 @@ int launch_tokcount_vs(const CorpusDev& c, const uint64_t* chunk_start, const ui
  * 16-byte aligned corpus base; -3 when the vocabulary exceeds K1_ST_MAX_CAP slots */
 int launch_tokcount_sl(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc, uint64_t c0,
                        uint64_t c1, const VocabDev& v, const K1Out* o_dev, hipStream_t s);
-/* K1 two-pass form (tokcount_sl.hip, TFIDF_K1=2p): K1a tokenizes and resolves every token into
- * a token stream of LDS keys (chunk ranges bounded by k_chunk_tokcap + a scan into chunk_tok),
- * K1b counts the stream per group with k_tokcount_sl's table and flush.  caps: nch + 1 u64
- * scratch; -3 when the vocabulary exceeds K1_SL_MAX_CAP slots, -2 when the arena is short */
-struct TokStream {
-    uint32_t* tok;                   /* token stream: 1 << 31 | document in group << sb | slot (0: unresolved) */
-    const uint64_t* chunk_tok;       /* nch + 1: each chunk's first stream index (scan of its bound) */
-    uint32_t* chunk_ntok;            /* nch: tokens of each chunk */
-    uint32_t* doc_tok;               /* per document starting a group (not a chunk): its chunk-local first token */
-    uint32_t* status;
-    unsigned long long* chunk_ctr;   /* K1a's chunk schedule (zeroed per run) */
-};
-int launch_tok_twopass(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc, uint64_t nch,
-                       const VocabDev& v, const TokStream& t, uint64_t* caps, const K1Out* o_dev, Arena& ar,
-                       hipStream_t s);
 
 
 /* vocabulary finalisation */
@@ -290,6 +275,25 @@ int launch_dense_gather(const uint32_t* dense, const uint32_t* pos, uint32_t V, 
  * dense[sumv] accumulates the keys first held by each rank (global V after the sum) */
 int launch_dense_merge_ids(const uint4* gkeys, uint64_t maxv, uint32_t R, uint32_t me, uint32_t V, uint32_t* lbm,
                            const uint32_t* df, uint64_t sumv, uint32_t* pos, uint32_t* dense, hipStream_t s);
+
+/* Cross-rank identity of terms of >= 16 bytes (engine.cpp exchange_long_check; TFIDF.c:229's
+ * strcmp): a long term's identity key is a 120-bit hash, so the ranks all-gather their long
+ * terms (key, length, bytes) and every rank checks each key two ranks share byte by byte. */
+struct LongEnt {
+    uint4 key;
+    uint32_t len, pad;
+    uint64_t boff;             /* its bytes in the rank's blob */
+};
+/* this rank's long terms: ents[0, cnt[0]) (blob offsets from an atomic byte counter cnt[1]),
+ * src[e] = the corpus offset of one occurrence (the vocabulary's rep) */
+int launch_long_list(const uint4* vkeys, const uint64_t* vrep, const uint32_t* slot_of_rank, uint32_t V, LongEnt* ents,
+                     uint64_t* src, unsigned long long* cnt, hipStream_t s);
+int launch_long_bytes(const LongEnt* ents, const uint64_t* src, uint32_t n, const uint8_t* bytes, uint8_t* blob,
+                      hipStream_t s);
+/* every gathered entry (R blocks of lcap, blobs of bcap bytes each; padding keys EMPTY)
+ * compared with the first entry of its key: a different length or byte sets ST_LONG_COLLIDE */
+int launch_long_verify(const LongEnt* g, uint64_t n, uint64_t lcap, const uint8_t* gblob, uint64_t bcap, uint4* tkey,
+                       uint32_t* tpos, uint64_t tcap, uint32_t* status, hipStream_t s);
 
 /* synthetic corpus generation on the device */
 struct SynSpecDev;

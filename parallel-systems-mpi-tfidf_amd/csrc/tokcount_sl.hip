@@ -205,12 +205,13 @@ __device__ __forceinline__ uint32_t bkt_match(const BktK& kk, uint32_t key) {
  * during a group, so a key is never claimed twice: a walker meets the key's slot (its CAS
  * returns the key) before any slot that was empty when the key was placed.  Occupancy from
  * the keys' top bits (every key has bit 31 set): the top bytes of four slots gathered by two
- * v_perm, their bit 7 moved to one bit each by a multiply. */
+ * v_perm, their bit 7 moved to one bit each. */
 __device__ __forceinline__ uint32_t bkt_occ(const BktK& kk) {   /* bit i: slot i holds a key */
     const uint32_t ta = __builtin_amdgcn_perm(kk.a.y, kk.a.x, 0x0C0C0703u) | __builtin_amdgcn_perm(kk.a.w, kk.a.z, 0x07030C0Cu);
     const uint32_t tb = __builtin_amdgcn_perm(kk.b.y, kk.b.x, 0x0C0C0703u) | __builtin_amdgcn_perm(kk.b.w, kk.b.z, 0x07030C0Cu);
-    /* bits 7, 15, 23, 31 -> bits 28..31 (no carries: the partial products do not overlap) */
-    return (((ta & 0x80808080u) * 0x00204081u) >> 28) | ((((tb & 0x80808080u) * 0x00204081u) >> 28) << 4);
+    /* bit 7 of each byte, weighted 1..128 by two v_dot4_u32_u8 */
+    return __builtin_amdgcn_udot4(ta & 0x80808080u, 0x08040201u,
+                                  __builtin_amdgcn_udot4(tb & 0x80808080u, 0x80402010u, 0u, false), false) >> 7;
 }
 __device__ __forceinline__ uint32_t bkt_pref(uint32_t key) { return (key * 0x85EBCA77u) >> 29; }
 /* the first slot at or after p (cyclically) that `occ` marks empty; BW when none */
@@ -543,7 +544,7 @@ __device__ __forceinline__ void sl_flush_few(SlShared& S, const K1Out* o, uint32
 }
 
 /* The LDS count of one round's keys (key32 = 1 << 31 | document in group << sb | vocabulary slot;
- * 0: no token), shared by k_tokcount_sl and the two-pass form's counting kernel. */
+ * 0: no token). */
 #ifdef SL_STAMPS
 #define SL_STC , st_cnt
 #define SL_STC_ARG , unsigned long long* st_cnt
@@ -560,12 +561,11 @@ __device__ __forceinline__ void lds_count(SlShared& S, const K1Out* o, uint32_t 
     const bool over = wclaims >= WAVE_CLAIMS;
     const uint32_t b = bkt_hash(key);
     const BktK kk = bkt_read(S.TK, b);
-    /* the key's slot: independent compares OR-ed into the index (at most one
-     * slot matches), no select chain */
+    /* the key's slot: at most one slot matches, so its index bits are ORs of the lane masks
+     * (scalar ORs, three selects; seven selects before) */
     const bool m0 = kk.a.x == key, m1 = kk.a.y == key, m2 = kk.a.z == key, m3 = kk.a.w == key;
     const bool m4 = kk.b.x == key, m5 = kk.b.y == key, m6 = kk.b.z == key, m7 = kk.b.w == key;
-    const uint32_t j = (m1 ? 1u : 0u) | (m2 ? 2u : 0u) | (m3 ? 3u : 0u) | (m4 ? 4u : 0u) | (m5 ? 5u : 0u) |
-                       (m6 ? 6u : 0u) | (m7 ? 7u : 0u);
+    const uint32_t j = ((m1 | m3 | m5 | m7) ? 1u : 0u) | ((m2 | m3 | m6 | m7) ? 2u : 0u) | ((m4 | m5 | m6 | m7) ? 4u : 0u);
     const bool found = m0 | m1 | m2 | m3 | m4 | m5 | m6 | m7;
     const uint32_t pref = bkt_pref(key);
     uint32_t occ = bkt_occ(kk);
@@ -1062,418 +1062,5 @@ int launch_tokcount_sl(const CorpusDev& c, const uint64_t* chunk_start, const ui
     const uint64_t wgs = (uint64_t)ncu * WG_PER_CU;
     const uint64_t grid = (c1 - c0) < wgs ? (c1 - c0) : wgs;
     k_tokcount_sl<<<(unsigned)grid, NT, 0, s>>>(c, chunk_start, chunk_doc, c0, c1, v, o_dev, sbits, gcap);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-/* =========================================================================================
- * Two-pass form (TFIDF_K1=2p).  The fused kernel above holds a tokenizer, a vocabulary
- * round pipeline and a 28 KiB LDS count table in one workgroup, which leaves it 126 VGPRs,
- * four waves per SIMD and a block barrier per group; its waves wait on dependent LDS and
- * memory round trips most of their time.  Here the same work is split at the
- * round's (document, slot) key:
- *   K1a k_tok_resolve — one wave per chunk, no LDS table and no block barrier: tokenize,
- *       build each term's identity key, resolve it in the vocabulary (the same round
- *       pipeline and rare paths as k_tokcount_sl) and store the token's LDS key
- *       (1 << 31 | document in group << sb | slot; 0: unresolved) in the chunk's range of a
- *       token stream, in corpus order;
- *   K1b k_tok_count — k_tokcount_sl's workgroup, table and flush, fed from the token stream
- *       (one coalesced dword per token) instead of a tokenizer: docSize and the token total
- *       are counted from the keys.
- * The stream costs 4 bytes per token written and read (c2: 0.53 GB each way).  A chunk's
- * range is bounded before K1a runs (k_chunk_tokcap): tokens start only after whitespace or at
- * a document start, so a document piece of b bytes holds at most (b + 1) / 2 tokens.
- * Replaces the same reference loops as k_tokcount_sl (TFIDF.c:130-196).
- * ========================================================================================= */
-namespace {
-
-constexpr int A_NT = 256;
-constexpr int A_NWAVE = A_NT / 64;
-#ifndef TA_WPS
-#define TA_WPS 6            /* waves per SIMD the tokenize pass is compiled for (<= 80 VGPRs) */
-#endif
-#ifndef TA_WG_PER_CU
-#define TA_WG_PER_CU 6
-#endif
-
-constexpr int TLA = 992;              /* token entries per wave and step: one per byte of the step's 62 owned
-                                         groups at most (document starts need no whitespace before them), so
-                                         one list always takes a whole step */
-struct TaWave {
-    uint4 stage[64];                    /* the wave's step: [sb - 16, sb + 1008) */
-    uint32_t tl[TLA];                   /* token entries */
-    int32_t gdoc[GCAP + 1];             /* document starts of the group, relative to b0 (clamped) */
-};
-struct TaShared {
-    TaWave w[A_NWAVE];
-    uint4 sel[16];                      /* v_perm selectors of a term of length n */
-};
-
-/* a round of tokens between issue (vocabulary loads sent) and their store.  A round never
- * spans two groups or chunks, so its tokens are consecutive in the stream and share the
- * wave-uniform bases below; per lane only the key, the home pair and the token's place. */
-struct RoundA {
-    uint32_t k0, k1, k2, k3;            /* identity key */
-    uint32_t h;                         /* even home slot */
-    uint32_t rk;                        /* document in group << 2 | kind (0 none, 1 short, 2 long / past the window) */
-    int32_t ap;                         /* token start relative to the round's b0 (kind 2) */
-    uint4 s0, s1;                       /* the pair's two slots */
-};
-struct RoundBase {                      /* wave-uniform */
-    uint64_t dst;                       /* stream index of lane 0's token */
-    uint64_t b0;                        /* the chunk's base */
-    uint32_t gd0;                       /* the group's first document */
-};
-
-__global__ void k_chunk_tokcap(const uint64_t* __restrict__ chunk_start, const uint32_t* __restrict__ chunk_doc,
-                               uint64_t nch, uint64_t* __restrict__ cap) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nch) return;
-    const uint64_t len = chunk_start[i + 1] - chunk_start[i];
-    cap[i] = len / 2 + (uint64_t)(chunk_doc[i + 1] - chunk_doc[i] + 1) + 2;
-}
-
-}  // namespace
-
-__global__ __launch_bounds__(A_NT, TA_WPS) void k_tok_resolve(CorpusDev c, const uint64_t* __restrict__ chunk_start,
-                                                              const uint32_t* __restrict__ chunk_doc, uint64_t nch,
-                                                              VocabDev v, TokStream t, uint32_t sb, uint32_t gcap) {
-    __shared__ __attribute__((aligned(16))) TaShared S;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if (tid < 64) {
-        const uint32_t n = (uint32_t)tid >> 2, k = (uint32_t)tid & 3u;
-        (&S.sel[n].x)[k] = perm_sel(n, k);
-    }
-    lds_barrier();   /* the only block barrier: the waves are independent from here on */
-    TaWave& W = S.w[wid];
-    uint8_t* const stage = reinterpret_cast<uint8_t*>(&W.stage[0]);
-    uint32_t* const tl = W.tl;
-    const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void*)v.keys, 0, (int)((v.mask + 1) * 16),
-                                                                         RSRC_WORD3);
-    uint32_t* const tok = t.tok;
-    uint32_t* const status = t.status;
-
-    RoundA pend, acc;
-    pend.k0 = pend.k1 = pend.k2 = pend.k3 = 0;
-    pend.h = pend.rk = 0;
-    pend.ap = 0;
-    pend.s0 = pend.s1 = make_uint4(0, 0, 0, 0);
-    acc = pend;
-    RoundBase pb{0, 0, 0}, ab{0, 0, 0};
-    uint32_t fill = 0;   /* wave-uniform: built lanes of acc */
-
-    auto promote = [&]() {
-        pend.k0 = acc.k0; pend.k1 = acc.k1; pend.k2 = acc.k2; pend.k3 = acc.k3;
-        pend.h = acc.h; pend.rk = acc.rk; pend.ap = acc.ap;
-        pend.s0 = bload16<0>(vrs, (int32_t)(pend.h << 4));
-        pend.s1 = bload16<0>(vrs, (int32_t)(pend.h << 4) + 16);
-        pb = ab;
-        acc.rk = 0u;
-        fill = 0u;
-    };
-    auto finish = [&]() {
-        const RoundA& r = pend;
-        const bool h0 = ((r.s0.x ^ r.k0) | (r.s0.y ^ r.k1) | (r.s0.z ^ r.k2) | (r.s0.w ^ r.k3)) == 0u;
-        const bool h1 = ((r.s1.x ^ r.k0) | (r.s1.y ^ r.k1) | (r.s1.z ^ r.k2) | (r.s1.w ^ r.k3)) == 0u;
-        uint32_t slot = r.h + (h0 ? 0u : 1u);
-        const uint32_t kind = r.rk & 3u;
-        const bool need = (kind == 2u) | ((kind == 1u) & !(h0 | h1));
-        if (__ballot(need) != 0ull) {
-            if (need) {
-                const uint64_t dend = c.doc_off[pb.gd0 + (r.rk >> 2) + 1];   /* unclamped: long terms cross chunks */
-                slot = resolve_slow(c.bytes, v.keys, v.rep, v.mask, status, kind, r.k0, r.k1, r.k2, r.k3,
-                                    pb.b0 + (uint64_t)(int64_t)r.ap, dend);
-            }
-        }
-        if (kind != 0u)
-            gmem(tok)[pb.dst + (uint32_t)lane] = slot != INVALID_SLOT ? (0x80000000u | ((r.rk >> 2) << sb) | slot) : 0u;
-    };
-    /* a round is cut at every group and chunk end: the partial round goes out as it is */
-    auto cut = [&]() {
-        if (fill) {
-            finish();
-            promote();
-        }
-    };
-
-    uint64_t chunk;
-    {
-        unsigned long long x = 0;
-        if (lane == 0) x = gatomic_add(t.chunk_ctr, 1ull);
-        chunk = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x) |
-                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32);
-    }
-    while (chunk < nch) {
-        /* the next claim's round trip hides behind this chunk */
-        unsigned long long nxv = 0;
-        if (lane == 0) nxv = gatomic_add(t.chunk_ctr, 1ull);
-        const uint64_t cs = chunk_start[chunk], ce = chunk_start[chunk + 1];
-        const uint32_t dfirst = chunk_doc[chunk], dlast = chunk_doc[chunk + 1];
-        const uint64_t tbase = t.chunk_tok[chunk];
-        const uint64_t tcap = t.chunk_tok[chunk + 1] - tbase;
-        uint32_t ti = 0;   /* wave-uniform: tokens of the chunk so far */
-        if (cs < ce) {
-            const uint64_t b0 = cs & ~(uint64_t)15;
-            const uint64_t rb = b0 >= 16 ? b0 - 16 : 0;
-            const int32_t shift = (int32_t)(b0 - rb);
-            const uint64_t avail = c.nbytes > rb ? ((c.nbytes - rb + 15) & ~(uint64_t)15) : 0;
-            const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(c.bytes + rb), 0, (int)(avail < 0x7FFFFFF0ull ? avail : 0x7FFFFFF0ull), RSRC_WORD3);
-            const int32_t span = (int32_t)(ce - b0);
-            const int32_t cs_rel = (int32_t)(cs - b0);
-            const int32_t lo_rel = c.lo > b0 ? (c.lo - b0 > (uint64_t)span ? span : (int32_t)(c.lo - b0)) : -64;
-            const int32_t hi_rel = c.hi - b0 > (uint64_t)span + 64 ? span + 64 : (int32_t)(c.hi - b0);
-            for (uint32_t gd0 = dfirst; gd0 <= dlast; gd0 += gcap) {
-                const uint32_t ng = (dlast + 1 - gd0) < gcap ? (dlast + 1 - gd0) : gcap;
-                if (gd0 != dfirst && lane == 0) gmem(t.doc_tok)[gd0] = ti;   /* K1b's group boundary */
-                for (uint32_t k = (uint32_t)lane; k <= ng; k += 64) {
-                    const uint64_t d = c.doc_off[gd0 + k];
-                    W.gdoc[k] = d < b0 ? -64 : (d - b0 > (uint64_t)span + 64 ? span + 64 : (int32_t)(d - b0));
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                const int32_t g0 = __builtin_amdgcn_readfirstlane(W.gdoc[0]);
-                const int32_t gn = __builtin_amdgcn_readfirstlane(W.gdoc[ng]);
-                const int32_t gs = g0 > cs_rel ? g0 : cs_rel;
-                const int32_t ge = gn < span ? gn : span;
-                if (gs < ge) {
-                    const int32_t bs = gs & ~15;
-                    const int32_t nsteps = (ge - bs + WSTEP - 1) / WSTEP;
-                    const bool inner_all = bs >= lo_rel + 16 && bs + nsteps * WSTEP + 16 <= hi_rel;
-                    uint4 pf = bload16<2>(crs, bs + 16 * lane - 16 + shift);
-                    uint32_t wr = 0;
-                    int32_t wcur = g0, wnext = ng > 1 ? __builtin_amdgcn_readfirstlane(W.gdoc[1]) : gn;
-                    for (int32_t s = 0; s < nsteps; ++s) {
-                        const int32_t sbp = bs + s * WSTEP;
-                        uint32_t ntok;
-                        {   /* tokenize the step into the wave's token list */
-                            const int32_t gpos = sbp + 16 * lane - 16;
-                            const uint4 cur = pf;
-                            pf = bload16<2>(crs, sbp + WSTEP + 16 * lane - 16 + shift);   /* next step (harmless past ge) */
-                            reinterpret_cast<uint4*>(stage)[lane] = cur;
-                            uint32_t lt9 = 0;
-                            uint32_t ws = ws_mask16_dot(cur, lt9);
-                            if (!inner_all) ws |= outside16(gpos, lo_rel, hi_rel);
-                            while (wr + 1 < ng && wnext <= sbp) {
-                                ++wr;
-                                wcur = wnext;
-                                wnext = __builtin_amdgcn_readfirstlane(W.gdoc[wr + 1]);
-                            }
-                            uint32_t ds = 0, base = wr;
-                            const bool multi = wnext < sbp + WSTEP + 16 || wcur + 16 >= sbp;
-                            if (multi) {
-                                for (uint32_t k = wr; k <= ng; ++k) {
-                                    const int32_t sk = __builtin_amdgcn_readfirstlane(W.gdoc[k]);
-                                    if (sk >= sbp + WSTEP + 16) break;
-                                    base += (k > wr && sk < gpos) ? 1u : 0u;
-                                    if (sk >= gpos && sk < gpos + 16) ds |= 1u << (uint32_t)(sk - gpos);
-                                }
-                            }
-                            const uint32_t prev = (lane_prev(ws) >> 15) & 1u;
-                            uint32_t own = (lane >= 1 && lane <= 62) ? 0xFFFFu : 0u;
-                            if (!(sbp >= gs && sbp + WSTEP <= ge) && own) own &= ~outside16(gpos, gs, ge);
-                            const uint32_t starts = ~ws & ((ws << 1) | prev | ds) & own & 0xFFFFu;
-                            uint32_t nul = 0;
-                            if (__ballot(lt9 != 0u) != 0ull)
-                                nul = compress4(zero_bits(cur.x)) | (compress4(zero_bits(cur.y)) << 4) |
-                                      (compress4(zero_bits(cur.z)) << 8) | (compress4(zero_bits(cur.w)) << 12);
-                            const uint32_t stop = ws | ds;
-                            const uint32_t stop32 = stop | (lane_next(stop) << 16), nul32 = nul | (lane_next(nul) << 16);
-                            const uint32_t nmine = (uint32_t)__popc(starts);
-                            const uint32_t incl = wave_incl_scan(nmine);
-                            ntok = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-                            if ((uint64_t)ti + ntok > tcap) {   /* the chunk's bound (never, by the count argument) */
-                                if (lane == 0) atomicOr(status, ST_BOUNDS);
-                                ntok = 0;
-                            }
-                            if (ntok == 0) continue;
-                            uint32_t sm = starts, idx = incl - nmine;
-                            while (sm) {
-                                const uint32_t i = __builtin_ctz(sm);
-                                sm &= sm - 1;
-                                const uint32_t e = ((stop32 >> i) & ~1u) | (nul32 >> i);
-                                const uint32_t len = e ? (uint32_t)__builtin_ctz(e) : LEN_LONG;
-                                uint32_t rel = base;
-                                if (ds & ((2u << i) - 1u))
-                                    while (rel + 1 < ng && W.gdoc[rel + 1] <= gpos + (int32_t)i) ++rel;
-                                tl[idx] = ((uint32_t)lane << 4 | i) | ((len < 16u ? len : LEN_LONG) << 10) | (rel << 16);
-                                ++idx;
-                            }
-                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                            __builtin_amdgcn_wave_barrier();
-                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                        }
-                        /* rounds of 64 filled across steps; each round's tokens are consecutive */
-                        for (uint32_t tt = 0; tt < ntok;) {
-                            if (fill == 0u) {
-                                ab.dst = tbase + ti + tt;
-                                ab.b0 = b0;
-                                ab.gd0 = gd0;
-                            }
-                            const uint32_t m = (64u - fill) < (ntok - tt) ? (64u - fill) : (ntok - tt);
-                            if ((uint32_t)lane >= fill && (uint32_t)lane < fill + m) {
-                                const uint32_t e = tl[tt + (uint32_t)lane - fill];
-                                const uint32_t pos = e & 1023u, len = (e >> 10) & 31u;
-                                acc.rk = ((e >> 16) << 2) | (len == LEN_LONG ? 2u : 1u);
-                                acc.ap = sbp - 16 + (int32_t)pos;
-                                const u32x4u raw = *reinterpret_cast<const u32x4u*>(stage + pos);
-                                const uint4 sl = S.sel[len & 15u];
-                                acc.k0 = __builtin_amdgcn_perm(0x09090909u, raw.x, sl.x);
-                                acc.k1 = __builtin_amdgcn_perm(0x09090909u, raw.y, sl.y);
-                                acc.k2 = __builtin_amdgcn_perm(0x09090909u, raw.z, sl.z);
-                                acc.k3 = __builtin_amdgcn_perm(0x09090909u, raw.w, sl.w);
-                                acc.h = (uint32_t)key_hash(((uint64_t)acc.k1 << 32) | acc.k0,
-                                                           ((uint64_t)acc.k3 << 32) | acc.k2) &
-                                        (uint32_t)v.mask & ~1u;
-                            }
-                            tt += m;
-                            fill += m;
-                            if (fill == 64u) {
-                                finish();
-                                promote();
-                            }
-                        }
-                        ti += ntok;
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                        __builtin_amdgcn_wave_barrier();
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    }
-                }
-                cut();
-            }
-        }
-        if (lane == 0) gmem(t.chunk_ntok)[chunk] = ti;
-        chunk = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)nxv) |
-                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(nxv >> 32)) << 32);
-    }
-    cut();
-    finish();   /* drain */
-}
-
-__global__ __launch_bounds__(NT, WG_PER_CU * NT / 256) void k_tok_count(const uint64_t* __restrict__ doc_off,
-                                                                      const uint64_t* __restrict__ chunk_start,
-                                                                      const uint32_t* __restrict__ chunk_doc,
-                                                                      uint64_t nch, TokStream t,
-                                                                      const K1Out* __restrict__ o, uint32_t sb,
-                                                                      uint32_t gcap) {
-    __shared__ __attribute__((aligned(16))) SlShared S;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    unsigned long long tokens_w = 0;
-    bool clean = false;
-#ifdef SL_STAMPS
-    unsigned long long st_cnt[8] = {};
-#endif
-    const uint32_t* const tok = t.tok;
-    if (tid == 0) S.next_chunk = gatomic_add(o->chunk_ctr, 1ull);
-    lds_barrier();
-    unsigned long long claim = 0;
-    for (uint64_t chunk = (uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S.next_chunk) |
-                          ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S.next_chunk >> 32)) << 32);
-         chunk < nch;) {
-        if (tid == 0) claim = gatomic_add(o->chunk_ctr, 1ull);
-        const uint64_t cs = chunk_start[chunk], ce = chunk_start[chunk + 1];
-        const uint32_t dfirst = chunk_doc[chunk], dlast = chunk_doc[chunk + 1];
-        const uint64_t tbase = t.chunk_tok[chunk];
-        const uint32_t ntk = t.chunk_ntok[chunk];
-        /* the chunk's stream range as a buffer: 16-byte loads past its end read zeros */
-        const __amdgpu_buffer_rsrc_t trs =
-            __builtin_amdgcn_make_buffer_rsrc((void*)(tok + tbase), 0, (int)(ntk * 4u), RSRC_WORD3);
-        if (cs < ce) {
-            if (!clean) {
-                uint4* tt = reinterpret_cast<uint4*>(S.TK);
-                for (int j = tid; j < 2 * TB / 4; j += NT) tt[j] = make_uint4(0, 0, 0, 0);
-                clean = true;
-            }
-            for (uint32_t gd0 = dfirst; gd0 <= dlast; gd0 += gcap) {
-                const uint32_t ng = (dlast + 1 - gd0) < gcap ? (dlast + 1 - gd0) : gcap;
-                const uint32_t t0 = gd0 == dfirst ? 0u : t.doc_tok[gd0];
-                const bool more = gd0 + gcap > gd0 && gd0 + gcap <= dlast;
-                uint32_t t1 = more ? t.doc_tok[gd0 + gcap] : ntk;
-                if (t1 < t0 || t1 > ntk) {   /* K1a's boundaries (never) */
-                    if (tid == 0) atomicOr(o->status, ST_BOUNDS);
-                    t1 = t0;
-                }
-                if (tid < GCAP) { S.dsz[tid] = 0; S.dpart[tid] = 0; }
-                if ((uint32_t)tid < ng) S.dfull[tid] = doc_off[gd0 + tid] >= cs && doc_off[gd0 + tid + 1] <= ce;
-                lds_barrier();
-                uint32_t wclaims = 0;
-                /* super-rounds of 256 tokens: lane L holds tokens 4L .. 4L+3 of one 16-byte load (a
-                 * 1 KiB piece per wave, the next one in flight while four rounds are counted: one
-                 * dword per lane and round left each wave HBM-latency-bound) */
-                const uint32_t nsr = (t1 - t0 + 255u) / 256u;
-                uint32_t i = t0 + (uint32_t)wid * 256u + 4u * (uint32_t)lane;
-                uint4 nk = bload16<2>(trs, (int32_t)(i * 4u));
-                for (uint32_t k = (uint32_t)wid; k < nsr; k += NWAVE) {
-                    const uint4 cur = nk;
-                    const uint32_t i0 = i;
-                    i += 256u * NWAVE;
-                    nk = bload16<2>(trs, (int32_t)(i * 4u));   /* the wave's next super-round (zeros past the range) */
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const uint32_t key = (i0 + (uint32_t)q < t1) ? (&cur.x)[q] : 0u;
-                        if (key) wave_agg_add(S.dsz, (key & 0x7FFFFFFFu) >> sb);
-                        tokens_w += (uint32_t)__popcll(__ballot(key != 0u));
-                        lds_count(S, o, key, wclaims, gd0, sb SL_STC);
-                    }
-                }
-#ifdef SL_STAMPS
-                if (ng <= FEW) {
-                    unsigned long long st_acc[SL_NPH] = {};
-                    unsigned long long st_t = 0;
-                    sl_flush_few(S, o, gd0, ng, sb, st_acc, st_t);
-                } else
-#else
-                if (ng <= FEW) sl_flush_few(S, o, gd0, ng, sb);
-                else
-#endif
-                    sl_flush(S, o, gd0, ng, sb);
-                if ((uint32_t)tid < ng) {
-                    const uint32_t n = S.dsz[tid];
-                    if (n) {
-                        if (S.dfull[tid]) gmem(o->doc_size)[gd0 + tid] = n;
-                        else atomicAdd(&o->doc_size[gd0 + tid], n);
-                    }
-                }
-                lds_barrier();
-                if (gd0 + gcap < gd0) break;   /* overflow guard */
-            }
-        }
-        if (tid == 0) S.next_chunk = claim;
-        lds_barrier();
-        chunk = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S.next_chunk) |
-                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S.next_chunk >> 32)) << 32);
-    }
-    if (lane == 0 && tokens_w) atomicAdd(o->ntokens, tokens_w);
-}
-
-int launch_tok_twopass(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc, uint64_t nch,
-                       const VocabDev& v, const TokStream& t, uint64_t* caps, const K1Out* o_dev, Arena& ar,
-                       hipStream_t s) {
-    if (nch == 0) return 0;
-    if (v.mask >= (1ull << SLOT_BITS)) return -3;
-    static_assert(sizeof(TaShared) * TA_WG_PER_CU <= 163840, "LDS of TA_WG_PER_CU tokenize workgroups per CU");
-    static_assert(sizeof(SlShared) * WG_PER_CU <= 163840, "LDS of WG_PER_CU workgroups per CU");
-    const uint32_t sbits = (uint32_t)__builtin_popcountll(v.mask);
-    const uint32_t gcap = (1u << (31u - sbits)) >= (uint32_t)GCAP ? (uint32_t)GCAP : (1u << (31u - sbits));
-    k_chunk_tokcap<<<(unsigned)((nch + 255) / 256), 256, 0, s>>>(chunk_start, chunk_doc, nch, caps);
-    if (hipGetLastError() != hipSuccess) return -1;
-    const int rc = scan_excl_u64(caps, const_cast<uint64_t*>(t.chunk_tok), nch, ar, s);
-    if (rc) return rc;
-    static int ncu = 0;
-    if (!ncu) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-            ncu = 256;
-    }
-    const uint64_t wa = (uint64_t)ncu * TA_WG_PER_CU;
-    const uint64_t ga = (nch + A_NWAVE - 1) / A_NWAVE < wa ? (nch + A_NWAVE - 1) / A_NWAVE : wa;
-    k_tok_resolve<<<(unsigned)ga, A_NT, 0, s>>>(c, chunk_start, chunk_doc, nch, v, t, sbits, gcap);
-    if (hipGetLastError() != hipSuccess) return -1;
-    const uint64_t wb = (uint64_t)ncu * WG_PER_CU;
-    const uint64_t gb = nch < wb ? nch : wb;
-    k_tok_count<<<(unsigned)gb, NT, 0, s>>>(c.doc_off, chunk_start, chunk_doc, nch, t, o_dev, sbits, gcap);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -128,6 +128,112 @@ def test_group_long_terms(xchg, monkeypatch):
     assert all(i["nterms_global"] == ora["nterms"] for i in infos)
 
 
+_M64 = (1 << 64) - 1
+
+
+def _long_key16(t):
+    """dev_common.h make_long_key's 120-bit hash truncated to the 16 bits the test build
+    lib/libtfidf_hip_longtag16.so keeps"""
+    def mix64(z):
+        z ^= z >> 30
+        z = (z * 0xBF58476D1CE4E5B9) & _M64
+        z ^= z >> 27
+        z = (z * 0x94D049BB133111EB) & _M64
+        return z ^ (z >> 31)
+    n = len(t)
+    h1 = 0x243F6A8885A308D3 ^ n
+    h2 = (0x13198A2E03707344 + n * 0x9E3779B97F4A7C15) & _M64
+    for c in t:
+        h1 = ((h1 ^ c) * 0x100000001B3) & _M64
+        h2 = ((h2 + c + 1) * 0xC2B2AE3D27D4EB4F) & _M64
+        h2 ^= h2 >> 29
+    return mix64(h1 ^ ((h2 << 1) & _M64)) & 0xFFFF
+
+
+def _colliding_long_pair():
+    seen = {}
+    for i in range(100000):
+        t = b"crossrankcollision%05d" % i
+        k = _long_key16(t)
+        if k in seen:
+            return seen[k], t
+        seen[k] = t
+    raise AssertionError("no 16-bit collision found")
+
+
+def _long_pair_shards(a, b):
+    """two c2 shards, rank 0 with a document holding term a, rank 1 one holding term b"""
+    base = _shards("c2", 0.002, 2)
+    N = base[0][3] + 2
+    nid = int(max(int(s[2].max()) for s in base)) + 1
+    shards = []
+    for r, (d, o, ids, _) in enumerate(base):
+        x = np.frombuffer(b"w " + (a, b)[r] + b" z\n", dtype=np.uint8)
+        shards.append((np.concatenate([d, x]), np.concatenate([o, [o[-1] + len(x)]]).astype(np.uint64),
+                       np.concatenate([ids, [nid + r]]).astype(np.uint32), N))
+    return shards
+
+
+_CROSS_LONG_CHILD = r"""
+import sys
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2]); sys.path.insert(0, sys.argv[3])
+import numpy as np, tfidf_abi, test_gpu_multirank as t
+a, b = t._colliding_long_pair()
+# one rank holding both: the in-rank byte verification (dev_vocab.h) reports the pair
+# (this also pins the test's copy of the hash to the device's)
+with tfidf_abi.Engine(0) as e:
+    x = b"w " + a + b" z\nq " + b + b"\n"
+    try:
+        e.run_host(np.frombuffer(x, dtype=np.uint8), np.array([0, 5 + len(a), len(x)], dtype=np.uint64))
+        print("RESULT one merged")
+    except tfidf_abi.TfidfError as ex:
+        print("RESULT one rc=%d" % ex.rc)
+# one term on each rank: only the exchange meets them, and its check reports them
+for xchg in ("dense", "owner"):
+    import os
+    os.environ["TFIDF_XCHG"] = xchg
+    with tfidf_abi.Group(2, devices=[0, 0]) as g:
+        try:
+            g.run_host(t._long_pair_shards(a, b))
+            print("RESULT two %s merged" % xchg)
+        except tfidf_abi.TfidfError as ex:
+            print("RESULT two %s rc=%d" % (xchg, ex.rc))
+"""
+
+
+def test_cross_rank_long_term_collision_is_reported():
+    """Cross-rank identity of terms of >= 16 bytes is byte-exact (engine.cpp
+    exchange_long_check): the DF exchange meets long terms by their 120-bit hash keys, so every
+    key two ranks share is then compared byte by byte, as TFIDF.c:229's strcmp would.  The
+    test library truncates the keys to 16 bits: two distinct long terms with one 16-bit key,
+    one per rank, fail the run with TFIDF_E_CAPACITY on both exchange forms (never merged);
+    on one rank the in-rank verification reports the same pair."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    pydir = os.path.join(os.path.dirname(here), "parallel-systems-mpi-tfidf_amd", "python")
+    env = dict(os.environ, TFIDF_LIB="longtag16")
+    import sys
+    r = subprocess.run([sys.executable, "-c", _CROSS_LONG_CHILD, pydir, here, os.path.join(os.path.dirname(here), "oracle")],
+                       env=env, capture_output=True, text=True, timeout=240, cwd=here)
+    out = [l for l in r.stdout.splitlines() if l.startswith("RESULT")]
+    assert out == ["RESULT one rc=-9", "RESULT two dense rc=-9", "RESULT two owner rc=-9"], r.stdout + r.stderr[-3000:]
+    assert "on different ranks share their 120-bit identity key" in r.stderr
+
+
+@pytest.mark.parametrize("xchg", ["dense", "owner"])
+def test_cross_rank_distinct_long_terms_equal_oracle(xchg, monkeypatch):
+    """The same pair under the product library's full 120-bit keys: two distinct terms, the
+    check passes and the shards equal the single-rank oracle."""
+    monkeypatch.setenv("TFIDF_XCHG", xchg)
+    shards = _long_pair_shards(*_colliding_long_pair())
+    texts, res, infos = _run_group(shards, 2)
+    data = np.concatenate([shards[0][0], shards[1][0]])
+    off = np.concatenate([shards[0][1], shards[0][1][-1] + shards[1][1][1:]])
+    ids = np.concatenate([shards[0][2], shards[1][2]])
+    ora = oracle_py.run(data, off, ids, shards[0][3])
+    assert sorted(b"".join(texts).split(b"\n")) == sorted(ora["output_txt"].split(b"\n"))
+    assert all(i["nterms_global"] == ora["nterms"] for i in infos)
+
+
 def test_group_retry_is_collective(monkeypatch):
     """A 1024-slot starting vocabulary makes every rank grow its table and repeat the run;
     the repeats are agreed at the exchange (no rank re-enters the collectives alone)."""

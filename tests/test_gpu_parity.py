@@ -240,7 +240,7 @@ def test_k1_variants_agree(cfg, scale):
     p = tfidf_configs.plan(cfg, scale=scale)
     data, off = tfidf_abi.synth_host(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"])
     outs = []
-    modes = [("auto", 2), ("sl", 2), ("2p", 2), ("vs", 2), ("general", 0)]
+    modes = [("auto", 2), ("sl", 2), ("vs", 2), ("general", 0)]
     for mode, flag in modes:
         os.environ["TFIDF_K1"] = mode
         try:
@@ -248,10 +248,8 @@ def test_k1_variants_agree(cfg, scale):
                 e.run_host(data, off, p["doc_ids"], p["ndocs_total"])
                 f = e.info()["flags"]
                 assert (f & 3) == flag
-                if mode in ("auto", "sl", "2p") and cfg != "c4":
+                if mode in ("auto", "sl") and cfg != "c4":
                     assert f & tfidf_abi.RUN_K1_SL
-                if mode == "2p" and cfg != "c4":
-                    assert f & tfidf_abi.RUN_K1_2P
                 outs.append(e.fetch())
         finally:
             os.environ.pop("TFIDF_K1", None)
