@@ -199,7 +199,7 @@ typedef struct tfidf_run_info {
 #define TFIDF_RUN_K1_VS   2u  /* slot-keyed tokenize+count kernel (the default path; the general
                                  kernel of TFIDF_K1=general or an unaligned corpus leaves it clear) */
 #define TFIDF_RUN_K1_ST   4u  /* retired: round 3's k_tokcount_st (removed in round 5), never set */
-#define TFIDF_RUN_K1_SL   8u  /* ... run as k_tokcount_sl (the default, vocabulary table <= 4M slots);
+#define TFIDF_RUN_K1_SL   8u  /* ... run as k_tokcount_sl (the default, vocabulary table <= 32M slots);
                                  neither ST nor SL with VS set: k_tokcount_vs (larger tables) */
 #define TFIDF_RUN_XCHG_DENSE 16u  /* multi-rank: the DF exchange used the dense all-reduce form
                                      (else the hash-owner all-to-all; single rank: no exchange) */

@@ -113,7 +113,7 @@ struct tfidf_ctx {
     Xport* xp = nullptr;    /* peers of the DF exchange (RCCL or in-process); owned */
     int rank = 0, nranks = 1;
     int timing = 1;         /* tfidf_set_timing: 0 none, 1 every stage, 2 K1 and the whole run only */
-    int k1_mode = 0;        /* 0 auto (k_tokcount_sl up to K1_ST_MAX_CAP slots, k_tokcount_vs beyond),
+    int k1_mode = 0;        /* 0 auto (k_tokcount_sl up to K1_SL_MAX_CAP slots, k_tokcount_vs beyond),
                                1 round-1 kernel (TFIDF_K1=vs), 2 general K1 (TFIDF_K1=general),
                                3 k_tokcount_sl (TFIDF_K1=sl) — cross-checks and A/B timing;
                                round 3's k_tokcount_st was retired in round 5, round 6's two-pass form of
@@ -127,7 +127,7 @@ struct tfidf_ctx {
     DevBuf stamps;
     bool k1_vs = false;     /* last run used the slot-keyed kernel (default) */
     bool k1_sl = false;     /* ... or tokcount_sl (else tokcount_vs) */
-    uint64_t sl_maxcap = K1_ST_MAX_CAP;   /* env TFIDF_SL_MAXCAP: tokcount_sl up to this many vocabulary slots */
+    uint64_t sl_maxcap = K1_SL_MAX_CAP;   /* env TFIDF_SL_MAXCAP: tokcount_sl up to this many vocabulary slots */
     K1Out* k1out_host = nullptr;   /* pinned: tokcount_sl's output block, copied to k1out_dev per run */
     DevBuf k1out_dev;
     bool k1out_valid = false;      /* k1out_dev holds *k1out_host (the copy is skipped when a run's block is the same) */
@@ -962,16 +962,17 @@ static int run_local(tfidf_ctx* ctx, const CorpusDev& c, const uint32_t* dev_ids
     const uint64_t span = c.hi - c.lo;
     /* K1 variant: the slot-keyed kernels (tokcount_st / tokcount_vs) need a 16-byte aligned
      * corpus base; TFIDF_K1=general selects the general kernel (cross-checks).  The LDS-staged
-     * kernel is the low-cardinality one: with a vocabulary table past K1_ST_MAX_CAP slots
-     * (config 4: ~1e7 terms, nearly every token a new (doc, term) pair) its bucketed LDS count
-     * table runs full and the round-1 kernel is 2.3x faster (c4: 11.5 vs 26.2 ms) */
+     * kernel runs up to the largest table it addresses (2^25 slots): round 6's leaner rounds
+     * made it faster than the round-1 kernel on config 4 too (a 32M-slot table for ~1e7 terms,
+     * nearly every token a new (doc, term) pair: K1 4.67 vs 5.02 ms, c4 76.8 vs 75.0 GB/s,
+     * profiles/r06_k1_ab_c2.txt call r06l); beyond, k_tokcount_vs */
     const bool aligned = (((uintptr_t)c.bytes & 15u) == 0);
     ctx->k1_vs = aligned && ctx->k1_mode != 2;
     if (ctx->k1_vs && ctx->vcap > K1_VS_MAX_CAP) return TFIDF_E_CAPACITY;
     ctx->k1_sl = ctx->k1_vs && (ctx->k1_mode == 0 || ctx->k1_mode == 3) &&
                  ctx->vcap <= ctx->sl_maxcap;
-    /* tokcount_sl over a high-cardinality table (TFIDF_SL_MAXCAP): half-size chunks, as
-     * tokcount_vs, since nearly every token is a new pair for its LDS table */
+    /* tokcount_sl over a high-cardinality table (past K1_ST_MAX_CAP slots): half-size chunks,
+     * as tokcount_vs, since nearly every token is a new pair for its LDS table */
     const uint32_t cb = ctx->k1_sl ? (ctx->vcap > K1_ST_MAX_CAP ? CHUNK_BYTES : CHUNK_BYTES_ST) : CHUNK_BYTES;
     const uint64_t nchunks = span ? (span + cb - 1) / cb : 0;
     if (ctx->rec_cap == 0) ctx->rec_cap = span / 6 + 4096;

@@ -101,11 +101,12 @@ int launch_tokcount_vs(const CorpusDev& c, const uint64_t* chunk_start, const ui
                        uint64_t c1, const VocabDev& v, const K1Out& o, hipStream_t s);
 #define K1_VS_MAX_CAP (1ull << 28)
 
-#define K1_ST_MAX_CAP (1ull << 22)   /* tokcount_sl up to this vocabulary capacity, tokcount_vs beyond */
-#define K1_SL_MAX_CAP (1ull << 25)   /* the largest table tokcount_sl can address (TFIDF_SL_MAXCAP, A/B) */
+#define K1_ST_MAX_CAP (1ull << 22)   /* tokcount_sl past this vocabulary capacity: half-size chunks */
+#define K1_SL_MAX_CAP (1ull << 25)   /* the largest table tokcount_sl addresses (the default limit;
+                                        TFIDF_SL_MAXCAP lowers it), tokcount_vs beyond */
 /* K1 default (tokcount_sl.hip): one workgroup per chunk, straight-line rounds; the output
  * block is read from device memory (o_dev: a K1Out the engine copies there per run).
- * 16-byte aligned corpus base; -3 when the vocabulary exceeds K1_ST_MAX_CAP slots */
+ * 16-byte aligned corpus base; -3 when the vocabulary exceeds K1_SL_MAX_CAP slots */
 int launch_tokcount_sl(const CorpusDev& c, const uint64_t* chunk_start, const uint32_t* chunk_doc, uint64_t c0,
                        uint64_t c1, const VocabDev& v, const K1Out* o_dev, hipStream_t s);
 

@@ -573,9 +573,11 @@ __device__ __forceinline__ void lds_count(SlShared& S, const K1Out* o, uint32_t 
     const bool hit = key != 0u && found;
     const bool claim = key != 0u && !found && n < BW && !over;
     const uint32_t idx = bkt_slot(b, found ? j : (n & (BW - 1u)));
-    /* only a new key waits for an LDS round trip (its CAS); a match adds at once */
+    /* only a new key waits for an LDS round trip (its CAS); a match adds at once.  The slot
+     * holds the key after the CAS exactly when the CAS returned the key (a match, or a peer
+     * lane claimed it for the same key first) or returned 0 to a claim */
     const uint32_t old = atomicCAS(&S.TK[idx], hit ? key : (claim ? 0u : 0x7FFFFFFFu), key);
-    const bool ok = hit || (claim && (old == 0u || old == key));
+    const bool ok = key != 0u && (old == key || (claim && old == 0u));
     atomicAdd(&S.TC[idx], ok ? 1u : 0u);
     bool claimed = claim && old == 0u;
     bool slow = key != 0u && !ok;

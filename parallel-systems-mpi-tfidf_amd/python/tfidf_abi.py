@@ -22,7 +22,7 @@ TFIDF_CORPUS_DEVICE = 1
 UNIQUE_ID_BYTES = 128
 RUN_K1_VS = 2   # tfidf_run_info.flags (include/tfidf.h): slot-keyed K1 ...
 RUN_K1_ST = 4   # retired (round 3's k_tokcount_st, removed in round 5): never set
-RUN_K1_SL = 8   # ... run as k_tokcount_sl (the default up to 4M vocabulary slots; else k_tokcount_vs)
+RUN_K1_SL = 8   # ... run as k_tokcount_sl (the default up to 32M vocabulary slots; else k_tokcount_vs)
 RUN_XCHG_DENSE = 16  # multi-rank: the DF exchange used the dense all-reduce form
 ABI_VERSION = 2  # TFIDF_ABI_VERSION of include/tfidf.h this binding is written for
 
