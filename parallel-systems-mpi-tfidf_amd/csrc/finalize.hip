@@ -740,8 +740,10 @@ int launch_dense_emit(const uint32_t* dense, uint32_t nb, uint32_t V, const uint
 
 /* -------------------------------------------------------------------- DF -- */
 
-constexpr uint32_t DFH_RECS = 65535;      /* records per workgroup: u16 bins cannot overflow */
+constexpr uint32_t DFH_RECS = 65535;      /* records per workgroup up to which no u16 bin can wrap */
 constexpr uint32_t DFH_MAXV = 65536;
+constexpr uint32_t DFH_ROUNDS = 4;        /* workgroups per resident slot at most: beyond 4 x 65535 records
+                                             per slot a workgroup takes more than DFH_RECS (the wide form) */
 
 /* LDS-privatised DF histogram: 1024 threads (16 waves; at V = 65536 the 128 KB bin array allows one
  * workgroup per CU).  Each thread owns 64 records of the workgroup's range and keeps
@@ -761,13 +763,20 @@ constexpr int DFH_B = DFH_B_N;
 constexpr uint32_t DFH_CK = 1u << DFH_CK_BITS;   /* LDS slot -> rank cache entries (4096: 32 KB; with V = 65536 the
                                                     bins + cache fill the 160 KB of LDS exactly) */
 __device__ __forceinline__ uint32_t dfh_cslot(uint32_t slot) { return (slot * 0x9E3779B1u) >> (32 - DFH_CK_BITS); }
+/* WIDE: a workgroup takes more than DFH_RECS records (large corpora: c3's 2.9e9 records in
+ * 1024 workgroups instead of 44 K, so 100 MB of partial histograms are written and summed
+ * instead of 4.4 GB).  A u16 counter then moves 0x8000 into the global df whenever it
+ * reaches 0x8000: the one add that returned 0x7FFF does it, so every crossing is moved once
+ * and no counter passes 0x8000 + the adds in flight (< 0xFFFF): no field wraps or carries. */
+template <bool WIDE>
 __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ rec_slot, uint64_t nrec,
                                                         const uint32_t* __restrict__ nrec_extra,
                                                         const uint32_t* __restrict__ rank_of_slot,
                                                         const uint16_t* __restrict__ rank16, uint32_t V,
                                                         uint64_t slot_cap, uint64_t ranked_from,
-                                                        uint32_t* __restrict__ status, uint32_t per,
-                                                        uint32_t* __restrict__ part /* [grid][V/2 words] */) {
+                                                        uint32_t* __restrict__ status, uint64_t per,
+                                                        uint32_t* __restrict__ part /* [grid][V/2 words] */,
+                                                        uint32_t* __restrict__ df) {
     extern __shared__ __attribute__((aligned(16))) uint32_t bins[]; /* V/2 words of two u16 counters */
     const uint32_t W = (V + 1) / 2;
     for (uint32_t k = threadIdx.x; k < W; k += DFH_NT) bins[k] = 0;
@@ -823,7 +832,16 @@ __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ r
 #pragma unroll
         for (int q = 0; q < DFH_B; ++q) {
             if (sl[q] == 0xFFFFFFFFu) continue;
-            atomicAdd(&bins[r[q] >> 1], 1u << (16 * (r[q] & 1)));
+            const uint32_t sh = 16 * (r[q] & 1);
+            if (WIDE) {
+                const uint32_t old = atomicAdd(&bins[r[q] >> 1], 1u << sh);
+                if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {
+                    atomicSub(&bins[r[q] >> 1], 0x8000u << sh);
+                    atomicAdd(&df[r[q]], 0x8000u);
+                }
+            } else {
+                atomicAdd(&bins[r[q] >> 1], 1u << sh);
+            }
             /* records carry term ranks from here on: K5 reads them without a gather */
             if (i + (uint64_t)q * DFH_NT < ranked_from) __builtin_nontemporal_store(r[q], &rec_slot[i + (uint64_t)q * DFH_NT]);
         }
@@ -977,11 +995,13 @@ __global__ __launch_bounds__(DFS_NT) void k_dfs_slice(const uint32_t* __restrict
     for (uint32_t j = threadIdx.x; j < sw; j += DFS_NT) df[s0 + j] = accumulate ? df[s0 + j] + sbins[j] : sbins[j];
 }
 
-/* the LDS histogram's split of nrec_max records: records per workgroup (<= DFH_RECS) so
- * that the workgroups fill whole waves of the CUs' resident slots (c2: 946 x 65535 records
- * = 3.7 waves -> 1024 x 60548, no tail) */
-static void df_lds_plan(uint64_t nrec_max, uint32_t V, uint32_t* per_out, uint32_t* nparts_out) {
-    uint32_t nparts = (uint32_t)((nrec_max + DFH_RECS - 1) / DFH_RECS);
+/* the LDS histogram's split of nrec_max records: records per workgroup so that the
+ * workgroups fill whole waves of the CUs' resident slots (c2: 946 x 65535 records = 3.7
+ * waves -> 1024 x 60548, no tail), at most DFH_ROUNDS waves (c3: 1024 x 2.8 M records, the
+ * wide form).  TFIDF_DF_WGS=<n> fixes the number of workgroups (tests of the wide form on
+ * small inputs). */
+static void df_lds_plan(uint64_t nrec_max, uint32_t V, uint64_t* per_out, uint32_t* nparts_out) {
+    uint64_t nparts = (nrec_max + DFH_RECS - 1) / DFH_RECS;
     const uint32_t W = (V + 1) / 2;
     static int ncu = 0;
     if (!ncu) {
@@ -993,9 +1013,14 @@ static void df_lds_plan(uint64_t nrec_max, uint32_t V, uint32_t* per_out, uint32
     const uint64_t wg_lds = (uint64_t)((W + 1) & ~1u) * 4 + (uint64_t)DFH_CK * 8;
     const uint64_t per_cu = (uint64_t)163840 / wg_lds >= 2 ? 2 : 1;   /* 1024-thread workgroups */
     const uint64_t slots = (uint64_t)ncu * per_cu;
-    const uint64_t full = (nparts + slots - 1) / slots * slots;
-    uint32_t per = (uint32_t)((nrec_max + full - 1) / full);
-    if (per < 8192u) per = 8192u;   /* small inputs: few workgroups (each clears and writes W words) */
+    uint64_t full = (nparts + slots - 1) / slots * slots;
+    if (full > DFH_ROUNDS * slots) full = DFH_ROUNDS * slots;
+    const char* fe = getenv("TFIDF_DF_WGS");
+    const uint64_t forced = fe ? strtoull(fe, nullptr, 0) : 0ull;
+    if (forced >= 1 && forced <= (1u << 20)) full = forced;
+    uint64_t per = (nrec_max + full - 1) / full;
+    if (per < 8192u && !forced) per = 8192u;   /* small inputs: few workgroups (each clears and writes W words) */
+    if (per == 0) per = 1;
     *per_out = per;
     *nparts_out = (uint32_t)((nrec_max + per - 1) / per);
 }
@@ -1003,7 +1028,8 @@ static void df_lds_plan(uint64_t nrec_max, uint32_t V, uint32_t* per_out, uint32
 size_t df_hist_scratch(uint64_t nrec_max, uint32_t V) {
     if (V == 0 || nrec_max == 0) return 256;
     if (V <= DFH_MAXV) {
-        uint32_t per = 0, nparts = 0;
+        uint64_t per = 0;
+        uint32_t nparts = 0;
         df_lds_plan(nrec_max, V, &per, &nparts);
         return (size_t)nparts * ((V + 1) / 2) * 4 + 256;
     }
@@ -1024,7 +1050,8 @@ int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra
     if (nrec_max == 0)
         return accumulate ? 0 : hipMemsetAsync(df, 0, (size_t)V * 4, s) == hipSuccess ? 0 : -1;
     if (V <= DFH_MAXV) {
-        uint32_t per = 0, nparts = 0;
+        uint64_t per = 0;
+        uint32_t nparts = 0;
         df_lds_plan(nrec_max, V, &per, &nparts);
         const uint32_t W = (V + 1) / 2;
         size_t m = ar.mark();
@@ -1032,8 +1059,12 @@ int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra
         if (!part) return -2;
         if (!accumulate && hipMemsetAsync(df, 0, (size_t)V * 4, s) != hipSuccess) return -1;
         const size_t lds = (size_t)((W + 1) & ~1u) * 4 + (size_t)DFH_CK * 8;
-        k_df_hist_lds<<<nparts, DFH_NT, lds, s>>>(rec_slot, nrec, nrec_extra, rank_of_slot, rank16, V, slot_cap,
-                                                             ranked_from, status, per, part);
+        if (per > DFH_RECS)
+            k_df_hist_lds<true><<<nparts, DFH_NT, lds, s>>>(rec_slot, nrec, nrec_extra, rank_of_slot, rank16, V,
+                                                            slot_cap, ranked_from, status, per, part, df);
+        else
+            k_df_hist_lds<false><<<nparts, DFH_NT, lds, s>>>(rec_slot, nrec, nrec_extra, rank_of_slot, rank16, V,
+                                                             slot_cap, ranked_from, status, per, part, df);
         k_df_colsum<<<dim3(grid_for(V), (nparts + DFC_G - 1) / DFC_G), NT, 0, s>>>(part, nparts, V, df);
         ar.release(m);
         return ok();

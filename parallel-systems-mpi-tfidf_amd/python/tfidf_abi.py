@@ -6,6 +6,7 @@ no Python or CPU fallback for any stage.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
 
@@ -327,6 +328,30 @@ class Engine:
         out = np.zeros(v.size * 32, dtype=np.uint8)
         _chk(lib().tfidf_format_f64(self.h, v.ctypes.data, v.size, out.ctypes.data), "tfidf_format_f64")
         return [bytes(out[i * 32:(i + 1) * 32]).rstrip(b"\0") for i in range(v.size)]
+
+    @contextlib.contextmanager
+    def fetched(self):
+        """The last run's result as numpy views of the library's host arrays (tfidf_fetch
+        without copies and without the text; valid inside the with block): for full-size
+        runs whose pairs do not fit twice in host memory."""
+        r = Result()
+        _chk(lib().tfidf_fetch(self.h, C.byref(r)), "tfidf_fetch")
+        try:
+            P, N, V = int(r.npairs), int(r.ndocs), int(r.nterms)
+
+            def view(p, n):
+                return np.ctypeslib.as_array(p, shape=(n,)) if n else np.zeros(0, dtype=np.uint8)
+
+            yield {
+                "npairs": P, "ndocs": N, "nterms": V, "ndocs_total": int(r.ndocs_total),
+                "doc": view(r.pair_doc, P), "term": view(r.pair_term, P), "count": view(r.pair_count, P),
+                "docsize": view(r.pair_docsize, P), "df": view(r.pair_df, P), "score": view(r.pair_score, P),
+                "doc_id": view(r.doc_id, N), "doc_size": view(r.doc_size, N), "term_df": view(r.term_df, V),
+                "term_off": view(r.term_off, V + 1),
+                "term_bytes": view(r.term_bytes, int(r.term_off[V]) if V else 0),
+            }
+        finally:
+            lib().tfidf_result_free(C.byref(r))
 
     def fetch(self) -> dict:
         r = Result()

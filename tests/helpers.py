@@ -91,3 +91,81 @@ def assert_same_result(gpu: dict, ora: dict, exact_scores: bool = True):
         np.testing.assert_array_equal(gpu["score"].view(np.uint64), ora["score"].view(np.uint64))
     else:
         np.testing.assert_allclose(gpu["score"], ora["score"], rtol=1e-12, atol=0)
+
+
+def _chunk_bounds(doc: np.ndarray, chunk: int):
+    """pair ranges of about `chunk` pairs, each starting at a document's first pair"""
+    P = len(doc)
+    b = [0]
+    for t in range(chunk, P, chunk):
+        if t <= b[-1]:
+            continue
+        j, w = t, 1 << 16
+        while j < P:
+            seg = doc[j - 1:j + w]
+            ch = np.flatnonzero(seg[1:] != seg[:-1])
+            if len(ch):
+                j += int(ch[0])
+                break
+            j += w
+        if j < P:
+            b.append(j)
+    b.append(P)
+    return b
+
+
+def check_full_properties(r: dict, ntokens: int, threads: int = 8, chunk: int = 1 << 26):
+    """Size-independent properties of a result (the views of Engine.fetched(), any size),
+    checked in document-aligned chunks on a thread pool so that full-size configurations
+    need no copy of the pairs:
+      counts sum to the tokens; per document (a contiguous run of pairs): sum of counts =
+      docSize (TFIDF.c:141-167), docSize as the run's documents report it; terms strictly
+      increasing inside a document and documents strictly increasing in "docN@" strcmp
+      order, each document one run (TFIDF.c:245,273); DF = pairs per term (TFIDF.c:169-234);
+      score = count/docSize * log(N/df) within 1e-12 relative (TFIDF.c:202,243-244)."""
+    from concurrent.futures import ThreadPoolExecutor
+    import tfidf_configs
+    P, V, N = r["npairs"], r["nterms"], r["ndocs_total"]
+    doc, term, cnt, dsz, df, score, tdf = (r[k] for k in ("doc", "term", "count", "docsize", "df", "score", "term_df"))
+    assert P > 0 and len(doc) == P
+    bounds = _chunk_bounds(doc, chunk)
+
+    def one(i):
+        a, b = bounds[i], bounds[i + 1]
+        d, t, c = doc[a:b], term[a:b], cnt[a:b].astype(np.int64)
+        st = np.flatnonzero(np.r_[True, d[1:] != d[:-1]])
+        assert np.array_equal(np.add.reduceat(c, st), dsz[a:b][st].astype(np.int64)), "per-document sums"
+        same = d[1:] == d[:-1]
+        assert np.all(~same | (t[1:] > t[:-1])), "term order inside a document"
+        assert np.all(~same | (dsz[a + 1:b] == dsz[a:b - 1])), "docSize constant inside a document"
+        assert np.array_equal(df[a:b], tdf[t]), "df = the term's df"
+        ds = dsz[a:b].astype(np.float64)
+        ref = (c / ds) * np.log(N / df[a:b].astype(np.float64))
+        err = np.abs(score[a:b] - ref)
+        assert np.all(err <= 1e-12 * np.abs(ref) + 1e-300), "scores"
+        return int(c.sum()), np.bincount(t, minlength=V), d[st].copy(), dsz[a:b][st].copy()
+
+    with ThreadPoolExecutor(threads) as ex:
+        parts = list(ex.map(one, range(len(bounds) - 1)))
+    assert sum(p[0] for p in parts) == ntokens
+    dfc = np.zeros(V, dtype=np.int64)
+    for p in parts:
+        dfc += p[1]
+    assert np.array_equal(dfc, tdf.astype(np.int64)), "DF = pairs per term"
+    runs = np.concatenate([p[2] for p in parts])
+    run_ds = np.concatenate([p[3] for p in parts])
+    key = tfidf_configs.doc_name_key(runs)
+    assert np.all(key[1:] > key[:-1]), "documents strictly increasing, one run each"
+    # the run's docSize is the document's (tfidf_result doc_id/doc_size); empty documents have no run
+    ids, sizes = r["doc_id"], r["doc_size"]
+    o = np.argsort(ids, kind="stable")
+    pos = np.searchsorted(ids[o], runs)
+    assert np.array_equal(ids[o][pos], runs) and np.array_equal(sizes[o][pos], run_ds)
+    assert int(sizes.astype(np.int64).sum()) == ntokens
+    # term table in strcmp("word\t") order
+    toff, tb = r["term_off"], r["term_bytes"]
+    step = max(1, V // 200_000)
+    for i in range(0, V - 1, step):
+        x = bytes(tb[int(toff[i]):int(toff[i + 1])]) + b"\t"
+        y = bytes(tb[int(toff[i + 1]):int(toff[i + 2])]) + b"\t"
+        assert x < y, (i, x, y)

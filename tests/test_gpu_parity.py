@@ -15,7 +15,7 @@ import oracle_py
 import tfidf_abi
 import tfidf_configs
 from conftest import golden_cases, GOLDEN
-from helpers import assert_same_result, docs_to_arrays, jobs_from_result, load_golden
+from helpers import assert_same_result, check_full_properties, docs_to_arrays, jobs_from_result, load_golden
 
 pytestmark = pytest.mark.gpu
 
@@ -191,45 +191,25 @@ def test_cli_error_contract():
             assert p.returncode == 0 and p.stdout == b"Error Opening File: output.txt\n", (p.stdout, p.stderr)
 
 
-@pytest.mark.parametrize("cfg", ["c2", "c4", "c5"])
+@pytest.mark.parametrize("cfg", ["c2", "c4", "c5", "c3"])
 def test_full_config_properties(cfg):
-    """BASELINE configs at full size, device-generated: c2 (1e5 docs, ~1 GB), c4 (V = 1e7:
-    ~1e7 distinct terms, vocabulary-table growth, radix-sorted vocabulary), c5 (four 100 MB
-    documents among 1e6 ~600 B ones).  Size-independent properties — sum of counts =
-    tokens, per-document sums = docSize, DF = pairs per term, strict output order, scores
-    recomputed (<= 1e-12 relative)."""
+    """BASELINE configs at full size on one GPU, device-generated: c2 (1e5 docs, ~1 GB), c4
+    (V = 1e7: ~1e7 distinct terms, vocabulary-table growth, radix-sorted vocabulary), c5
+    (four 100 MB documents among 1e6 ~600 B ones), c3 (1e7 documents, ~40 GB, ~2.9e9 pairs:
+    the whole 8-GPU workload on one GPU).  Size-independent properties
+    (helpers.check_full_properties) — sum of counts = tokens, per-document sums = docSize,
+    DF = pairs per term, strict output order, scores recomputed (<= 1e-12 relative) — on
+    views of the fetched arrays, in chunks."""
     p = tfidf_configs.plan(cfg)
     with tfidf_abi.Engine(0) as e:
         c = e.synth_device(p["seed"], p["V"], p["mode"], p["cdf"], p["doc_ids"], p["ntok"], p["ndocs_total"])
         e.run_corpus(c)
         info = e.info()
-        r = e.fetch()
-    assert info["ntokens"] == int(p["ntok"].sum())
-    P = r["npairs"]
-    assert P == info["npairs"] and P > 1_000_000
-    cnt = r["count"].astype(np.int64)
-    assert cnt.sum() == info["ntokens"]
-    # per document: sum of counts == docSize (docs are contiguous runs in the output)
-    starts = np.flatnonzero(np.r_[True, r["doc"][1:] != r["doc"][:-1]])
-    sums = np.add.reduceat(cnt, starts)
-    assert np.array_equal(sums, r["docsize"][starts].astype(np.int64))
-    ds = dict(zip(r["doc_id"].tolist(), r["doc_size"].tolist()))
-    assert sum(ds.values()) == info["ntokens"]
-    # DF == number of pairs per term
-    dfc = np.bincount(r["term"], minlength=r["nterms"])
-    assert np.array_equal(dfc, r["term_df"])
-    assert np.array_equal(r["df"], r["term_df"][r["term"]])
-    # strict strcmp order: (doc key, term rank) increasing
-    dk = tfidf_configs.doc_name_key(r["doc"]).astype(np.uint64)
-    key = (dk.astype(object) * 0)  # placeholder to keep numpy from overflowing below
-    del key
-    assert np.all((dk[1:] > dk[:-1]) | ((dk[1:] == dk[:-1]) & (r["term"][1:] > r["term"][:-1])))
-    terms = r["terms"]
-    assert all((terms[i] + b"\t") < (terms[i + 1] + b"\t") for i in range(0, len(terms) - 1, 97))
-    # scores
-    N = r["ndocs_total"]
-    ref = (cnt / r["docsize"].astype(np.float64)) * np.log(N / r["df"].astype(np.float64))
-    np.testing.assert_allclose(r["score"], ref, rtol=1e-12, atol=1e-300)
+        assert info["ntokens"] == int(p["ntok"].sum())
+        with e.fetched() as r:
+            assert r["npairs"] == info["npairs"] and r["npairs"] > 1_000_000
+            assert r["ndocs"] == len(p["ntok"]) and r["ndocs_total"] == (p["ndocs_total"] or len(p["ntok"]))
+            check_full_properties(r, info["ntokens"])
 
 
 @pytest.mark.parametrize("cfg,scale", [("c2", 0.002), ("c5", 0.0005), ("c4", 0.001)])
@@ -463,20 +443,52 @@ def test_many_long_terms_sharing_prefixes(engine):
     check_vs_oracle(engine, *docs_to_arrays(docs))
 
 
-def test_df_histogram_bin_overflow(engine):
+@pytest.mark.parametrize("wgs", [None, "16"])
+def test_df_histogram_bin_overflow(wgs, monkeypatch):
     """17 M one-word documents: every record is the same term, the case where a u16 LDS bin
-    of the DF histogram would wrap if a workgroup took more than 65535 records (k_df_hist_lds
-    caps its share there; a one-workgroup-per-CU split with wrap correction measured slower);
-    df is N for every pair, each score log(N/N) = 0 (TFIDF.c:243-244)."""
+    of the DF histogram would wrap.  Default split: 65535 records or fewer per workgroup.
+    TFIDF_DF_WGS=16: 1.06 M records per workgroup, the wide form (k_df_hist_lds<true>, the
+    one c3 runs), whose counter moves 0x8000 to the global df at each crossing — 32 per
+    workgroup here, all on one LDS word.  df is N for every pair, each score log(N/N) = 0
+    (TFIDF.c:243-244)."""
+    if wgs:
+        monkeypatch.setenv("TFIDF_DF_WGS", wgs)
     N = 17_000_000
     data = np.frombuffer(b"a\n" * N, dtype=np.uint8).copy()
     off = (np.arange(N + 1, dtype=np.uint64) * 2)
-    engine.run_host(data, off)
-    info = engine.info()
-    assert info["npairs"] == N and info["nterms"] == 1
-    r = engine.fetch()
-    assert np.all(r["df"] == N) and np.all(r["count"] == 1) and np.all(r["docsize"] == 1)
-    assert np.all(r["score"] == 0.0)
+    with tfidf_abi.Engine(0) as engine:
+        engine.run_host(data, off)
+        info = engine.info()
+        assert info["npairs"] == N and info["nterms"] == 1
+        with engine.fetched() as r:
+            assert np.all(r["df"] == N) and np.all(r["count"] == 1) and np.all(r["docsize"] == 1)
+            assert np.all(r["score"] == 0.0)
+
+
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_df_wide_form_vs_oracle(split, monkeypatch):
+    """The wide DF form (TFIDF_DF_WGS=3: ~100 K records per workgroup) against the oracle on
+    300 K short documents over a 40-term Zipf-like vocabulary plus rare terms — the frequent
+    terms' u16 counters cross 0x8000 in every workgroup, the rare ones never — with the DF
+    pass split beside the merge and not (TFIDF_DF_SPLIT)."""
+    monkeypatch.setenv("TFIDF_DF_WGS", "3")
+    monkeypatch.setenv("TFIDF_DF_SPLIT", split)
+    rng = np.random.default_rng(5)
+    vocab = np.array([b"f%02d" % i for i in range(40)] + [b"rare%05d" % i for i in range(20000)], dtype=object)
+    p = np.r_[1.0 / np.arange(1, 41), np.full(20000, 0.0005)]
+    n = 300_000
+    lens = rng.integers(1, 6, size=n)
+    toks = vocab[rng.choice(len(vocab), size=int(lens.sum()), p=p / p.sum())]
+    cut = np.r_[0, np.cumsum(lens)]
+    docs = [b" ".join(toks[cut[i]:cut[i + 1]]) for i in range(n)]
+    data, off = docs_to_arrays(docs)
+    ora = oracle_py.run(data, off)
+    with tfidf_abi.Engine(0) as e:
+        e.run_host(data, off)
+        assert e.info()["npairs"] > 3 * 65535
+        res = e.fetch()
+    assert_same_result(res, ora)
+    assert res["output_txt"] == ora["output_txt"]
 
 
 def _doc_with_terms(rng, n, vocab):

@@ -9,11 +9,12 @@ import subprocess
 import tempfile
 import shutil
 
+import numpy as np
 import pytest
 
 import oracle_py
 from conftest import golden_cases, GOLDEN
-from helpers import load_golden, sorted_lines
+from helpers import check_full_properties, load_golden, sorted_lines
 
 
 @pytest.mark.parametrize("case", golden_cases())
@@ -73,3 +74,62 @@ def test_sharded_cpu_baseline_equals_oracle():
         first = tfidf_configs.shard_cuts(sizes, k)
         txt, npairs = oracle_py.run_sharded(data, off, p["doc_ids"], p["ndocs_total"], order, first)
         assert txt == ref and npairs == ref.count(b"\n")
+
+
+def _as_views(r: dict, doc_off, ids) -> dict:
+    """the oracle's result in the layout of tfidf_abi.Engine.fetched()"""
+    V = r["nterms"]
+    order = sorted(range(V), key=lambda i: r["terms"][i] + b"\t")   # term ids in strcmp("word\t") order
+    rank = np.zeros(V, dtype=np.uint32)
+    rank[order] = np.arange(V, dtype=np.uint32)
+    terms = [r["terms"][i] for i in order]
+    pool = b"".join(terms)
+    toff = np.zeros(V + 1, dtype=np.uint64)
+    toff[1:] = np.cumsum([len(t) for t in terms])
+    term = rank[r["term"]]
+    sizes = np.zeros(len(ids), dtype=np.uint32)
+    first = {}
+    for i, d in enumerate(r["doc"].tolist()):
+        first.setdefault(d, i)
+    for k, d in enumerate(ids.tolist()):
+        sizes[k] = r["docsize"][first[d]] if d in first else 0
+    return dict(npairs=r["npairs"], nterms=V, ndocs=len(ids), ndocs_total=len(ids), doc=r["doc"], term=term,
+                count=r["count"], docsize=r["docsize"], df=r["df"], score=r["score"], doc_id=ids, doc_size=sizes,
+                term_df=np.bincount(term, minlength=V).astype(np.uint32), term_off=toff,
+                term_bytes=np.frombuffer(pool, dtype=np.uint8))
+
+
+def test_full_size_checker_on_oracle():
+    """helpers.check_full_properties — the checker the full-size GPU tests (c2..c5 at
+    BASELINE size) rely on — accepts the oracle's result at chunk sizes that split it into
+    many document-aligned chunks, and rejects a changed count, a changed score and two
+    documents out of order."""
+    rng = np.random.default_rng(7)
+    words = [b"w%d" % i for i in range(300)] + [b"x" * 20 + b"%d" % i for i in range(5)]
+    docs = [b" ".join(words[j] for j in rng.integers(0, len(words), int(rng.integers(0, 60)))) for _ in range(120)]
+    data = np.frombuffer(b"".join(docs), dtype=np.uint8)
+    off = np.zeros(len(docs) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(d) for d in docs])
+    ids = np.arange(1, len(docs) + 1, dtype=np.uint32)
+    r = oracle_py.run(data, off)
+    ntok = sum(len(d.split()) for d in docs)
+    for chunk in (1, 37, 1 << 20):
+        check_full_properties(_as_views(r, off, ids), ntok, threads=3, chunk=chunk)
+    bad = _as_views(r, off, ids)
+    bad["count"] = bad["count"].copy()
+    bad["count"][5] += 1
+    with pytest.raises(AssertionError):
+        check_full_properties(bad, ntok, chunk=37)
+    bad = _as_views(r, off, ids)
+    bad["score"] = bad["score"].copy()
+    bad["score"][11] *= 1 + 1e-9
+    with pytest.raises(AssertionError):
+        check_full_properties(bad, ntok, chunk=37)
+    v = _as_views(r, off, ids)
+    st = np.flatnonzero(np.r_[True, v["doc"][1:] != v["doc"][:-1]])
+    a, b, c = int(st[3]), int(st[4]), int(st[5])   # swap documents 3 and 4 (whole runs)
+    perm = np.r_[np.arange(a), np.arange(b, c), np.arange(a, b), np.arange(c, v["npairs"])]
+    for k in ("doc", "term", "count", "docsize", "df", "score"):
+        v[k] = v[k][perm]
+    with pytest.raises(AssertionError):
+        check_full_properties(v, ntok, chunk=37)
