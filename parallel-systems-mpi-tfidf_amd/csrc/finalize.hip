@@ -790,13 +790,44 @@ __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ r
     if (nrec_extra) nrec += *nrec_extra; /* merged partial records, counted on the device */
     const uint64_t r0 = (uint64_t)blockIdx.x * per;
     const uint64_t r1 = r0 + per < nrec ? r0 + per : nrec;
-    for (uint64_t i = r0 + threadIdx.x; i < r1; i += (uint64_t)DFH_B * DFH_NT) {
+    /* The ranks go back into the records one iteration late, after the next iteration's
+     * loads, and every load and store is unconditional (buffer instructions: a record past
+     * the range reads as 0 and is replaced, a store with an offset past the range is
+     * dropped by the hardware), so the compiler can count them: the first use of a loaded
+     * record waits for the loads only (in-order vmcnt), not for the stores behind them.
+     * With stores in branches it waited for everything, and with the stores at the end of
+     * the iteration the next loads waited for the stores (their data registers) — a third
+     * memory round trip per iteration. */
+    const uint32_t nr = r1 > r0 ? (uint32_t)(r1 - r0) : 0u;   /* this workgroup's records, relative */
+    /* records from rk on hold ranks already (the merged ones) */
+    const uint32_t rk = ranked_from <= r0 ? 0u : ranked_from - r0 >= nr ? nr : (uint32_t)(ranked_from - r0);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(rec_slot + r0), 0, (int)(nr * 4u),
+                                                                        0x00020000);
+    /* the slot -> rank maps through buffer loads too: 32-bit offsets, no 64-bit addresses */
+    const __amdgpu_buffer_rsrc_t ms = __builtin_amdgcn_make_buffer_rsrc(
+        rank16 ? (void*)rank16 : (void*)rank_of_slot, 0,
+        (int)(slot_cap * (rank16 ? 2u : 4u) < 0x7FFFFFF0ull ? slot_cap * (rank16 ? 2u : 4u) : 0x7FFFFFF0ull), 0x00020000);
+    uint32_t rp[DFH_B];   /* the previous iteration's ranks to store */
+    uint32_t pofs = 0xFFFFFFF0u;   /* their first byte offset (past the range: none) */
+    uint32_t pvalid = 0;           /* bit q: record q of the previous iteration is stored */
+#pragma unroll
+    for (int q = 0; q < DFH_B; ++q) rp[q] = 0u;
+    auto store_prev = [&]() {
+#pragma unroll
+        for (int q = 0; q < DFH_B; ++q)
+            __builtin_amdgcn_raw_buffer_store_b32(rp[q], rs,
+                                                  ((pvalid >> q) & 1u) ? pofs + (uint32_t)q * DFH_NT * 4u : 0xFFFFFFF0u,
+                                                  0, 2 /* nt */);
+    };
+    for (uint32_t j = threadIdx.x; j < nr; j += (uint32_t)DFH_B * DFH_NT) {
         uint32_t sl[DFH_B], r[DFH_B], g[DFH_B];
+        const uint32_t ofs = j * 4u;
 #pragma unroll
         for (int q = 0; q < DFH_B; ++q) {
-            const uint64_t k = i + (uint64_t)q * DFH_NT;
-            sl[q] = k < r1 ? __builtin_nontemporal_load(&rec_slot[k]) : 0xFFFFFFFFu;
+            const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rs, ofs + (uint32_t)q * DFH_NT * 4u, 0, 2 /* nt */);
+            sl[q] = j + (uint32_t)q * DFH_NT < nr ? v : 0xFFFFFFFFu;
         }
+        store_prev();
         /* classify without branches around loads: every lane reads its cache entry; a
          * miss's rank gather is one unconditional load per record (lanes that need none
          * read entry 0), all DFH_B of them in flight before the first is used (a gather
@@ -804,7 +835,7 @@ __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ r
         uint32_t miss = 0;   /* bit q: record q's rank comes from global memory */
 #pragma unroll
         for (int q = 0; q < DFH_B; ++q) {
-            const bool ranked = i + (uint64_t)q * DFH_NT >= ranked_from;   /* merged records hold ranks */
+            const bool ranked = j + (uint32_t)q * DFH_NT >= rk;   /* merged records hold ranks */
             if (sl[q] != 0xFFFFFFFFu && sl[q] >= (ranked ? (uint64_t)V : slot_cap)) {
                 atomicOr(status, ST_BOUNDS);
                 sl[q] = 0xFFFFFFFFu;
@@ -817,10 +848,12 @@ __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ r
         }
         if (rank16) {
 #pragma unroll
-            for (int q = 0; q < DFH_B; ++q) g[q] = rank16[((miss >> q) & 1u) ? sl[q] : 0u];
+            for (int q = 0; q < DFH_B; ++q)
+                g[q] = __builtin_amdgcn_raw_buffer_load_b16(ms, ((miss >> q) & 1u) ? sl[q] * 2u : 0u, 0, 0);
         } else {
 #pragma unroll
-            for (int q = 0; q < DFH_B; ++q) g[q] = rank_of_slot[((miss >> q) & 1u) ? sl[q] : 0u];
+            for (int q = 0; q < DFH_B; ++q)
+                g[q] = __builtin_amdgcn_raw_buffer_load_b32(ms, ((miss >> q) & 1u) ? sl[q] * 4u : 0u, 0, 0);
         }
 #pragma unroll
         for (int q = 0; q < DFH_B; ++q) {
@@ -829,8 +862,12 @@ __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ r
                 cache[dfh_cslot(sl[q])] = ((unsigned long long)(sl[q] + 1u) << 32) | r[q];
             }
         }
+        pvalid = 0;
 #pragma unroll
         for (int q = 0; q < DFH_B; ++q) {
+            /* records carry term ranks from here on: K5 reads them without a gather */
+            rp[q] = r[q];
+            pvalid |= sl[q] != 0xFFFFFFFFu && j + (uint32_t)q * DFH_NT < rk ? 1u << q : 0u;
             if (sl[q] == 0xFFFFFFFFu) continue;
             const uint32_t sh = 16 * (r[q] & 1);
             if (WIDE) {
@@ -842,10 +879,10 @@ __global__ __launch_bounds__(DFH_NT) void k_df_hist_lds(uint32_t* __restrict__ r
             } else {
                 atomicAdd(&bins[r[q] >> 1], 1u << sh);
             }
-            /* records carry term ranks from here on: K5 reads them without a gather */
-            if (i + (uint64_t)q * DFH_NT < ranked_from) __builtin_nontemporal_store(r[q], &rec_slot[i + (uint64_t)q * DFH_NT]);
         }
+        pofs = ofs;
     }
+    store_prev();
     __syncthreads();
     uint32_t* out = part + (uint64_t)blockIdx.x * W;
     for (uint32_t k = threadIdx.x; k < W; k += DFH_NT) out[k] = bins[k];
@@ -1020,6 +1057,7 @@ static void df_lds_plan(uint64_t nrec_max, uint32_t V, uint64_t* per_out, uint32
     if (forced >= 1 && forced <= (1u << 20)) full = forced;
     uint64_t per = (nrec_max + full - 1) / full;
     if (per < 8192u && !forced) per = 8192u;   /* small inputs: few workgroups (each clears and writes W words) */
+    if (per > (1u << 28)) per = 1u << 28;       /* a workgroup's records: 32-bit byte offsets */
     if (per == 0) per = 1;
     *per_out = per;
     *nparts_out = (uint32_t)((nrec_max + per - 1) / per);
