@@ -1558,8 +1558,10 @@ static int run_post(tfidf_ctx* ctx, uint64_t Nt) {
     a.idf_idx = full_lut ? nullptr : ctx->present.as<uint32_t>();   /* null: idf indexed by df */
     a.idf = ctx->idf_vals.as<double>();
     a.idf_rank = ctx->idf_rank.as<double>();
-    /* large V: 4-byte df gathers + the small idf-by-df table instead of 8-byte idf gathers */
-    a.idf_by_df = (full_lut && V >= (1u << 21)) ? 1u : 0u;
+    /* large V: 4-byte df gathers + the small idf-by-df table instead of 8-byte idf gathers;
+     * only with ranks over 21 bits (the score kernels' wide instance: k5_radix and the
+     * common instance read idf by rank) */
+    a.idf_by_df = (full_lut && V > (1u << 21)) ? 1u : 0u;
     a.large_list = ctx->large_list.as<uint32_t>() + 1;
     a.large_count = ctx->large_list.as<uint32_t>();
     a.cls_nblk = (N + 255) / 256;

@@ -1217,8 +1217,9 @@ constexpr int K5_BATCH = 8;           /* gathers per lane in flight together */
 #define K5_EB 4                       /* wide path: idf gathers per lane in flight together */
 #endif
 #ifndef K5_EMIT
-#define K5_EMIT 8                     /* bucket path's emission: positions per lane whose idf are gathered
-                                         before any of their stores */
+#define K5_EMIT 2                     /* bucket path's emission: positions per lane whose idf are gathered
+                                         before any of their stores (8: 15 VGPRs spilled, slower;
+                                         profiles/r06_k1_ab_c2.txt call r06q) */
 #endif
 #ifndef K5_WPS
 #define K5_WPS 4                      /* waves per SIMD the wave kernel is compiled for */
@@ -1241,20 +1242,26 @@ __global__ void k_idf_of_rank(const uint32_t* __restrict__ df_of_rank, const uin
     if (r < V) out[r] = idf_idx ? idf[idf_idx[df_of_rank[r]]] : idf[df_of_rank[r]];   /* null: table over all df */
 }
 
-/* idf of term rank r: the per-rank table, or (idf_by_df) the idf table over df values
- * indexed by the term's df */
+/* idf of term rank r: the per-rank table, or (BYDF: a.idf_by_df) the idf table over df
+ * values indexed by the term's df.  A compile-time choice (every score kernel is
+ * instantiated for both): as a run-time branch, the join after it made the compiler wait
+ * with vmcnt(0) before every idf gather of the by-rank case (the other branch's df load
+ * might still be in flight), so a batch's gathers ran one after another and each also
+ * waited for every store before it. */
+template <bool BYDF>
 __device__ __forceinline__ double k5_idf(const K5Args& a, uint32_t r) {
-    if (a.idf_by_df) return G(a.idf)[G(a.df_of_rank)[r]];
-    return G(a.idf_rank)[r];
+    if constexpr (BYDF) return G(a.idf)[G(a.df_of_rank)[r]];
+    else return G(a.idf_rank)[r];
 }
 
 /* The output is 16 bytes per pair (term rank, count, score): the document, docSize and
  * df of a pair are per-document / per-term values the fetch expands on the host. */
+template <bool BYDF>
 __device__ __forceinline__ void k5_emit(const K5Args& a, uint64_t o, double ds, uint32_t rank, uint32_t cnt) {
     const double tf = (double)cnt / ds;   /* TFIDF.c:202 */
     sto(&a.out_term[o], (uint32_t)(rank));
     sto(&a.out_cnt[o], (uint32_t)(cnt));
-    sto(&a.out_score[o], (double)(tf * k5_idf(a, rank))); /* TFIDF.c:243-244 (idf from the host-libm LUT) */
+    sto(&a.out_score[o], (double)(tf * k5_idf<BYDF>(a, rank))); /* TFIDF.c:243-244 (idf from the host-libm LUT) */
 }
 
 /* records hold term ranks once the DF pass has run (k_df_hist_* rewrite them in place) */
@@ -1390,8 +1397,9 @@ __device__ __forceinline__ uint32_t lane_id_fresh() {
 
 /* WIDE: the instance launched when ranks exceed 32 - K5_IDX_BITS bits (its extra path
  * costs registers the common instance must not pay: c2 score 0.88 -> 1.16 ms with it) */
-template <bool WIDE>
+template <bool WIDE, bool BYDF>
 __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(K5Args a) {
+    static_assert(WIDE || !BYDF, "idf by df only with wide ranks (V > 2^21; k5_radix reads idf by rank)");
     __shared__ __attribute__((aligned(16))) uint32_t kb[NT / 64][2][K5_WAVE];
     __shared__ uint32_t hist[NT / 64][K5_NB];
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1477,7 +1485,7 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
 #pragma unroll
             for (int q = 0; q < K5_RQ; ++q) {
                 const uint32_t j = 64u * q + lane;
-                if (j < n) k5_emit(a, ob + j, ds, r[q], buf0[j]);
+                if (j < n) k5_emit<BYDF>(a, ob + j, ds, r[q], buf0[j]);
             }
             continue;
         }
@@ -1512,7 +1520,7 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
             }
             double idf[QC];
 #pragma unroll
-            for (int q = 0; q < QC; ++q) idf[q] = (64u * q + lane < n) ? k5_idf(a, r[q]) : 0.0;
+            for (int q = 0; q < QC; ++q) idf[q] = (64u * q + lane < n) ? k5_idf<BYDF>(a, r[q]) : 0.0;
 #pragma unroll
             for (int q = 0; q < QC; ++q) {
                 const uint32_t j = 64u * q + lane;
@@ -1539,7 +1547,7 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
                     if (take_min ? (pk < key) : (pk > key)) { key = pk; val = pv; }
                 }
             }
-            if (lane < n) k5_emit(a, ob + lane, ds, key, val);
+            if (lane < n) k5_emit<BYDF>(a, ob + lane, ds, key, val);
             continue;
         }
         /* ---- bucket sort: ranks are distinct within a document, so an element's position
@@ -1606,7 +1614,7 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
                         pos[e] = gs + less;
                         cnt[e] = buf0[j];
                     }
-                    idf[e] = j < n ? k5_idf(a, rk) : 0.0;
+                    idf[e] = j < n ? k5_idf<BYDF>(a, rk) : 0.0;
                 }
 #pragma unroll
                 for (int e = 0; e < EB; ++e) {
@@ -1681,7 +1689,7 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
 #pragma unroll
             for (int q = 0; q < EB; ++q) {
                 const uint32_t j = j0 + 64 * q + lane;
-                idf[q] = k5_idf(a, (j < n ? buf1[j] : 0u) >> K5_IDX_BITS);
+                idf[q] = k5_idf<BYDF>(a, (j < n ? buf1[j] : 0u) >> K5_IDX_BITS);
             }
 #pragma unroll
             for (int q = 0; q < EB; ++q) {
@@ -1705,7 +1713,7 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
 /* Two instances share the list: MAXN = K5_MAX / 2 with 1024 buckets (38 KB of LDS: four
  * workgroups per CU) takes presorted documents and those of <= K5_MAX / 2 pairs; MAXN =
  * K5_MAX (72 KB: two per CU) the rest.  The bucket counters alias the radix scratch. */
-template <uint32_t MAXN, uint32_t NBB>
+template <uint32_t MAXN, uint32_t NBB, bool BYDF>
 __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
     constexpr uint32_t NB = 1u << NBB;
     __shared__ uint32_t kbuf[2][MAXN];
@@ -1763,7 +1771,7 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
             for (int e = 0; e < K5L_EB; ++e) {
                 const uint32_t j = j0 + NT * e + tid;
                 if (j < n) rk[e] = k5_rank(a, rk[e]);
-                f[e] = j < n ? k5_idf(a, rk[e]) : 0.0;
+                f[e] = j < n ? k5_idf<BYDF>(a, rk[e]) : 0.0;
             }
 #pragma unroll
             for (int e = 0; e < K5L_EB; ++e) {
@@ -1840,7 +1848,7 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
                         ps[e] = gs + less;
                         cn[e] = vbuf[0][vbuf[1][p]];
                     }
-                    f[e] = p < n ? k5_idf(a, kk[e]) : 0.0;
+                    f[e] = p < n ? k5_idf<BYDF>(a, kk[e]) : 0.0;
                 }
 #pragma unroll
                 for (int e = 0; e < K5L_EB; ++e) {
@@ -1900,7 +1908,7 @@ __global__ __launch_bounds__(NT) void k_score_large(K5Args a) {
         }
         cur ^= 1;
     }
-    for (uint32_t j = tid; j < n; j += NT) k5_emit(a, ob + j, ds, kbuf[cur][j], vbuf[cur][j]);
+    for (uint32_t j = tid; j < n; j += NT) k5_emit<BYDF>(a, ob + j, ds, kbuf[cur][j], vbuf[cur][j]);
     __syncthreads(); /* the next document reuses the LDS buffers */
     }
 }
@@ -1991,6 +1999,7 @@ __device__ __forceinline__ void k5s_batch(const K5Args& a, const uint32_t* L, ui
         ob = G(a.out_off)[i];
     }
 }
+template <bool BYDF>
 __global__ __launch_bounds__(256, K5S_OCC) void k_score_small(K5Args a) {
     __shared__ __attribute__((aligned(16))) uint32_t kb[K5S_WG][K5_SMALL_DOC + 4];
     __shared__ uint4 bm[K5S_WG][64];      /* the current batch's metadata (the next one: registers) */
@@ -2058,7 +2067,7 @@ __global__ __launch_bounds__(256, K5S_OCC) void k_score_small(K5Args a) {
         for (int q = 0; q < Q; ++q) {
             const bool v = 64u * q + lane < d.n;
             if (v) r[q] = k5_rank(a, r[q]);
-            f[q] = v ? k5_idf(a, r[q]) : 0.0;
+            f[q] = v ? k5_idf<BYDF>(a, r[q]) : 0.0;
         }
     };
     K5SDoc D0 = doc_at(0), D1 = doc_at(1);
@@ -2128,6 +2137,7 @@ __global__ __launch_bounds__(256, K5S_OCC) void k_score_small(K5Args a) {
     }
 }
 /* the chunk tasks of long presorted documents: one workgroup per 4096-pair chunk */
+template <bool BYDF>
 __global__ __launch_bounds__(256) void k_emit_split(K5Args a) {
     const uint32_t nt = *a.split_count < a.split_cap ? *a.split_count : a.split_cap;
     for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
@@ -2152,7 +2162,7 @@ __global__ __launch_bounds__(256) void k_emit_split(K5Args a) {
             for (int e = 0; e < K5L_EB; ++e) {
                 const uint32_t j = j0 + 256u * e + threadIdx.x;
                 if (j < j1) rk[e] = k5_rank(a, rk[e]);
-                f[e] = j < j1 ? k5_idf(a, rk[e]) : 0.0;
+                f[e] = j < j1 ? k5_idf<BYDF>(a, rk[e]) : 0.0;
             }
 #pragma unroll
             for (int e = 0; e < K5L_EB; ++e) {
@@ -2166,10 +2176,24 @@ __global__ __launch_bounds__(256) void k_emit_split(K5Args a) {
         }
     }
 }
+static void launch_score_wave(const K5Args& a, bool wide, uint32_t wg, hipStream_t s) {
+    if (!wide) k_score_wave<false, false><<<wg, NT, 0, s>>>(a);
+    else if (a.idf_by_df) k_score_wave<true, true><<<wg, NT, 0, s>>>(a);
+    else k_score_wave<true, false><<<wg, NT, 0, s>>>(a);
+}
+static void launch_emit_split(const K5Args& a, int ncu, hipStream_t s) {
+    if (a.idf_by_df) k_emit_split<true><<<(unsigned)ncu * 4u, 256, 0, s>>>(a);
+    else k_emit_split<false><<<(unsigned)ncu * 4u, 256, 0, s>>>(a);
+}
 static void launch_score_large(const K5Args& a, uint32_t grid, hipStream_t s) {
     static_assert(K5_MAX % 2 == 0 && K5_MAX / 2 >= 1024, "k_score_large instances");
-    k_score_large<(uint32_t)K5_MAX / 2, 10><<<grid, NT, 0, s>>>(a);
-    k_score_large<(uint32_t)K5_MAX, 11><<<grid, NT, 0, s>>>(a);
+    if (a.idf_by_df) {
+        k_score_large<(uint32_t)K5_MAX / 2, 10, true><<<grid, NT, 0, s>>>(a);
+        k_score_large<(uint32_t)K5_MAX, 11, true><<<grid, NT, 0, s>>>(a);
+    } else {
+        k_score_large<(uint32_t)K5_MAX / 2, 10, false><<<grid, NT, 0, s>>>(a);
+        k_score_large<(uint32_t)K5_MAX, 11, false><<<grid, NT, 0, s>>>(a);
+    }
 }
 int launch_score_order(const K5Args& a, Arena& ar, hipStream_t s, hipStream_t s2, hipEvent_t ev_fork,
                        hipEvent_t ev_join) {
@@ -2210,7 +2234,9 @@ int launch_score_order(const K5Args& a, Arena& ar, hipStream_t s, hipStream_t s2
     k_k5_classify<<<a.cls_nblk, 256, 0, s>>>(a);
     if (scan_excl_u32(a.cls_off, a.cls_off, 3ull * a.cls_nblk + 1, ar, s)) return -1;
     k_k5_scatter<<<a.cls_nblk, 256, 0, s>>>(a);
-    k_score_small<<<(unsigned)ncu * (unsigned)K5S_OCC, 256, 0, s>>>(a);
+    if (a.idf_by_df && !wide) return -1;   /* the engine sets idf_by_df only with wide ranks */
+    if (a.idf_by_df) k_score_small<true><<<(unsigned)ncu * (unsigned)K5S_OCC, 256, 0, s>>>(a);
+    else k_score_small<false><<<(unsigned)ncu * (unsigned)K5S_OCC, 256, 0, s>>>(a);
     /* k_score_large after the wave kernel on the same stream: beside it on the side stream
      * (-DK5_CONCURRENT_LARGE) measured c2 score 0.74 vs 0.76 ms but c4 3.18-3.29 vs
      * 3.04-3.11 and c5 0.83 vs 0.81 */
@@ -2219,20 +2245,18 @@ int launch_score_order(const K5Args& a, Arena& ar, hipStream_t s, hipStream_t s2
         /* the wave kernel first (its persistent grid takes the CUs), k_score_large on the
          * side stream fills them as the wave kernel's workgroups retire */
         if (hipEventRecord(ev_fork, s) != hipSuccess) return -1;
-        if (wide) k_score_wave<true><<<wg, NT, 0, s>>>(a);
-        else k_score_wave<false><<<wg, NT, 0, s>>>(a);
+        launch_score_wave(a, wide, wg, s);
         if (hipStreamWaitEvent(s2, ev_fork, 0) != hipSuccess) return -1;
         launch_score_large(a, grid, s2);
-        if (a.split_count) k_emit_split<<<(unsigned)ncu * 4u, 256, 0, s2>>>(a);
+        if (a.split_count) launch_emit_split(a, ncu, s2);
         if (hipEventRecord(ev_join, s2) != hipSuccess) return -1;
         if (hipStreamWaitEvent(s, ev_join, 0) != hipSuccess) return -1;
         if (wide) launch_score_large(hand, grid, s);
         return ok();
     }
 #endif
-    if (wide) k_score_wave<true><<<wg, NT, 0, s>>>(a);
-    else k_score_wave<false><<<wg, NT, 0, s>>>(a);
-    if (a.split_count) k_emit_split<<<(unsigned)ncu * 4u, 256, 0, s>>>(a);
+    launch_score_wave(a, wide, wg, s);
+    if (a.split_count) launch_emit_split(a, ncu, s);
     launch_score_large(a, grid, s);
     if (wide) launch_score_large(hand, grid, s);
     return ok();
