@@ -743,7 +743,7 @@ int launch_dense_emit(const uint32_t* dense, uint32_t nb, uint32_t V, const uint
 constexpr uint32_t DFH_RECS = 65535;      /* records per workgroup up to which no u16 bin can wrap */
 constexpr uint32_t DFH_MAXV = 65536;
 constexpr uint32_t DFH_ROUNDS = 4;        /* workgroups per resident slot at most: beyond 4 x 65535 records
-                                             per slot a workgroup takes more than DFH_RECS (the wide form) */
+                                             per slot one workgroup per slot (the wide form) */
 
 /* LDS-privatised DF histogram: 1024 threads (16 waves; at V = 65536 the 128 KB bin array allows one
  * workgroup per CU).  Each thread owns 64 records of the workgroup's range and keeps
@@ -764,7 +764,7 @@ constexpr uint32_t DFH_CK = 1u << DFH_CK_BITS;   /* LDS slot -> rank cache entri
                                                     bins + cache fill the 160 KB of LDS exactly) */
 __device__ __forceinline__ uint32_t dfh_cslot(uint32_t slot) { return (slot * 0x9E3779B1u) >> (32 - DFH_CK_BITS); }
 /* WIDE: a workgroup takes more than DFH_RECS records (large corpora: c3's 2.9e9 records in
- * 1024 workgroups instead of 44 K, so 100 MB of partial histograms are written and summed
+ * 256 workgroups instead of 44 K, so 25 MB of partial histograms are written and summed
  * instead of 4.4 GB).  A u16 counter then moves 0x8000 into the global df whenever it
  * reaches 0x8000: the one add that returned 0x7FFF does it, so every crossing is moved once
  * and no counter passes 0x8000 + the adds in flight (< 0xFFFF): no field wraps or carries. */
@@ -1034,8 +1034,8 @@ __global__ __launch_bounds__(DFS_NT) void k_dfs_slice(const uint32_t* __restrict
 
 /* the LDS histogram's split of nrec_max records: records per workgroup so that the
  * workgroups fill whole waves of the CUs' resident slots (c2: 946 x 65535 records = 3.7
- * waves -> 1024 x 60548, no tail), at most DFH_ROUNDS waves (c3: 1024 x 2.8 M records, the
- * wide form).  TFIDF_DF_WGS=<n> fixes the number of workgroups (tests of the wide form on
+ * waves -> 1024 x 60548, no tail), at most DFH_ROUNDS waves (c3: one per slot, 256 x 11 M
+ * records, the wide form).  TFIDF_DF_WGS=<n> fixes the number of workgroups (tests of the wide form on
  * small inputs). */
 static void df_lds_plan(uint64_t nrec_max, uint32_t V, uint64_t* per_out, uint32_t* nparts_out) {
     uint64_t nparts = (nrec_max + DFH_RECS - 1) / DFH_RECS;
@@ -1051,7 +1051,11 @@ static void df_lds_plan(uint64_t nrec_max, uint32_t V, uint64_t* per_out, uint32
     const uint64_t per_cu = (uint64_t)163840 / wg_lds >= 2 ? 2 : 1;   /* 1024-thread workgroups */
     const uint64_t slots = (uint64_t)ncu * per_cu;
     uint64_t full = (nparts + slots - 1) / slots * slots;
-    if (full > DFH_ROUNDS * slots) full = DFH_ROUNDS * slots;
+    /* beyond DFH_ROUNDS waves of 65535-record workgroups: one workgroup per slot (the wide
+     * form; c3 DF 11.2 -> 10.2 ms against four per slot, profiles/r06_k1_ab_c2.txt call
+     * r06r — the smaller splits keep several rounds, so that the merge stage's kernels beside
+     * the main pass find free CUs between them: c5 merge 0.70 vs 0.82 ms) */
+    if (full > DFH_ROUNDS * slots) full = slots;
     const char* fe = getenv("TFIDF_DF_WGS");
     const uint64_t forced = fe ? strtoull(fe, nullptr, 0) : 0ull;
     if (forced >= 1 && forced <= (1u << 20)) full = forced;
