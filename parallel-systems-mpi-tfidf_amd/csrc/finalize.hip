@@ -655,7 +655,6 @@ int launch_part_dense(const uint32_t* part_doc, const uint32_t* part_slot, const
                       const uint32_t* big_idx, const uint32_t* rank_of_slot, uint32_t V, uint32_t* dense,
                       uint64_t* keys, uint32_t* seq, uint32_t* cnt_out, uint32_t* nkeep, hipStream_t s) {
     if (!q) return 0;
-#ifndef PDL_OFF
     if (V <= 2u * PDL_SLICE) {
         const dim3 grid((uint32_t)((q + PDL_RECS - 1) / PDL_RECS), (V + PDL_SLICE - 1) / PDL_SLICE);
         const uint32_t lds = (V < PDL_SLICE ? V : PDL_SLICE) * 4u;
@@ -663,7 +662,6 @@ int launch_part_dense(const uint32_t* part_doc, const uint32_t* part_slot, const
                                                    keys, seq, cnt_out, nkeep);
         return ok();
     }
-#endif
     k_part_dense<<<grid_for(q), NT, 0, s>>>(part_doc, part_slot, part_cnt, q, big_idx, rank_of_slot, V, dense, keys,
                                            seq, cnt_out, nkeep);
     return ok();
@@ -1111,7 +1109,6 @@ int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra
         ar.release(m);
         return ok();
     }
-#ifndef DFS_OFF
     {
         const uint32_t nsl = (uint32_t)(((uint64_t)V + DFS_SLICE - 1) / DFS_SLICE);
         const uint64_t ntiles = (nrec_max + DFS_TILE - 1) / DFS_TILE;
@@ -1134,7 +1131,6 @@ int launch_df_hist(uint32_t* rec_slot, uint64_t nrec, const uint32_t* nrec_extra
             }
         }
     }
-#endif
     if (!accumulate && hipMemsetAsync(df, 0, (size_t)V * 4, s) != hipSuccess) return -1;
     k_df_hist_atomic<<<4096, NT, 0, s>>>(rec_slot, nrec, nrec_extra, rank_of_slot, slot_cap, ranked_from, V, status,
                                          df);
@@ -1276,11 +1272,7 @@ __device__ __forceinline__ uint32_t k5_rank(const K5Args& a, uint32_t r) {
 
 /* ranks up to 32 - K5_IDX_BITS bits pack (rank, index) keys; up to K5_WIDE_BITS the wave
  * kernel's bucket sort packs only the rank bits below the bucket (wide mode) */
-#ifndef K5_NO_WIDE
 constexpr uint32_t K5_WIDE_BITS = 32 - K5_IDX_BITS + K5_NB_BITS;
-#else
-constexpr uint32_t K5_WIDE_BITS = 32 - K5_IDX_BITS;
-#endif
 /* which kernel sorts a document of n pairs */
 __device__ __forceinline__ bool k5_by_wave(const K5Args& a, uint32_t n, bool presorted) {
     if (presorted) return n <= K5_WAVE;
@@ -1585,7 +1577,6 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
             if (lane == 0) G(a.large_list)[atomicAdd(a.large_count, 1u)] = i;
             continue;
         }
-#ifndef K5_NO_WIDE
         if constexpr (WIDE) if (wide) {
             /* wide ranks (V > 2^21): keys hold the rank bits below the bucket and the index;
              * each lane counts its own elements' smaller bucket mates and stores its pairs
@@ -1634,7 +1625,6 @@ __global__ __launch_bounds__(NT, WIDE ? K5_WPS_WIDE : K5_WPS) void k_score_wave(
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             continue;
         }
-#endif
         if (gmax > K5_GROUP_MAX) { /* skewed ranks: stable radix passes over buf0 */
 #pragma unroll
             for (int q = 0; q < K5_RQ; ++q) {
@@ -2241,24 +2231,9 @@ int launch_score_order(const K5Args& a, Arena& ar, hipStream_t s, hipStream_t s2
     if (a.idf_by_df && !wide) return -1;   /* the engine sets idf_by_df only with wide ranks */
     if (a.idf_by_df) k_score_small<true><<<(unsigned)ncu * (unsigned)K5S_OCC, 256, 0, s>>>(a);
     else k_score_small<false><<<(unsigned)ncu * (unsigned)K5S_OCC, 256, 0, s>>>(a);
-    /* k_score_large after the wave kernel on the same stream: beside it on the side stream
-     * (-DK5_CONCURRENT_LARGE) measured c2 score 0.74 vs 0.76 ms but c4 3.18-3.29 vs
-     * 3.04-3.11 and c5 0.83 vs 0.81 */
-#ifdef K5_CONCURRENT_LARGE
-    if (s2 && ev_fork && ev_join) {
-        /* the wave kernel first (its persistent grid takes the CUs), k_score_large on the
-         * side stream fills them as the wave kernel's workgroups retire */
-        if (hipEventRecord(ev_fork, s) != hipSuccess) return -1;
-        launch_score_wave(a, wide, wg, s);
-        if (hipStreamWaitEvent(s2, ev_fork, 0) != hipSuccess) return -1;
-        launch_score_large(a, grid, s2);
-        if (a.split_count) launch_emit_split(a, ncu, s2);
-        if (hipEventRecord(ev_join, s2) != hipSuccess) return -1;
-        if (hipStreamWaitEvent(s, ev_join, 0) != hipSuccess) return -1;
-        if (wide) launch_score_large(hand, grid, s);
-        return ok();
-    }
-#endif
+    /* k_score_large after the wave kernel on the same stream (beside it on the side stream,
+     * round 5's A/B: c2 score 0.74 vs 0.76 ms but c4 3.18-3.29 vs 3.04-3.11 and c5 0.83 vs
+     * 0.81) */
     launch_score_wave(a, wide, wg, s);
     if (a.split_count) launch_emit_split(a, ncu, s);
     launch_score_large(a, grid, s);
