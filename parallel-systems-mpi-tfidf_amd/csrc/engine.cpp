@@ -629,7 +629,7 @@ static int exchange_owner(tfidf_ctx* ctx, uint32_t V, const std::vector<uint64_t
      * rank's terms; a failure travels as the status word of the count row (below) */
     int arc = 0;
     auto ens = [&](DevBuf& b, size_t bytes) { if (!arc && b.ensure(bytes) != 0) arc = TFIDF_E_NOMEM; };
-    ens(ctx->x_mine, (size_t)V * 16 + 16);
+    if (!ctx->sorted_skey) ens(ctx->x_mine, (size_t)V * 16 + 16);
     ens(ctx->x_srec, (size_t)V * 20 + 20);
     ens(ctx->x_sidx, (size_t)V * 4 + 4);
     ens(ctx->x_back, ((size_t)V + R) * 4 + 4);
@@ -654,8 +654,18 @@ static int exchange_owner(tfidf_ctx* ctx, uint32_t V, const std::vector<uint64_t
     uint32_t* roff = soff + (R + 1);
     uint32_t* cur = roff + (R + 1);
     if (!arc) {
-        XCHK(launch_keys_by_rank(ctx->vkeys.as<uint4>(), ctx->slot_of_rank.as<uint32_t>(), V, ctx->x_mine.as<uint4>(), s));
-        XCHK(launch_owner_partition(ctx->x_mine.as<uint4>(), ctx->df_local.as<uint32_t>(), V, (uint32_t)R, row, cur,
+        /* the keys straight from the vocabulary sort (run_local): sorted by rank after the
+         * tile sort (and gathered so for the long-term fix-up after the radix sort), else
+         * gathered here from the radix sort's compact keys in dense order */
+        OwnerKeySrc ks;
+        ks.skey = ctx->sorted_skey;
+        if (!ks.skey) {
+            XCHK(launch_gather_u128(ctx->skey0.as<uint4>(), ctx->sorted_dense, V, ctx->x_mine.as<uint4>(), s));
+            ks.skey = ctx->x_mine.as<uint4>();
+        }
+        ks.slot_of_rank = ctx->slot_of_rank.as<uint32_t>();
+        ks.vkeys = ctx->vkeys.as<uint4>();
+        XCHK(launch_owner_partition(ks, ctx->df_local.as<uint32_t>(), V, (uint32_t)R, row, cur,
                                     ctx->x_srec.as<uint32_t>(), ctx->x_sidx.as<uint32_t>(), s));
     } else {
         HIPCHK(hipMemsetAsync(row, 0, (size_t)R * 4, s));

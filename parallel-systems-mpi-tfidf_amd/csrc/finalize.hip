@@ -2266,13 +2266,25 @@ __device__ __forceinline__ uint32_t owner_of(const uint4 k, uint32_t R) {
     return (uint32_t)(((h >> 32) * (uint64_t)R) >> 32);
 }
 constexpr uint32_t XO_MAXR = 1024;   /* ranks (tfidf_group_open's limit) */
+/* term rank i's identity key from the vocabulary sort's keys (OwnerKeySrc): round 5 gathered
+ * every key through the slot table (k_keys_by_rank: a random 16-byte read per term from a
+ * table of ~3x the terms' size, 0.33-0.43 ms per rank at c4 / 8 shards).  Byte 15 of
+ * a short identity key is 0x00 or 0x09 (dev_common.h); a long term's sort key holds its 16th
+ * byte there, which is neither NUL nor whitespace. */
+__device__ __forceinline__ uint4 owner_key(const OwnerKeySrc& ks, uint32_t i) {
+    const uint4 s = gload(ks.skey + i);
+    const uint32_t b15 = s.x & 0xFFu;
+    if (b15 == 0x00u || b15 == 0x09u)
+        return make_uint4(__builtin_bswap32(s.w), __builtin_bswap32(s.z), __builtin_bswap32(s.y), __builtin_bswap32(s.x));
+    return gload(ks.vkeys + G(ks.slot_of_rank)[i]);
+}
 /* per-owner counts of this rank's terms (LDS histogram, one device atomic per block and owner) */
-__global__ void k_owner_count(const uint4* __restrict__ keys, uint32_t V, uint32_t R, uint32_t* __restrict__ cnt) {
+__global__ void k_owner_count(const OwnerKeySrc ks, uint32_t V, uint32_t R, uint32_t* __restrict__ cnt) {
     __shared__ uint32_t h[XO_MAXR];
     for (uint32_t o = threadIdx.x; o < R; o += blockDim.x) h[o] = 0;
     __syncthreads();
     for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < V; r += gridDim.x * blockDim.x)
-        atomicAdd(&h[owner_of(keys[r], R)], 1u);
+        atomicAdd(&h[owner_of(owner_key(ks, r), R)], 1u);
     __syncthreads();
     for (uint32_t o = threadIdx.x; o < R; o += blockDim.x)
         if (h[o]) atomicAdd(&cnt[o], h[o]);
@@ -2280,7 +2292,7 @@ __global__ void k_owner_count(const uint4* __restrict__ keys, uint32_t V, uint32
 /* The send buffer grouped by owner as 20-byte records (the 16-byte key and the local df:
  * one all-to-all instead of two); order inside an owner's segment is free (the replies come
  * back in send order, sidx maps them to term ranks).  cur[o] starts at 0. */
-__global__ void k_owner_scatter(const uint4* __restrict__ keys, const uint32_t* __restrict__ df, uint32_t V, uint32_t R,
+__global__ void k_owner_scatter(const OwnerKeySrc ks, const uint32_t* __restrict__ df, uint32_t V, uint32_t R,
                                 const uint32_t* __restrict__ cnt, uint32_t* __restrict__ cur, uint32_t* __restrict__ srec,
                                 uint32_t* __restrict__ sidx) {
     __shared__ uint32_t h[XO_MAXR], base[XO_MAXR], seg[XO_MAXR];
@@ -2296,7 +2308,7 @@ __global__ void k_owner_scatter(const uint4* __restrict__ keys, const uint32_t* 
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const uint32_t r = r0 + q * blockDim.x + threadIdx.x;
-        own[q] = r < V ? owner_of(keys[r], R) : 0xFFFFFFFFu;
+        own[q] = r < V ? owner_of(owner_key(ks, r), R) : 0xFFFFFFFFu;
         pos[q] = own[q] != 0xFFFFFFFFu ? atomicAdd(&h[own[q]], 1u) : 0u;
     }
     __syncthreads();
@@ -2307,7 +2319,7 @@ __global__ void k_owner_scatter(const uint4* __restrict__ keys, const uint32_t* 
         const uint32_t r = r0 + q * blockDim.x + threadIdx.x;
         if (own[q] == 0xFFFFFFFFu) continue;
         const uint32_t p = base[own[q]] + pos[q];
-        const uint4 k = keys[r];
+        const uint4 k = owner_key(ks, r);
         uint32_t* d = srec + 5ull * p;
         d[0] = k.x; d[1] = k.y; d[2] = k.z; d[3] = k.w; d[4] = df[r];
         sidx[p] = r;
@@ -2422,8 +2434,24 @@ __global__ void k_owner_reply(const uint32_t* __restrict__ rslot, uint64_t n, co
 __global__ void k_owner_back(const uint32_t* __restrict__ back, const uint32_t* __restrict__ soff, uint32_t R,
                              const uint32_t* __restrict__ sidx, uint32_t V, uint32_t* __restrict__ df_global,
                              uint32_t* __restrict__ vg) {
+    /* the segment search over an LDS copy of soff (a search in memory is a chain of dependent
+     * loads per thread); segments are long, so most blocks lie in one and search nothing */
+    __shared__ uint32_t so[XO_MAXR + 1];
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < V) df_global[sidx[j]] = back[j + seg_of(soff, R, j)];
+    if (R <= XO_MAXR) {
+        for (uint32_t p = threadIdx.x; p <= R; p += blockDim.x) so[p] = soff[p];
+        __syncthreads();
+        if (j < V) {
+            uint32_t lo = 0, hi = R;
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (so[mid] <= j) lo = mid; else hi = mid;
+            }
+            df_global[sidx[j]] = back[j + lo];
+        }
+    } else if (j < V) {
+        df_global[sidx[j]] = back[j + seg_of(soff, R, j)];
+    }
     if (blockIdx.x == 0) {
         uint32_t t = 0;
         for (uint32_t p = threadIdx.x; p < R; p += blockDim.x) t += back[(uint64_t)soff[p + 1] + p];
@@ -2454,15 +2482,15 @@ __global__ void k_owner_offsets(const uint32_t* __restrict__ m, uint32_t R, uint
         roff[R] = b;
     }
 }
-int launch_owner_partition(const uint4* keys, const uint32_t* df, uint32_t V, uint32_t R, uint32_t* cnt, uint32_t* cur,
+int launch_owner_partition(const OwnerKeySrc& ks, const uint32_t* df, uint32_t V, uint32_t R, uint32_t* cnt, uint32_t* cur,
                            uint32_t* srec, uint32_t* sidx, hipStream_t s) {
     if (R < 1 || R > XO_MAXR) return -3;
     if (hipMemsetAsync(cnt, 0, (size_t)R * 4, s) != hipSuccess || hipMemsetAsync(cur, 0, (size_t)R * 4, s) != hipSuccess)
         return -1;
     if (!V) return 0;
     const uint32_t nb = (V + NT * 8 - 1) / (NT * 8);
-    k_owner_count<<<nb < 1024 ? nb : 1024, NT, 0, s>>>(keys, V, R, cnt);
-    k_owner_scatter<<<nb, NT, 0, s>>>(keys, df, V, R, cnt, cur, srec, sidx);
+    k_owner_count<<<nb < 1024 ? nb : 1024, NT, 0, s>>>(ks, V, R, cnt);
+    k_owner_scatter<<<nb, NT, 0, s>>>(ks, df, V, R, cnt, cur, srec, sidx);
     return ok();
 }
 int launch_owner_offsets(const uint32_t* m, uint32_t R, uint32_t me, uint32_t* soff, uint32_t* roff, hipStream_t s) {
@@ -2491,7 +2519,8 @@ int launch_owner_aggregate(const uint32_t* rrec, uint64_t n, const uint32_t* rof
  * the records: round 4's per-record returning atomic for the bucket rank and its scattered
  * 24-byte stores (c4 at 8 shards: 1.2 ms of the owner's 2.1 ms) are gone, and the bucket
  * workgroups read the records in place through the sorted indices. */
-constexpr uint32_t XB_MEAN = 512;    /* mean records per bucket (at most) */
+constexpr uint32_t XB_MEAN = 512;    /* mean records per bucket (at most; 256 measured no faster at c4 /
+                                        8 shards, profiles/r06_k1_ab_c2.txt call r06ad) */
 constexpr uint32_t XB_T = 2048;      /* LDS slots of the largest table (4x the mean; a bucket's table is
                                         the power of two >= 2x its records, cleared per bucket) */
 /* bucket = the top bits of a 64-bit mix (key_hash is 32-bit; its low bits pick the LDS slot),
@@ -2758,16 +2787,42 @@ int launch_sum_rows_u32(const uint32_t* rows, uint32_t nrows, uint64_t n, uint32
     k_sum_rows_u32<<<grid_for(n), NT, 0, s>>>(rows, nrows, n, out);
     return ok();
 }
-/* every word of every segment by one grid-stride pass (segment of a word: a search of off) */
-__global__ void k_xcopy(const XCopyList l) {
+/* every word of every segment, in tiles of XC_TILE words (grid-stride over tiles).  A tile
+ * inside one segment (nearly all: segments are long) finds it by one block-uniform search and
+ * moves its words with XC_PER independent coalesced loads per thread, then the stores; a
+ * tile across a boundary searches per word.  (Round 5 searched the kernel-argument offsets
+ * per word — a chain of dependent loads for every 4 bytes: 8 concurrent 98 MB copies at
+ * c4 / 8 shards took ~1 ms.) */
+constexpr uint32_t XC_PER = 4;
+constexpr uint32_t XC_TILE = NT * XC_PER;
+__global__ __launch_bounds__(NT) void k_xcopy(const XCopyList l) {
     const uint64_t total = l.off[l.n];
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
-        uint32_t lo = 0, hi = l.n;   /* last segment with off <= i */
+    for (uint64_t t0 = (uint64_t)blockIdx.x * XC_TILE; t0 < total; t0 += (uint64_t)gridDim.x * XC_TILE) {
+        uint32_t lo = 0, hi = l.n;   /* last segment with off <= t0 (uniform) */
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
-            if (l.off[mid] <= i) lo = mid; else hi = mid;
+            if (l.off[mid] <= t0) lo = mid; else hi = mid;
         }
-        l.dst[lo][i - l.off[lo]] = l.src[lo][i - l.off[lo]];
+        if (t0 + XC_TILE <= l.off[lo + 1]) {
+            const uint32_t* src = l.src[lo] + (t0 - l.off[lo]);
+            uint32_t* dst = l.dst[lo] + (t0 - l.off[lo]);
+            uint32_t v[XC_PER];
+#pragma unroll
+            for (uint32_t q = 0; q < XC_PER; ++q) v[q] = __builtin_nontemporal_load(src + q * NT + threadIdx.x);
+#pragma unroll
+            for (uint32_t q = 0; q < XC_PER; ++q) dst[q * NT + threadIdx.x] = v[q];   /* read next by the receiver */
+            continue;
+        }
+        for (uint32_t q = 0; q < XC_PER; ++q) {
+            const uint64_t i = t0 + q * NT + threadIdx.x;
+            if (i >= total) break;
+            uint32_t a = lo, b = l.n;
+            while (b - a > 1) {
+                const uint32_t mid = (a + b) >> 1;
+                if (l.off[mid] <= i) a = mid; else b = mid;
+            }
+            l.dst[a][i - l.off[a]] = l.src[a][i - l.off[a]];
+        }
     }
 }
 __global__ void k_xsum_slice(const XCopyList l, uint64_t lo, uint64_t len, uint32_t* __restrict__ out) {
@@ -2784,7 +2839,7 @@ static unsigned xgrid(uint64_t n) {
 int launch_xcopy(const XCopyList& l, hipStream_t s) {
     if (l.n < 1 || l.n > XCOPY_MAX) return -3;
     if (!l.off[l.n]) return 0;
-    k_xcopy<<<xgrid(l.off[l.n]), NT, 0, s>>>(l);
+    k_xcopy<<<xgrid((l.off[l.n] + XC_PER - 1) / XC_PER), NT, 0, s>>>(l);
     return ok();
 }
 int launch_xsum_slice(const XCopyList& l, uint64_t lo, uint64_t len, uint32_t* out, hipStream_t s) {

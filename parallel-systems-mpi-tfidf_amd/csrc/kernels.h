@@ -234,7 +234,16 @@ int launch_keys_by_rank(const uint4* vkeys, const uint32_t* slot_of_rank, uint32
  * received records on the owner (table of tcap = 2^k >= 1.5 n slots; *used = distinct keys)
  * and reply per sender (segment + one trailer word = *used); write the returned global df at
  * the term ranks and global V (the trailers summed) to *vg */
-int launch_owner_partition(const uint4* keys, const uint32_t* df, uint32_t V, uint32_t R, uint32_t* cnt, uint32_t* cur,
+/* where the partition reads this rank's term keys: the vocabulary sort's own keys in rank
+ * order (skey[r] = the strcmp sort key of term rank r), not a gather through the slot table.
+ * A short term's sort key is its identity key byte-swapped; a long term's identity key is
+ * read from vkeys at its slot */
+struct OwnerKeySrc {
+    const uint4* skey;
+    const uint32_t* slot_of_rank;   /* long terms */
+    const uint4* vkeys;
+};
+int launch_owner_partition(const OwnerKeySrc& ks, const uint32_t* df, uint32_t V, uint32_t R, uint32_t* cnt, uint32_t* cur,
                            uint32_t* srec, uint32_t* sidx, hipStream_t s);
 int launch_owner_offsets(const uint32_t* m, uint32_t R, uint32_t me, uint32_t* soff, uint32_t* roff, hipStream_t s);
 int launch_owner_aggregate(const uint32_t* rrec, uint64_t n, const uint32_t* roff, uint32_t R, uint4* tkey, uint64_t tcap,
