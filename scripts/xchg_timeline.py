@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """The DF exchange of the last step of a K-shard run from a rocprofv3 kernel-trace csv:
-every kernel from the first k_keys_by_rank (round 5) or k_owner_count of the last step to the last k_owner_back, with
+every kernel from the first k_keys_by_rank (round 5), k_ssb_keys or k_owner_count of the last step to the last k_owner_back, with
 its start (us from the first), duration and queue (one queue per rank's stream), then the
 summed duration per kernel name.
     python3 scripts/xchg_timeline.py <kernel_trace.csv>"""
@@ -12,7 +12,8 @@ import sys
 def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    first = "k_keys_by_rank" if any("k_keys_by_rank" in r["Kernel_Name"] for r in rows) else "k_owner_count"
+    first = next(f for f in ("k_keys_by_rank", "k_ssb_keys", "k_owner_count")
+                 if any(f in r["Kernel_Name"] for r in rows))
     kb = [i for i, r in enumerate(rows) if first in r["Kernel_Name"]]
     ob = [i for i, r in enumerate(rows) if "k_owner_back" in r["Kernel_Name"]]
     nr = 8
